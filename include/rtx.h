@@ -1,0 +1,246 @@
+/*
+ * rtx.h — C-ABI of the MI355X path-tracing megakernel (librtx.so).
+ *
+ * This is the drop-in boundary for the hot path of TwFlem/raytracer-go:
+ *
+ *   func (c *Camera) Render(world Hittable, writer io.Writer) error      internal/camera.go:180
+ *
+ * The reference runs the per-pixel / per-sample loop on the CPU
+ * (internal/camera.go:254-299 -> internal/ray.go:32-54 -> internal/bvh.go:220-249 ->
+ * internal/hittables.go:96-132 -> internal/materials.go:33-193).  A drop-in host
+ * (the Go package via cgo, or the C++ mirror in raytracer-go_amd/host/) walks its
+ * Hittable tree once, flattens it into the POD tables below, and calls
+ * rtx_scene_create() + rtx_render() instead of spawning one goroutine per pixel.
+ * PPM formatting (camera.go:183-188, 212-215) stays on the host.
+ *
+ * Rules of the ABI
+ *  - POD structs only, fixed-width types, little-endian; every array is 16-B aligned.
+ *  - The caller owns every input table and the output buffer for the duration of a
+ *    call.  The library copies what it needs into device memory and never retains a
+ *    caller pointer (cgo rule: C must not keep Go memory).
+ *  - Functions return 0 on success and a negative RTX_ERR_* code on failure; the
+ *    message is available from rtx_last_error() (thread-local).  No exception or
+ *    abort crosses the ABI.  This is what Render's `error` return maps to
+ *    (camera.go:180, 230).
+ *  - rtx_render* are blocking and not re-entrant for one rtx_scene (internal mutex).
+ */
+#ifndef RTX_H
+#define RTX_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RTX_ABI_VERSION 1
+
+/* ---- status codes ------------------------------------------------------------ */
+enum {
+    RTX_OK = 0,
+    RTX_ERR_INVALID_ARG = -1, /* null pointer, out-of-range index, bad size          */
+    RTX_ERR_HIP = -2,         /* a HIP runtime call failed                            */
+    RTX_ERR_RCCL = -3,        /* an RCCL call failed (multi-GPU gather)               */
+    RTX_ERR_UNSUPPORTED = -4, /* a feature outside the GPU path (e.g. Perlin noise)   */
+    RTX_ERR_NO_DEVICE = -5,   /* no gfx950 device visible                             */
+    RTX_ERR_OOM = -6          /* device allocation failed                             */
+};
+
+/* ---- scene tables ------------------------------------------------------------ */
+
+/* Child / root reference.  ref >= 0: index into rtx_scene_desc.nodes.
+ * ref < 0: a primitive, p = ~ref, type = p >> 28 (RTX_PRIM_*), index = p & 0x0FFFFFFF. */
+#define RTX_PRIM_SPHERE 0u
+#define RTX_PRIM_QUAD 1u
+#define RTX_REF_PRIM(type, index) ((int32_t) ~((int32_t)(((uint32_t)(type) << 28) | ((uint32_t)(index)&0x0FFFFFFFu))))
+
+/* A BVH interior node exactly as internal/bvh.go:132-185 builds it: an AABB
+ * (bvh.go:36-50, from NewAabbFromBoxes) and two children.  A one-element split
+ * produces left == right (bvh.go:162-165); that is kept as-is in the table.   32 B */
+typedef struct rtx_bvh_node {
+    float bmin[3];
+    int32_t left;
+    float bmax[3];
+    int32_t right;
+} rtx_bvh_node;
+
+/* internal/hittables.go:78-94 (NewSphere).                                       32 B */
+typedef struct rtx_sphere {
+    float center[3];
+    float radius;
+    uint32_t material;
+    uint32_t pad[3];
+} rtx_sphere;
+
+/* internal/hittables.go:138-165 (NewQuad) — derived fields as the constructor
+ * computes them.  Reserved for the Quad/Box row.                  64 B */
+typedef struct rtx_quad {
+    float q[3];
+    uint32_t material;
+    float u[3];
+    float d;
+    float v[3];
+    float pad0;
+    float w[3];
+    float pad1;
+    float normal[3];
+    float pad2;
+} rtx_quad;
+
+/* Materials, internal/materials.go:9-119, 297-313.                               */
+enum {
+    RTX_MAT_LAMBERTIAN = 0,    /* albedo = textures[texture]       materials.go:23-42   */
+    RTX_MAT_METAL = 1,         /* albedo[3], fuzz                  materials.go:44-75   */
+    RTX_MAT_DIELECTRIC = 2,    /* ior                              materials.go:77-119  */
+    RTX_MAT_DIFFUSE_LIGHT = 3  /* emit = textures[texture]         materials.go:297-313 */
+};
+typedef struct rtx_material { /* 32 B */
+    uint32_t type;
+    uint32_t texture;
+    float fuzz;
+    float ior;
+    float albedo[3];
+    float pad;
+} rtx_material;
+
+/* Textures, internal/materials.go:121-193, 280-295.                              */
+enum {
+    RTX_TEX_SOLID = 0,     /* even[3] = colour                       materials.go:151-163 */
+    RTX_TEX_CHECKERED = 1, /* scale, even[3], odd[3]                 materials.go:121-145 */
+    RTX_TEX_IMAGE = 2,     /* width x height RGBA8 texels at texel_offset (row-major,
+                              y down, as image.RGBA.At)             materials.go:165-193 */
+    RTX_TEX_NOISE = 3      /* Perlin; not on the GPU path (RTX_ERR_UNSUPPORTED)         */
+};
+typedef struct rtx_texture { /* 48 B */
+    uint32_t type;
+    float scale;
+    uint32_t width;
+    uint32_t height;
+    float even[3];
+    uint32_t texel_offset;
+    float odd[3];
+    float pad;
+} rtx_texture;
+
+typedef struct rtx_scene_desc {
+    const rtx_bvh_node* nodes;
+    uint32_t n_nodes;
+    uint32_t n_roots;
+    /* The world handed to Render: a BVH gives one root ref (the tree); a plain World
+     * (hittables.go:39-76, linear closest-hit scan in insertion order) gives its items. */
+    const int32_t* roots;
+    const rtx_sphere* spheres;
+    uint32_t n_spheres;
+    uint32_t n_quads;
+    const rtx_quad* quads;
+    const rtx_material* materials;
+    uint32_t n_materials;
+    uint32_t n_textures;
+    const rtx_texture* textures;
+    const uint32_t* texels; /* RGBA8, r in the low byte */
+    uint64_t n_texels;
+} rtx_scene_desc;
+
+/* ---- camera ------------------------------------------------------------------ */
+/* The derived state of Camera.init (internal/camera.go:128-165), computed by the
+ * host exactly as the reference does and uploaded as kernel constants.           */
+typedef struct rtx_camera {
+    uint32_t image_width;       /* int(c.imageWidth)                     camera.go:181 */
+    uint32_t image_height;      /* int(c.imageHeight)                    camera.go:182 */
+    uint32_t samples_per_pixel; /* c.samplesPerPixel                     camera.go:256 */
+    uint32_t max_depth;         /* c.bounceDepth                         camera.go:258 */
+    float center[3];
+    float defocus_angle; /* radians; > 0 enables the thin lens          camera.go:279 */
+    float pixel00[3];
+    float pad0;
+    float pixel_du[3];
+    float pad1;
+    float pixel_dv[3];
+    float pad2;
+    float defocus_disk_u[3];
+    float pad3;
+    float defocus_disk_v[3];
+    float pad4;
+    float background[3];
+    float pad5;
+} rtx_camera;
+
+/* ---- render region / shard ---------------------------------------------------- */
+/* Pixels x in [x0, x0+width), rows y = y0 + r for r in [0, height) with
+ * r % world == rank (row-interleaved shard, so sky and ground are balanced across
+ * GPUs).  Output rows are stored compacted in shard order: out[(r/world)*width + x].
+ * The RNG is keyed by the GLOBAL pixel index y*image_width + x, so every pixel's
+ * value is independent of the region and of the shard count.                     */
+typedef struct rtx_region {
+    uint32_t x0, y0, width, height;
+    uint32_t rank, world;
+} rtx_region;
+
+/* Work counters of one render (filled when RTX_FLAG_COUNTERS is set).  These are
+ * the units of SURVEY.md §8(d): segments = world.Hit calls (ray.go:36).          */
+typedef struct rtx_stats {
+    uint64_t samples;
+    uint64_t segments;
+    uint64_t node_visits;  /* AABB slab tests   (bvh.go:221)                        */
+    uint64_t prim_tests;   /* ray-primitive tests (hittables.go:96), duplicates of
+                              a one-element split skipped (bit-identical, §8a a5)   */
+    uint64_t hits;         /* segments that hit a primitive                          */
+    uint64_t texel_fetches;
+    uint64_t rng_draws;
+    double kernel_ms;      /* device time of the render kernel(s), HIP events       */
+    double gather_ms;      /* multi-GPU gather (rtx_render with n_gpus > 1)         */
+} rtx_stats;
+
+#define RTX_FLAG_COUNTERS 1u /* count work units (separate kernel instantiation) */
+
+typedef struct rtx_scene rtx_scene;
+
+/* ---- entry points ------------------------------------------------------------- */
+
+/* ABI version (RTX_ABI_VERSION) and a static build string. */
+int rtx_version(void);
+const char* rtx_build_info(void);
+
+/* Last error message of this thread ("" if none). */
+const char* rtx_last_error(void);
+
+/* Number of visible GPUs (0 if none). */
+int rtx_device_count(void);
+
+/* Validate the tables, convert them to the device layout and upload them once to
+ * the current HIP device (replicated to further devices lazily by rtx_render).
+ * Replaces the tree walk the reference does on every ray (bvh.go:220).           */
+int rtx_scene_create(const rtx_scene_desc* desc, rtx_scene** out);
+
+/* Release device memory owned by the scene (NULL is a no-op). */
+void rtx_scene_destroy(rtx_scene* scene);
+
+/* Size of the device layout in bytes (entries + materials + textures + texels). */
+uint64_t rtx_scene_device_bytes(const rtx_scene* scene);
+
+/* The whole of Camera.Render's pixel loop (camera.go:198-222): render every pixel
+ * of the image, averaged over samples_per_pixel, linear (pre-gamma) float32 RGB,
+ * row-major, rows top to bottom, into caller-owned host memory out_rgb[W*H*3].
+ * n_gpus > 1 row-interleaves the image over devices 0..n_gpus-1 of this process
+ * and gathers the bands to device 0 with RCCL before the copy to the host.       */
+int rtx_render(rtx_scene* scene, const rtx_camera* cam, uint64_t seed, int n_gpus, float* out_rgb,
+               rtx_stats* stats);
+
+/* Render one region/shard on the CURRENT device into device memory d_out (float32
+ * RGB, compacted shard rows, see rtx_region) on the given HIP stream (hipStream_t,
+ * NULL = default stream).  Returns after enqueueing unless stats != NULL, in which
+ * case it synchronises the stream and fills stats (kernel_ms from HIP events
+ * recorded on that same stream).  This is the entry a one-process-per-GPU launcher
+ * (torch.distributed / RCCL) uses.                                               */
+int rtx_render_region_device(rtx_scene* scene, const rtx_camera* cam, uint64_t seed, const rtx_region* region,
+                             float* d_out, void* hip_stream, uint32_t flags, rtx_stats* stats);
+
+/* Number of output rows of a region shard: ceil((height - rank) / world). */
+uint32_t rtx_region_rows(const rtx_region* region);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RTX_H */

@@ -1,0 +1,49 @@
+/*
+ * rtx_host.h — C entry points of librtxhost.so, the C++ mirror of the reference's Go
+ * `internal` package (raytracer-go_amd/host/).  These let test drivers and bench.py
+ * (Python, via ctypes) build the reference's scenes exactly as main.go does and run
+ * the full Camera.Render drop-in path; a Go host would not need them (it builds its
+ * scenes in Go and calls rtx.h directly).
+ */
+#ifndef RTX_HOST_H
+#define RTX_HOST_H
+
+#include <stdint.h>
+
+#include "rtx.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct rtxhost_scene rtxhost_scene;
+
+/* Build a scene of main.go by name: "random_spheres" (main.go:227-289),
+ * "stress_100k" (config 4), "earth_dielectric" (config 5), "earth" (main.go:80-104).
+ * The BVH is built by the NewBVH restatement (bvh.go:142-185) and flattened. */
+int rtxhost_build_scene(const char* name, uint64_t seed, rtxhost_scene** out);
+void rtxhost_scene_free(rtxhost_scene* s);
+
+/* The flattened tables (valid until rtxhost_scene_free). */
+const rtx_scene_desc* rtxhost_scene_desc(const rtxhost_scene* s);
+
+/* The scene's camera (NewCamera with main.go's options), with overrides; a value
+ * <= 0 keeps the scene's own setting. */
+int rtxhost_scene_camera(const rtxhost_scene* s, int32_t image_width, int32_t samples_per_pixel, int32_t max_depth,
+                         rtx_camera* out);
+
+/* The whole drop-in path: NewCamera(...).Render(world, file) -> PPM at `path`. */
+int rtxhost_render_ppm(const char* scene_name, uint64_t scene_seed, int32_t image_width, int32_t samples_per_pixel,
+                       int32_t max_depth, uint64_t render_seed, int32_t n_gpus, const char* path);
+
+/* PPM body lines for a linear float RGB image (ToGamma2, ToRGB, String per pixel);
+ * returns the byte count, writing at most cap bytes (call with cap = 0 to size). */
+uint64_t rtxhost_ppm_encode(const float* rgb, uint32_t width, uint32_t height, char* out, uint64_t cap);
+
+/* Last error of this thread from an rtxhost_* call. */
+const char* rtxhost_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

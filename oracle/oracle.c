@@ -1,0 +1,975 @@
+/*
+ * oracle.c — CPU restatement of TwFlem/raytracer-go's per-pixel hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY (see oracle.h): the checker for the HIP megakernel and the
+ * CPU baseline of bench.py.  Never linked into librtx.so / librtxhost.so.
+ * PARITY UNPINNED against the reference binary (Go is absent; the reference has no
+ * tests or fixtures) — pinned instead by Random123 KATs for the RNG and by
+ * source-derived known-answer tests.
+ *
+ * Build: gcc -O2 -std=c11 -ffp-contract=off -fno-fast-math (SSE2 scalar float32, the
+ * same IEEE single-precision semantics as Go's gc compiler on amd64 at GOAMD64=v1).
+ */
+#include "oracle.h"
+
+#include <math.h>
+#include <pthread.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* ============================================================================
+ * Vec3 — internal/vec3.go:9-139.  Every operation is written in the association
+ * order of the Go source (left to right), float32, no fused multiply-add.
+ * ========================================================================== */
+typedef struct { float x, y, z; } vec3;
+
+static inline vec3 v3(float x, float y, float z) { vec3 r = {x, y, z}; return r; }
+static inline vec3 v_add(vec3 a, vec3 b) { return v3(a.x + b.x, a.y + b.y, a.z + b.z); }   /* vec3.go:43-53 */
+static inline vec3 v_sub(vec3 a, vec3 b) { return v3(a.x - b.x, a.y - b.y, a.z - b.z); }   /* vec3.go:67-77 */
+static inline vec3 v_mul(vec3 a, vec3 b) { return v3(a.x * b.x, a.y * b.y, a.z * b.z); }   /* vec3.go:55-65 */
+static inline vec3 v_scale(vec3 a, float s) { return v3(a.x * s, a.y * s, a.z * s); }      /* vec3.go:91-101 */
+static inline float v_lensq(vec3 v) { return v.x * v.x + v.y * v.y + v.z * v.z; }           /* vec3.go:115-117 */
+static inline float v_dot(vec3 l, vec3 r) { return l.x * r.x + l.y * r.y + l.z * r.z; }     /* vec3.go:137-139 */
+static inline vec3 v_cross(vec3 l, vec3 r) {                                                 /* vec3.go:129-135 */
+    return v3(l.y * r.z - l.z * r.y, l.z * r.x - l.x * r.z, l.x * r.y - l.y * r.x);
+}
+/* vec3.go:103-113: l = float32(math.Sqrt(float64(lensq))); v.Scale(1 / l).
+ * sqrt in float64 of a float32, rounded back, equals the correctly rounded sqrtf. */
+static inline vec3 v_unit(vec3 v) {
+    float lensq = v_lensq(v);
+    float l = (float)sqrt((double)lensq);
+    return v_scale(v, 1.0f / l);
+}
+/* vec3.go:170-172 */
+static inline int v_near_zero(vec3 v) {
+    const float eps = 1e-8f;
+    return (float)fabs((double)v.x) < eps && (float)fabs((double)v.y) < eps && (float)fabs((double)v.z) < eps;
+}
+/* vec3.go:212-214 */
+static inline vec3 v_reflect(vec3 v, vec3 n) { return v_sub(v, v_scale(n, 2.0f * v_dot(v, n))); }
+/* vec3.go:216-221 */
+static inline vec3 v_refract(vec3 uv, vec3 n, float eta) {
+    float cos_theta = v_dot(v_scale(uv, -1.0f), n);
+    vec3 perp = v_scale(v_add(uv, v_scale(n, cos_theta)), eta);
+    vec3 par = v_scale(n, -1.0f * (float)sqrt(fabs((double)(1.0f - v_lensq(perp)))));
+    return v_add(par, perp);
+}
+
+/* Go math.Min / math.Max semantics (NaN wins, -0 < +0): math.go:38-44 via MinF32/MaxF32. */
+static inline double go_min(double a, double b) {
+    if (isnan(a) || isnan(b)) return NAN;
+    if (a == 0 && b == 0) return signbit(a) ? a : b;
+    return a < b ? a : b;
+}
+static inline double go_max(double a, double b) {
+    if (isnan(a) || isnan(b)) return NAN;
+    if (a == 0 && b == 0) return signbit(a) ? b : a;
+    return a > b ? a : b;
+}
+static inline float min_f32(float a, float b) { return (float)go_min((double)a, (double)b); } /* math.go:38 */
+static inline float max_f32(float a, float b) { return (float)go_max((double)a, (double)b); } /* math.go:42 */
+
+/* Go math.Pow(x, 5) for x >= 0 (Go 1.21 src/math/pow.go): y is integral, so Pow
+ * multiplies frexp-normalised mantissas by repeated squaring over the bits of 5 and
+ * applies Ldexp; scaling by powers of two is exact here, so the result is
+ * x * ((x*x) * (x*x)) in float64, with x == 0 -> 0 and x == 1 -> 1 as special cases. */
+static double go_pow5(double x) {
+    if (x == 1.0) return 1.0;
+    if (isnan(x)) return NAN;
+    if (x == 0.0) return 0.0;
+    int xe;
+    double x1 = frexp(x, &xe);
+    double a1 = 1.0;
+    int ae = 0;
+    for (long i = 5; i != 0; i >>= 1) {
+        if (i & 1) {
+            a1 *= x1;
+            ae += xe;
+        }
+        x1 *= x1;
+        xe <<= 1;
+        if (x1 < 0.5) {
+            x1 += x1;
+            xe--;
+        }
+    }
+    return ldexp(a1, ae);
+}
+
+/* ============================================================================
+ * RNG contract: Philox4x32-10, key = seed, counter =
+ * (global pixel index, sample index, draw block, stream); draw n is word n&3 of
+ * block n>>2; u = float32(x >> 8) * 2^-24 in [0, 1) — the range of rand.Float32.
+ * ========================================================================== */
+void oracle_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) {
+    uint32_t c0 = ctr[0], c1 = ctr[1], c2 = ctr[2], c3 = ctr[3];
+    uint32_t k0 = key[0], k1 = key[1];
+    for (int r = 0; r < 10; ++r) {
+        if (r > 0) {
+            k0 += 0x9E3779B9u;
+            k1 += 0xBB67AE85u;
+        }
+        uint64_t p0 = (uint64_t)0xD2511F53u * c0;
+        uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
+        uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
+        uint32_t n1 = (uint32_t)p1;
+        uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+        uint32_t n3 = (uint32_t)p0;
+        c0 = n0; c1 = n1; c2 = n2; c3 = n3;
+    }
+    out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+}
+
+static inline float u32_to_unit(uint32_t x) { return (float)(x >> 8) * 0x1.0p-24f; }
+
+typedef struct {
+    uint32_t key[2];
+    uint32_t pixel, sample, n;
+    uint32_t buf[4];
+    uint64_t* draws;
+} rng_t;
+
+static inline float rng_float32(rng_t* r) {
+    if ((r->n & 3u) == 0) {
+        uint32_t ctr[4] = {r->pixel, r->sample, r->n >> 2, 0u};
+        oracle_philox4x32_10(ctr, r->key, r->buf);
+    }
+    uint32_t w = r->buf[r->n & 3u];
+    r->n++;
+    if (r->draws) (*r->draws)++;
+    return u32_to_unit(w);
+}
+
+float oracle_pixel_draw(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t n) {
+    uint32_t ctr[4] = {pixel, sample, n >> 2, 0u};
+    uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
+    uint32_t out[4];
+    oracle_philox4x32_10(ctr, key, out);
+    return u32_to_unit(out[n & 3u]);
+}
+
+uint32_t oracle_stream_u32(uint64_t seed, uint32_t stream, uint64_t n) {
+    uint64_t blk = n >> 2;
+    uint32_t ctr[4] = {(uint32_t)blk, (uint32_t)(blk >> 32), 0u, stream};
+    uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
+    uint32_t out[4];
+    oracle_philox4x32_10(ctr, key, out);
+    return out[n & 3u];
+}
+
+/* RandF32N, math.go:30-32: min + Float32()*(max-min). */
+static inline float rand_f32n(rng_t* r, float mn, float mx) { return mn + rng_float32(r) * (mx - mn); }
+
+/* NewVec3UnitRandOnUnitSphere32, vec3.go:182-190 (arguments drawn x, y, z). */
+static vec3 rand_unit_on_sphere(rng_t* r) {
+    for (;;) {
+        float x = rand_f32n(r, -1.0f, 1.0f);
+        float y = rand_f32n(r, -1.0f, 1.0f);
+        float z = rand_f32n(r, -1.0f, 1.0f);
+        vec3 v = v3(x, y, z);
+        if (v_lensq(v) < 1.0f) return v_unit(v);
+    }
+}
+
+/* NewVec3RandInUnitDisk, vec3.go:203-210. */
+static vec3 rand_in_unit_disk(rng_t* r) {
+    for (;;) {
+        float x = rand_f32n(r, -1.0f, 1.0f);
+        float y = rand_f32n(r, -1.0f, 1.0f);
+        vec3 v = v3(x, y, 0.0f);
+        if (v_lensq(v) < 1.0f) return v;
+    }
+}
+
+/* ============================================================================
+ * Camera — internal/camera.go:104-178, math.go:48-52.
+ * ========================================================================== */
+static const float PI_F32 = 3.14159274101257324f;         /* float32(math.Pi)   math.go:48 */
+static const float RAD_RATIO = (float)(3.14159265358979323846 / 180.0); /* float32(pi/180), math.go:46;
+                                                             single- and double-rounding agree */
+
+float oracle_to_radians(float degrees) { return degrees * RAD_RATIO; }
+
+void oracle_camera_defaults(oracle_camera_opts* o) {
+    memset(o, 0, sizeof(*o));
+    o->samples_per_pixel = 100;                  /* camera.go:109 */
+    o->max_depth = 50;                           /* camera.go:110 */
+    o->fov_radians = (float)1.57079632679489662; /* float32(PiO2), camera.go:108 */
+    o->focus_dist = 10.0f;                       /* camera.go:111 */
+    o->defocus_radians = 0.0f;
+    o->look_at[0] = o->look_at[1] = o->look_at[2] = 0.0f;
+    o->look_from[0] = 0.0f; o->look_from[1] = 0.0f; o->look_from[2] = -1.0f;
+    o->vup[0] = 0.0f; o->vup[1] = 1.0f; o->vup[2] = 0.0f;
+    o->background[0] = o->background[1] = o->background[2] = 0.0f;
+}
+
+void oracle_camera_init(float aspect_ratio, int32_t image_width, const oracle_camera_opts* o, rtx_camera* out) {
+    memset(out, 0, sizeof(*out));
+    float image_w = (float)image_width;
+    vec3 look_from = v3(o->look_from[0], o->look_from[1], o->look_from[2]);
+    vec3 look_at = v3(o->look_at[0], o->look_at[1], o->look_at[2]);
+    vec3 vup = v3(o->vup[0], o->vup[1], o->vup[2]);
+    vec3 center = look_from;                                                   /* :130 */
+    vec3 dist = v_sub(look_from, look_at);                                     /* :132 */
+    float h = (float)tan((double)(o->fov_radians / 2.0f));                    /* :134 */
+    float viewport_h = 2.0f * h * o->focus_dist;                               /* :135 */
+    float image_h = (float)(floor((double)image_w) / (double)aspect_ratio);    /* :137 */
+    if (image_h < 1.0f) image_h = 1.0f;                                        /* :138 */
+    float viewport_w = viewport_h * (image_w / image_h);                       /* :141 */
+    vec3 w = v_unit(dist);                                                     /* :143 */
+    vec3 u = v_unit(v_cross(vup, w));                                          /* :144 */
+    vec3 v = v_cross(w, u);                                                    /* :145 */
+    vec3 viewport_u = v_scale(u, viewport_w);                                  /* :147 */
+    vec3 viewport_v = v_scale(v, -viewport_h);                                 /* :148 */
+    vec3 pixel_du = v_scale(viewport_u, 1.0f / image_w);                       /* :150-151 */
+    vec3 pixel_dv = v_scale(viewport_v, 1.0f / image_h);                       /* :152-153 */
+    vec3 ul = center;                                                          /* :155 */
+    ul = v_sub(ul, v_scale(w, o->focus_dist));                                 /* :156 */
+    ul = v_sub(ul, v_scale(viewport_u, 0.5f));                                 /* :157 */
+    ul = v_sub(ul, v_scale(viewport_v, 0.5f));                                 /* :158 */
+    vec3 pixel00 = v_add(ul, v_scale(v_add(pixel_du, pixel_dv), 0.5f));        /* :160-161 */
+    float defocus_r = o->focus_dist * (float)tan((double)(o->defocus_radians / 2.0f)); /* :163 */
+    vec3 disk_u = v_scale(u, defocus_r);                                       /* :164 */
+    vec3 disk_v = v_scale(v, defocus_r);                                       /* :165 */
+
+    out->image_width = (uint32_t)(int32_t)image_w;   /* int(c.imageWidth)  camera.go:181 */
+    out->image_height = (uint32_t)(int32_t)image_h;  /* int(c.imageHeight) camera.go:182 */
+    out->samples_per_pixel = (uint32_t)o->samples_per_pixel;
+    out->max_depth = (uint32_t)o->max_depth;
+    out->defocus_angle = o->defocus_radians;
+#define PUT(dst, src) do { (dst)[0] = (src).x; (dst)[1] = (src).y; (dst)[2] = (src).z; } while (0)
+    PUT(out->center, center);
+    PUT(out->pixel00, pixel00);
+    PUT(out->pixel_du, pixel_du);
+    PUT(out->pixel_dv, pixel_dv);
+    PUT(out->defocus_disk_u, disk_u);
+    PUT(out->defocus_disk_v, disk_v);
+#undef PUT
+    out->background[0] = o->background[0];
+    out->background[1] = o->background[1];
+    out->background[2] = o->background[2];
+}
+
+/* ============================================================================
+ * Ray / HitInfo / scene traversal — ray.go:9-54, hittables.go:7-136, bvh.go:9-253.
+ * ========================================================================== */
+typedef struct { vec3 origin, dir; } ray_t;
+
+static inline vec3 ray_at(const ray_t* r, float t) { return v_add(v_scale(r->dir, t), r->origin); } /* ray.go:25-30 */
+
+typedef struct {
+    vec3 point, normal;
+    float t, u, v;
+    uint32_t material;
+    int front;
+} hit_t;
+
+typedef struct {
+    const rtx_scene_desc* s;
+    const rtx_camera* cam;
+    uint64_t seed;
+    int order;
+    oracle_counters* c; /* per-thread */
+} ctx_t;
+
+/* NewHitInfo, hittables.go:22-37. */
+static hit_t new_hit_info(float t, float u, float v, vec3 dir, vec3 point, vec3 n, uint32_t mat) {
+    hit_t h;
+    h.front = v_dot(dir, n) < 0.0f;
+    if (!h.front) n = v_scale(n, -1.0f);
+    h.point = point;
+    h.normal = n;
+    h.t = t;
+    h.u = u;
+    h.v = v;
+    h.material = mat;
+    return h;
+}
+
+/* Interval.In, bvh.go:18-20 (padding 0). */
+static inline int interval_in(float mn, float mx, float v) { return mn - 0.0f < v && v < mx + 0.0f; }
+
+/* (*Sphere).Hit, hittables.go:96-132. */
+static int sphere_hit(const ctx_t* cx, const rtx_sphere* s, const ray_t* r, float tmin, float tmax, hit_t* out) {
+    vec3 c = v3(s->center[0], s->center[1], s->center[2]);
+    vec3 a_sub_c = v_sub(r->origin, c);                                    /* :97 */
+    float a = v_lensq(r->dir);                                             /* :98 */
+    float half_b = v_dot(r->dir, a_sub_c);                                 /* :99 */
+    float cc = v_lensq(a_sub_c) - s->radius * s->radius;                   /* :100 */
+    float disc = half_b * half_b - a * cc;                                 /* :102 */
+    if (disc < 0.0f) return 0;                                             /* :104 */
+    float sqt = (float)sqrt((double)disc);                                 /* :108 */
+    float t;
+    float r1 = (-half_b - sqt) / a;                                        /* :110 */
+    if (interval_in(tmin, tmax, r1)) {
+        t = r1;
+    } else {
+        float r2 = (-half_b + sqt) / a;                                    /* :112 */
+        if (interval_in(tmin, tmax, r2)) t = r2;
+        else return 0;
+    }
+    vec3 point = ray_at(r, t);                                             /* :118 */
+    vec3 norm = v_unit(v_scale(v_sub(point, c), s->radius));               /* :119-120 */
+    float theta = (float)acos(-(double)norm.y);                            /* :122 */
+    float phi = (float)(atan2(-(double)norm.z, (double)norm.x) + 3.14159265358979323846); /* :123 */
+    float u = (phi + 5.0f * PI_F32 / 12.0f) / (2.0f * PI_F32);             /* :125 typed consts fold in float32 */
+    float v = theta / PI_F32;                                              /* :126 */
+    (void)cx;
+    *out = new_hit_info(t, u, v, r->dir, point, norm, s->material);        /* :128 */
+    return 1;
+}
+
+/* InBoundary, bvh.go:84-102. */
+static inline int in_boundary(float dir, float origin, float amin, float amax, float* rmin, float* rmax) {
+    float inv_d = 1.0f / dir;
+    float t0 = (amin - origin) * inv_d;
+    float t1 = (amax - origin) * inv_d;
+    if (inv_d < 0.0f) {
+        float t = t0; t0 = t1; t1 = t;
+    }
+    if (t0 > *rmin) *rmin = t0;
+    if (t1 < *rmax) *rmax = t1;
+    return *rmin < *rmax;
+}
+
+/* (*Aabb).Hit, bvh.go:52-61: rT is passed by value. */
+static int aabb_hit(const rtx_bvh_node* n, const ray_t* r, float tmin, float tmax) {
+    if (in_boundary(r->dir.x, r->origin.x, n->bmin[0], n->bmax[0], &tmin, &tmax))
+        if (in_boundary(r->dir.y, r->origin.y, n->bmin[1], n->bmax[1], &tmin, &tmax))
+            if (in_boundary(r->dir.z, r->origin.z, n->bmin[2], n->bmax[2], &tmin, &tmax)) return 1;
+    return 0;
+}
+
+static int hit_ref(const ctx_t* cx, int32_t ref, const ray_t* r, float tmin, float tmax, hit_t* out, int dup);
+
+/* (*BVH).Hit, bvh.go:220-249. */
+static int bvh_hit(const ctx_t* cx, const rtx_bvh_node* n, const ray_t* r, float tmin, float tmax, hit_t* out) {
+    cx->c->node_visits++;
+    if (!aabb_hit(n, r, tmin, tmax)) return 0;                              /* :221 */
+    hit_t hl, hr;
+    int hit_left = hit_ref(cx, n->left, r, tmin, tmax, &hl, 0);             /* :225 */
+    float rmax = tmax;                                                      /* :227 */
+    if (hit_left) rmax = hl.t;                                              /* :228-230 */
+    int hit_right = hit_ref(cx, n->right, r, tmin, rmax, &hr, n->right == n->left); /* :232 */
+    if (hit_left && hit_right) {                                            /* :234 */
+        *out = (hl.t < hr.t) ? hl : hr;
+        return 1;
+    }
+    if (hit_right) { *out = hr; return 1; }
+    if (hit_left) { *out = hl; return 1; }
+    return 0;
+}
+
+static int hit_ref(const ctx_t* cx, int32_t ref, const ray_t* r, float tmin, float tmax, hit_t* out, int dup) {
+    if (ref >= 0) return bvh_hit(cx, &cx->s->nodes[ref], r, tmin, tmax, out);
+    uint32_t p = (uint32_t)(~ref);
+    uint32_t type = p >> 28, idx = p & 0x0FFFFFFFu;
+    if (type != RTX_PRIM_SPHERE) return 0; /* quads rejected by oracle_render */
+    cx->c->prim_tests_ref++;
+    if (!dup) cx->c->prim_tests++;
+    return sphere_hit(cx, &cx->s->spheres[idx], r, tmin, tmax, out);
+}
+
+/* The world passed to Render: a BVH (one root) or a World list, hittables.go:55-72. */
+static int world_hit(const ctx_t* cx, const ray_t* r, float tmin, float tmax, hit_t* out) {
+    int hit_any = 0;
+    float closest = tmax;
+    for (uint32_t i = 0; i < cx->s->n_roots; ++i) {
+        hit_t h;
+        if (hit_ref(cx, cx->s->roots[i], r, tmin, closest, &h, 0)) {
+            hit_any = 1;
+            *out = h;
+            closest = h.t;
+        }
+    }
+    return hit_any;
+}
+
+/* ============================================================================
+ * Textures and materials — internal/materials.go:9-193, 297-313.
+ * ========================================================================== */
+static vec3 texture_value(const ctx_t* cx, uint32_t ti, float u, float v, vec3 p) {
+    const rtx_texture* t = &cx->s->textures[ti];
+    switch (t->type) {
+    case RTX_TEX_SOLID:                                                     /* :151-163 */
+        return v3(t->even[0], t->even[1], t->even[2]);
+    case RTX_TEX_CHECKERED: {                                               /* :127-137 */
+        float inv_scale = 1.0f / t->scale;
+        int64_t x = (int64_t)floor((double)(inv_scale * p.x));
+        int64_t y = (int64_t)floor((double)(inv_scale * p.y));
+        int64_t z = (int64_t)floor((double)(inv_scale * p.z));
+        if ((x + y + z) % 2 == 0) return v3(t->even[0], t->even[1], t->even[2]);
+        return v3(t->odd[0], t->odd[1], t->odd[2]);
+    }
+    case RTX_TEX_IMAGE: {                                                   /* :175-193 */
+        if ((int32_t)t->height <= 0) return v3(0.0f, 1.0f, 1.0f);
+        /* Clamp(0, 1, x) passes NaN through (math.go:20-28). */
+        float uu = u < 0.0f ? 0.0f : (u > 1.0f ? 1.0f : u);
+        float vc = v < 0.0f ? 0.0f : (v > 1.0f ? 1.0f : v);
+        float vv = 1.0f - vc;
+        float fi = uu * (float)t->width;
+        float fj = vv * (float)t->height;
+        cx->c->texel_fetches++;
+        /* int(float32): truncation; NaN/out-of-range -> 0x8000000000000000 on amd64. */
+        int64_t i = isnan(fi) ? INT64_MIN : (int64_t)fi;
+        int64_t j = isnan(fj) ? INT64_MIN : (int64_t)fj;
+        /* image.RGBA.At outside Rect returns color.RGBA{} = black. */
+        if (i < 0 || j < 0 || i >= (int64_t)t->width || j >= (int64_t)t->height) return v3(0.0f, 0.0f, 0.0f);
+        uint32_t px = cx->s->texels[t->texel_offset + (uint64_t)j * t->width + (uint64_t)i];
+        /* color.RGBA.RGBA(): r |= r << 8; colScale = float32(1.0 / 65535.0). */
+        const float col_scale = 1.0f / 65535.0f;
+        uint32_t r8 = px & 0xFFu, g8 = (px >> 8) & 0xFFu, b8 = (px >> 16) & 0xFFu;
+        return v3((float)(r8 * 257u) * col_scale, (float)(g8 * 257u) * col_scale, (float)(b8 * 257u) * col_scale);
+    }
+    default:
+        return v3(0.0f, 0.0f, 0.0f);
+    }
+}
+
+/* Material.Emit: zero except DiffuseLight (materials.go:25, 51, 83, 311). */
+static vec3 material_emit(const ctx_t* cx, const hit_t* h, int* has) {
+    const rtx_material* m = &cx->s->materials[h->material];
+    if (m->type == RTX_MAT_DIFFUSE_LIGHT) {
+        *has = 1;
+        return texture_value(cx, m->texture, h->u, h->v, h->point);
+    }
+    *has = 0;
+    return v3(0.0f, 0.0f, 0.0f);
+}
+
+/* reflectance, materials.go:115-119. */
+static float reflectance(float cos_theta, float eta) {
+    float r0 = (1.0f - eta) / (1.0f + eta);
+    r0 *= r0;
+    return r0 + (1.0f - r0) * (float)go_pow5(1.0 - (double)cos_theta);
+}
+
+/* Material.Scatter.  Returns 1 and fills att/out if the ray scatters. */
+static int material_scatter(const ctx_t* cx, const ray_t* r, const hit_t* h, rng_t* rng, vec3* att, ray_t* out) {
+    const rtx_material* m = &cx->s->materials[h->material];
+    switch (m->type) {
+    case RTX_MAT_LAMBERTIAN: {                                              /* :33-42 */
+        vec3 dir = v_add(h->normal, rand_unit_on_sphere(rng));
+        if (v_near_zero(dir)) dir = h->normal;
+        out->origin = h->point;
+        out->dir = dir;
+        *att = texture_value(cx, m->texture, h->u, h->v, h->point);
+        return 1;
+    }
+    case RTX_MAT_METAL: {                                                   /* :60-75 */
+        vec3 unit_dir = v_unit(r->dir);
+        vec3 reflected = v_reflect(unit_dir, h->normal);
+        vec3 fuzz = rand_unit_on_sphere(rng);
+        fuzz = v_scale(fuzz, m->fuzz);
+        vec3 scattered = v_add(reflected, fuzz);
+        if (v_dot(scattered, h->normal) > 0.0f) {
+            out->origin = h->point;
+            out->dir = scattered;
+            *att = v3(m->albedo[0], m->albedo[1], m->albedo[2]);
+            return 1;
+        }
+        return 0;
+    }
+    case RTX_MAT_DIELECTRIC: {                                              /* :91-113 */
+        float eta = m->ior;
+        if (h->front) eta = 1.0f / m->ior;
+        vec3 unit_dir = v_unit(r->dir);
+        float cos_theta = (float)go_min((double)v_dot(v_scale(unit_dir, -1.0f), h->normal), 1.0);
+        float sin_theta = (float)sqrt(1.0 - (double)(cos_theta * cos_theta));
+        int cannot_refract = sin_theta * eta > 1.0f;
+        vec3 direction;
+        /* Short-circuit: the uniform is drawn only when refraction is possible.  The
+         * reference draws it from the global rand (materials.go:103); the contract
+         * moves it onto the per-ray stream. */
+        if (cannot_refract || reflectance(cos_theta, eta) > rng_float32(rng))
+            direction = v_reflect(unit_dir, h->normal);
+        else
+            direction = v_refract(unit_dir, h->normal, eta);
+        out->origin = h->point;
+        out->dir = direction;
+        *att = v3(1.0f, 1.0f, 1.0f);
+        return 1;
+    }
+    case RTX_MAT_DIFFUSE_LIGHT:                                             /* :303-305 */
+    default:
+        return 0;
+    }
+}
+
+/* (*Ray).GetColor, ray.go:32-54 — the recursion as written. */
+static vec3 ray_color_ref(const ctx_t* cx, const ray_t* r, rng_t* rng, int depth) {
+    if (depth <= 0) return v3(0.0f, 0.0f, 0.0f);
+    hit_t h;
+    cx->c->segments++;
+    const float inf = INFINITY;
+    if (world_hit(cx, r, 0.001f, inf, &h)) {
+        cx->c->hits++;
+        int has_emit;
+        vec3 emit = material_emit(cx, &h, &has_emit);
+        vec3 att;
+        ray_t scattered;
+        if (!material_scatter(cx, r, &h, rng, &att, &scattered)) return emit;
+        vec3 col = v_mul(att, ray_color_ref(cx, &scattered, rng, depth - 1));
+        return v_add(emit, col);
+    }
+    const float* bg = cx->cam->background;
+    return v3(bg[0], bg[1], bg[2]);
+}
+
+/* The same path, colour accumulated front to back (the kernel's order). */
+static vec3 ray_color_iter(const ctx_t* cx, ray_t r, rng_t* rng, int depth) {
+    vec3 thr = v3(1.0f, 1.0f, 1.0f);
+    vec3 acc = v3(0.0f, 0.0f, 0.0f);
+    for (; depth > 0; --depth) {
+        hit_t h;
+        cx->c->segments++;
+        if (!world_hit(cx, &r, 0.001f, INFINITY, &h)) {
+            const float* bg = cx->cam->background;
+            acc = v_add(acc, v_mul(thr, v3(bg[0], bg[1], bg[2])));
+            return acc;
+        }
+        cx->c->hits++;
+        int has_emit;
+        vec3 emit = material_emit(cx, &h, &has_emit);
+        if (has_emit) acc = v_add(acc, v_mul(thr, emit));
+        vec3 att;
+        ray_t scattered;
+        if (!material_scatter(cx, &r, &h, rng, &att, &scattered)) return acc;
+        thr = v_mul(thr, att);
+        r = scattered;
+    }
+    return acc;
+}
+
+/* GetRay + sampleUnitSquare, camera.go:265-299. */
+static ray_t get_ray(const ctx_t* cx, rng_t* rng, uint32_t i, uint32_t j) {
+    const rtx_camera* c = cx->cam;
+    vec3 du = v3(c->pixel_du[0], c->pixel_du[1], c->pixel_du[2]);
+    vec3 dv = v3(c->pixel_dv[0], c->pixel_dv[1], c->pixel_dv[2]);
+    vec3 du_off = v_scale(du, (float)i);                                    /* :266-267 */
+    vec3 dv_off = v_scale(dv, (float)j);                                    /* :269-270 */
+    vec3 pc = v3(c->pixel00[0], c->pixel00[1], c->pixel00[2]);              /* :272 */
+    pc = v_add(pc, du_off);                                                 /* :273 */
+    pc = v_add(pc, dv_off);                                                 /* :274 */
+    float dx = -0.5f + rng_float32(rng);                                    /* :290 */
+    float dy = -0.5f + rng_float32(rng);                                    /* :291 */
+    pc = v_add(pc, v_add(v_scale(du, dx), v_scale(dv, dy)));                /* :275, 293-298 */
+    vec3 disc = rand_in_unit_disk(rng);                                     /* :277 (always drawn) */
+    vec3 center = v3(c->center[0], c->center[1], c->center[2]);
+    vec3 origin = center;                                                   /* :278 */
+    if (c->defocus_angle > 0.0f) {                                          /* :279-281 */
+        vec3 ddu = v3(c->defocus_disk_u[0], c->defocus_disk_u[1], c->defocus_disk_u[2]);
+        vec3 ddv = v3(c->defocus_disk_v[0], c->defocus_disk_v[1], c->defocus_disk_v[2]);
+        origin = v_add(center, v_add(v_scale(ddu, disc.x), v_scale(ddv, disc.y)));
+    }
+    ray_t r;
+    r.origin = origin;
+    r.dir = v_sub(pc, origin);                                              /* :283-284 */
+    return r;
+}
+
+static vec3 sample_color(const ctx_t* cx, uint32_t i, uint32_t j, uint32_t k) {
+    rng_t rng;
+    rng.key[0] = (uint32_t)cx->seed;
+    rng.key[1] = (uint32_t)(cx->seed >> 32);
+    rng.pixel = j * cx->cam->image_width + i;
+    rng.sample = k;
+    rng.n = 0;
+    rng.draws = &cx->c->rng_draws;
+    ray_t r = get_ray(cx, &rng, i, j);
+    cx->c->samples++;
+    if (cx->order == ORACLE_ORDER_ITERATIVE) return ray_color_iter(cx, r, &rng, (int)cx->cam->max_depth);
+    return ray_color_ref(cx, &r, &rng, (int)cx->cam->max_depth);
+}
+
+/* GetPixelColor, camera.go:254-263. */
+static vec3 pixel_color(const ctx_t* cx, uint32_t i, uint32_t j) {
+    vec3 sum = v3(0.0f, 0.0f, 0.0f);
+    uint32_t spp = cx->cam->samples_per_pixel;
+    for (uint32_t k = 0; k < spp; ++k) sum = v_add(sum, sample_color(cx, i, j, k));
+    return v_scale(sum, 1.0f / (float)spp);
+}
+
+/* ============================================================================
+ * Region rendering, threads over rows.
+ * ========================================================================== */
+uint32_t oracle_region_rows(const rtx_region* r) {
+    if (r->world == 0 || r->rank >= r->world || r->height <= r->rank) return 0;
+    return (r->height - r->rank + r->world - 1) / r->world;
+}
+
+static int scene_supported(const rtx_scene_desc* s) {
+    if (!s || !s->roots || s->n_roots == 0) return 0;
+    for (uint32_t i = 0; i < s->n_materials; ++i)
+        if (s->materials[i].type > RTX_MAT_DIFFUSE_LIGHT) return 0;
+    for (uint32_t i = 0; i < s->n_textures; ++i)
+        if (s->textures[i].type > RTX_TEX_IMAGE) return 0;
+    if (s->n_quads) return 0;
+    return 1;
+}
+
+typedef struct {
+    const rtx_scene_desc* s;
+    const rtx_camera* cam;
+    uint64_t seed;
+    const rtx_region* reg;
+    int order;
+    float* out;
+    uint32_t rows;
+    uint32_t next_row;
+    pthread_mutex_t mu;
+    oracle_counters total;
+} job_t;
+
+static void* worker(void* arg) {
+    job_t* jb = (job_t*)arg;
+    oracle_counters local;
+    memset(&local, 0, sizeof(local));
+    ctx_t cx = {jb->s, jb->cam, jb->seed, jb->order, &local};
+    for (;;) {
+        pthread_mutex_lock(&jb->mu);
+        uint32_t lr = jb->next_row++;
+        pthread_mutex_unlock(&jb->mu);
+        if (lr >= jb->rows) break;
+        uint32_t y = jb->reg->y0 + jb->reg->rank + lr * jb->reg->world;
+        for (uint32_t xx = 0; xx < jb->reg->width; ++xx) {
+            vec3 c = pixel_color(&cx, jb->reg->x0 + xx, y);
+            float* o = jb->out + ((size_t)lr * jb->reg->width + xx) * 3;
+            o[0] = c.x; o[1] = c.y; o[2] = c.z;
+        }
+    }
+    pthread_mutex_lock(&jb->mu);
+    jb->total.samples += local.samples;
+    jb->total.segments += local.segments;
+    jb->total.node_visits += local.node_visits;
+    jb->total.prim_tests_ref += local.prim_tests_ref;
+    jb->total.prim_tests += local.prim_tests;
+    jb->total.hits += local.hits;
+    jb->total.texel_fetches += local.texel_fetches;
+    jb->total.rng_draws += local.rng_draws;
+    pthread_mutex_unlock(&jb->mu);
+    return NULL;
+}
+
+int oracle_render(const rtx_scene_desc* s, const rtx_camera* cam, uint64_t seed, const rtx_region* reg, int order,
+                  int threads, float* out, oracle_counters* counters) {
+    if (!s || !cam || !reg || !out || !scene_supported(s)) return -1;
+    if (cam->samples_per_pixel == 0 || reg->world == 0 || reg->rank >= reg->world) return -1;
+    if (reg->x0 + reg->width > cam->image_width || reg->y0 + reg->height > cam->image_height) return -1;
+    job_t jb;
+    memset(&jb, 0, sizeof(jb));
+    jb.s = s; jb.cam = cam; jb.seed = seed; jb.reg = reg; jb.order = order; jb.out = out;
+    jb.rows = oracle_region_rows(reg);
+    pthread_mutex_init(&jb.mu, NULL);
+    if (threads <= 1) {
+        worker(&jb);
+    } else {
+        pthread_t* th = (pthread_t*)calloc((size_t)threads, sizeof(pthread_t));
+        for (int t = 0; t < threads; ++t) pthread_create(&th[t], NULL, worker, &jb);
+        for (int t = 0; t < threads; ++t) pthread_join(th[t], NULL);
+        free(th);
+    }
+    pthread_mutex_destroy(&jb.mu);
+    if (counters) *counters = jb.total;
+    return 0;
+}
+
+int oracle_sample(const rtx_scene_desc* s, const rtx_camera* cam, uint64_t seed, uint32_t px, uint32_t py,
+                  uint32_t k, int order, float rgb[3], oracle_counters* counters) {
+    if (!s || !cam || !rgb || !scene_supported(s)) return -1;
+    oracle_counters local;
+    memset(&local, 0, sizeof(local));
+    ctx_t cx = {s, cam, seed, order, &local};
+    vec3 c = sample_color(&cx, px, py, k);
+    rgb[0] = c.x; rgb[1] = c.y; rgb[2] = c.z;
+    if (counters) *counters = local;
+    return 0;
+}
+
+/* ToGamma2 -> ToRGB -> String, vec3.go:141-166, math.go:20-28. */
+static int64_t go_int_of_f32(float f) {
+    /* amd64 CVTTSS2SQ: truncation; NaN and out-of-range give 0x8000000000000000. */
+    if (isnan(f) || f >= 9223372036854775808.0f || f < -9223372036854775808.0f) return INT64_MIN;
+    return (int64_t)f;
+}
+int oracle_ppm_pixel(const float rgb[3], char* buf) {
+    int64_t q[3];
+    for (int c = 0; c < 3; ++c) {
+        float v = (float)sqrt((double)rgb[c]);                 /* ToGamma2 */
+        if (v < 0.0f) v = 0.0f;                                 /* Clamp(0, 1, v) */
+        else if (v > 1.0f) v = 1.0f;
+        v *= 255.999f;                                          /* ToRGB */
+        q[c] = go_int_of_f32(v);                                /* String: int(v.X) */
+    }
+    return sprintf(buf, "%lld %lld %lld", (long long)q[0], (long long)q[1], (long long)q[2]);
+}
+
+/* ============================================================================
+ * Scene builders: main.go:227-289 randSpheres + bvh.go:138-185 NewBVH, with the
+ * reference's two RNGs restated as seeded streams: the global math/rand (stream 1;
+ * matPer, centres, and the BVH axis, main.go:251-252, bvh.go:147) and randCtx
+ * (stream 2; material values, main.go:259-265).
+ * ========================================================================== */
+enum { STREAM_GLOBAL = 1, STREAM_CTX = 2 };
+
+typedef struct {
+    uint64_t seed;
+    uint32_t stream;
+    uint64_t n;
+} host_rng;
+
+static inline uint32_t hr_u32(host_rng* r) { return oracle_stream_u32(r->seed, r->stream, r->n++); }
+static inline float hr_float32(host_rng* r) { return u32_to_unit(hr_u32(r)); }
+/* rand.Intn(n) of the contract: multiply-shift of one word. */
+static inline int hr_intn(host_rng* r, int n) { return (int)(((uint64_t)hr_u32(r) * (uint64_t)n) >> 32); }
+/* RandF32N on a host stream, math.go:30-32. */
+static inline float rand_f32n_host(host_rng* r, float mn, float mx) { return mn + hr_float32(r) * (mx - mn); }
+
+typedef struct { float mn[3], mx[3]; } aabb_t;
+
+struct oracle_scene {
+    rtx_scene_desc desc;
+    rtx_bvh_node* nodes;
+    uint32_t n_nodes, cap_nodes;
+    rtx_sphere* spheres;
+    uint32_t n_spheres, cap_spheres;
+    rtx_material* materials;
+    uint32_t n_materials, cap_materials;
+    rtx_texture* textures;
+    uint32_t n_textures, cap_textures;
+    int32_t root;
+    aabb_t* sphere_box;
+};
+
+#define GROW(arr, n, cap)                                                        \
+    do {                                                                         \
+        if ((n) >= (cap)) {                                                      \
+            (cap) = (cap) ? (cap)*2 : 64;                                        \
+            (arr) = realloc((arr), sizeof(*(arr)) * (size_t)(cap));              \
+        }                                                                        \
+    } while (0)
+
+static uint32_t add_texture(oracle_scene* s, rtx_texture t) {
+    GROW(s->textures, s->n_textures, s->cap_textures);
+    s->textures[s->n_textures] = t;
+    return s->n_textures++;
+}
+static uint32_t add_material(oracle_scene* s, rtx_material m) {
+    GROW(s->materials, s->n_materials, s->cap_materials);
+    s->materials[s->n_materials] = m;
+    return s->n_materials++;
+}
+static uint32_t solid(oracle_scene* s, float r, float g, float b) {        /* NewSolidColor, materials.go:159 */
+    rtx_texture t;
+    memset(&t, 0, sizeof(t));
+    t.type = RTX_TEX_SOLID;
+    t.even[0] = r; t.even[1] = g; t.even[2] = b;
+    return add_texture(s, t);
+}
+static uint32_t lambertian(oracle_scene* s, uint32_t tex) {
+    rtx_material m;
+    memset(&m, 0, sizeof(m));
+    m.type = RTX_MAT_LAMBERTIAN;
+    m.texture = tex;
+    return add_material(s, m);
+}
+static uint32_t metal(oracle_scene* s, vec3 albedo, float fuzz) {
+    rtx_material m;
+    memset(&m, 0, sizeof(m));
+    m.type = RTX_MAT_METAL;
+    m.albedo[0] = albedo.x; m.albedo[1] = albedo.y; m.albedo[2] = albedo.z;
+    m.fuzz = fuzz;
+    return add_material(s, m);
+}
+static uint32_t dielectric(oracle_scene* s, float ior) {
+    rtx_material m;
+    memset(&m, 0, sizeof(m));
+    m.type = RTX_MAT_DIELECTRIC;
+    m.ior = ior;
+    return add_material(s, m);
+}
+/* NewSphere, hittables.go:85-94: bbox = NewAabb(center + (-r), center + r). */
+static void add_sphere(oracle_scene* s, vec3 c, float r, uint32_t mat) {
+    GROW(s->spheres, s->n_spheres, s->cap_spheres);
+    rtx_sphere* sp = &s->spheres[s->n_spheres++];
+    memset(sp, 0, sizeof(*sp));
+    sp->center[0] = c.x; sp->center[1] = c.y; sp->center[2] = c.z;
+    sp->radius = r;
+    sp->material = mat;
+}
+static aabb_t sphere_bounds(const rtx_sphere* sp) {
+    vec3 c = v3(sp->center[0], sp->center[1], sp->center[2]);
+    vec3 rv = v3(sp->radius, sp->radius, sp->radius);
+    vec3 p1 = v_add(c, v_scale(rv, -1.0f)), p2 = v_add(c, rv);
+    aabb_t b;                                                              /* NewAabb, bvh.go:28-34 */
+    b.mn[0] = min_f32(p1.x, p2.x); b.mx[0] = max_f32(p1.x, p2.x);
+    b.mn[1] = min_f32(p1.y, p2.y); b.mx[1] = max_f32(p1.y, p2.y);
+    b.mn[2] = min_f32(p1.z, p2.z); b.mx[2] = max_f32(p1.z, p2.z);
+    return b;
+}
+static aabb_t box_union(aabb_t a, aabb_t b) {                               /* NewAabbFromBoxes, bvh.go:44-50 */
+    aabb_t r;
+    for (int k = 0; k < 3; ++k) {
+        r.mn[k] = min_f32(a.mn[k], b.mn[k]);
+        r.mx[k] = max_f32(a.mx[k], b.mx[k]);
+    }
+    return r;
+}
+
+typedef struct { int32_t ref; aabb_t box; } item_t;
+
+static aabb_t ref_box(const oracle_scene* s, int32_t ref) {
+    if (ref >= 0) {
+        aabb_t b;
+        memcpy(b.mn, s->nodes[ref].bmin, sizeof(b.mn));
+        memcpy(b.mx, s->nodes[ref].bmax, sizeof(b.mx));
+        return b;
+    }
+    return s->sphere_box[(~ref) & 0x0FFFFFFF];
+}
+
+/* HittableCompare{X,Y,Z}, bvh.go:187-218: +1 when h2.min > h1.min (sort descending).
+ * The contract's sort is stable (x/exp/slices.SortFunc is pdqsort and unstable; equal
+ * keys may land in either order in the reference). */
+static int cmp_axis(const item_t* a, const item_t* b, int axis) {
+    float diff = b->box.mn[axis] - a->box.mn[axis];
+    if (diff > 0.0f) return 1;
+    if (diff < 0.0f) return -1;
+    return 0;
+}
+static void stable_sort(item_t* h, size_t n, int axis) {
+    /* insertion sort in blocks + merge: n is small (<= a few 1e5); use a simple merge sort */
+    if (n < 2) return;
+    item_t* tmp = malloc(sizeof(item_t) * n);
+    for (size_t width = 1; width < n; width *= 2) {
+        for (size_t lo = 0; lo < n; lo += 2 * width) {
+            size_t mid = lo + width < n ? lo + width : n;
+            size_t hi = lo + 2 * width < n ? lo + 2 * width : n;
+            size_t i = lo, j = mid, k = lo;
+            while (i < mid && j < hi) {
+                if (cmp_axis(&h[j], &h[i], axis) < 0) tmp[k++] = h[j++];
+                else tmp[k++] = h[i++];
+            }
+            while (i < mid) tmp[k++] = h[i++];
+            while (j < hi) tmp[k++] = h[j++];
+        }
+        memcpy(h, tmp, sizeof(item_t) * n);
+    }
+    free(tmp);
+}
+
+/* NewBVH, bvh.go:142-185.  Returns the node index.  Nodes are numbered in creation
+ * (pre-)order: a node's index is reserved before its children are built. */
+static int32_t new_bvh(oracle_scene* s, host_rng* grng, const item_t* in, size_t n) {
+    item_t* h = malloc(sizeof(item_t) * n);                                  /* :144-145 */
+    memcpy(h, in, sizeof(item_t) * n);
+    int axis = hr_intn(grng, 3);                                             /* :147 */
+    GROW(s->nodes, s->n_nodes, s->cap_nodes);
+    int32_t me = (int32_t)s->n_nodes++;
+    int32_t left, right;
+    if (n == 1) {                                                            /* :162-165 */
+        left = right = h[0].ref;
+    } else if (n == 2) {                                                     /* :166-174 */
+        if (cmp_axis(&h[0], &h[1], axis) > 0) {
+            left = h[1].ref; right = h[0].ref;
+        } else {
+            left = h[0].ref; right = h[1].ref;
+        }
+    } else {                                                                 /* :175-180 */
+        stable_sort(h, n, axis);
+        size_t mid = n / 2;
+        left = new_bvh(s, grng, h, mid);
+        right = new_bvh(s, grng, h + mid, n - mid);
+    }
+    aabb_t b = box_union(ref_box(s, left), ref_box(s, right));               /* :182 */
+    rtx_bvh_node* node = &s->nodes[me];
+    memcpy(node->bmin, b.mn, sizeof(b.mn));
+    memcpy(node->bmax, b.mx, sizeof(b.mx));
+    node->left = left;
+    node->right = right;
+    free(h);
+    return me;
+}
+
+oracle_scene* oracle_build_random_spheres(uint64_t seed) {
+    oracle_scene* s = calloc(1, sizeof(oracle_scene));
+    host_rng grng = {seed, STREAM_GLOBAL, 0};
+    host_rng crng = {seed, STREAM_CTX, 0};
+    /* main.go:242-244 */
+    rtx_texture chk;
+    memset(&chk, 0, sizeof(chk));
+    chk.type = RTX_TEX_CHECKERED;
+    chk.scale = 0.32f;
+    chk.even[0] = 0.2f; chk.even[1] = 0.3f; chk.even[2] = 0.1f;
+    chk.odd[0] = 0.9f; chk.odd[1] = 0.9f; chk.odd[2] = 0.9f;
+    uint32_t ground = lambertian(s, add_texture(s, chk));
+    add_sphere(s, v3(0.0f, -1000.0f, 0.0f), 1000.0f, ground);
+    vec3 p = v3(4.0f, 0.2f, 0.0f);                                           /* :248 */
+    for (int i = -11; i < 11; ++i) {                                         /* :249 */
+        for (int j = -11; j < 11; ++j) {                                     /* :250 */
+            float mat_per = hr_float32(&grng);                               /* :251 */
+            float cx = (float)i + 0.9f * hr_float32(&grng);                  /* :252 */
+            float cz = (float)j + 0.9f * hr_float32(&grng);
+            vec3 center = v3(cx, 0.2f, cz);
+            vec3 dist = v_sub(center, p);                                    /* :254 */
+            float ln = (float)sqrt((double)v_lensq(dist));                   /* :255, vec3.go:119-121 */
+            if (ln > 0.9f) {                                                 /* :256 */
+                uint32_t m;
+                if (mat_per < 0.8f) {                                        /* :258-262 */
+                    float a0 = hr_float32(&crng), a1 = hr_float32(&crng), a2 = hr_float32(&crng);
+                    float b0 = hr_float32(&crng), b1 = hr_float32(&crng), b2 = hr_float32(&crng);
+                    vec3 col = v_mul(v3(a0, a1, a2), v3(b0, b1, b2));
+                    m = lambertian(s, solid(s, col.x, col.y, col.z));
+                } else if (mat_per < 0.95f) {                                /* :263-267 */
+                    float x = rand_f32n_host(&crng, 0.5f, 1.0f);
+                    float y = rand_f32n_host(&crng, 0.5f, 1.0f);
+                    float z = rand_f32n_host(&crng, 0.5f, 1.0f);
+                    float fuzz = rand_f32n_host(&crng, 0.0f, 0.5f);
+                    m = metal(s, v3(x, y, z), fuzz);
+                } else {                                                     /* :268-271 */
+                    m = dielectric(s, 1.5f);
+                }
+                add_sphere(s, center, 0.2f, m);                              /* :272 */
+            }
+        }
+    }
+    add_sphere(s, v3(0.0f, 1.0f, 0.0f), 1.0f, dielectric(s, 1.5f));          /* :278-279 */
+    add_sphere(s, v3(-4.0f, 1.0f, 0.0f), 1.0f, lambertian(s, solid(s, 0.4f, 0.2f, 0.1f))); /* :281-282 */
+    add_sphere(s, v3(4.0f, 1.0f, 0.0f), 1.0f, metal(s, v3(0.7f, 0.6f, 0.5f), 0.0f));       /* :284-285 */
+
+    /* NewBVHFromWorld, main.go:287 -> bvh.go:138-140 */
+    s->sphere_box = malloc(sizeof(aabb_t) * s->n_spheres);
+    item_t* items = malloc(sizeof(item_t) * s->n_spheres);
+    for (uint32_t k = 0; k < s->n_spheres; ++k) {
+        s->sphere_box[k] = sphere_bounds(&s->spheres[k]);
+        items[k].ref = RTX_REF_PRIM(RTX_PRIM_SPHERE, k);
+        items[k].box = s->sphere_box[k];
+    }
+    s->root = new_bvh(s, &grng, items, s->n_spheres);
+    free(items);
+
+    s->desc.nodes = s->nodes;
+    s->desc.n_nodes = s->n_nodes;
+    s->desc.n_roots = 1;
+    s->desc.roots = &s->root;
+    s->desc.spheres = s->spheres;
+    s->desc.n_spheres = s->n_spheres;
+    s->desc.materials = s->materials;
+    s->desc.n_materials = s->n_materials;
+    s->desc.textures = s->textures;
+    s->desc.n_textures = s->n_textures;
+    return s;
+}
+
+const rtx_scene_desc* oracle_scene_desc(const oracle_scene* s) { return &s->desc; }
+
+void oracle_scene_free(oracle_scene* s) {
+    if (!s) return;
+    free(s->nodes);
+    free(s->spheres);
+    free(s->materials);
+    free(s->textures);
+    free(s->sphere_box);
+    free(s);
+}

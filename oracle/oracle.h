@@ -1,0 +1,105 @@
+/*
+ * oracle.h — CPU restatement of TwFlem/raytracer-go's hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg may load liboracle.so, and only as the checker / CPU baseline,
+ * never as the product path.
+ *
+ * Parity status: PARITY UNPINNED against the reference binary.  The reference is Go
+ * (no Go toolchain in this image or on the GPU box), it ships no tests, no fixtures
+ * and no golden image (its one PPM is stripped, .MISSING_LARGE_BLOBS:1), and it is
+ * nondeterministic by construction (time-seeded RNGs, camera.go:170, main.go:246;
+ * global rand in materials.go:103 and bvh.go:147).  The oracle is therefore a
+ * line-by-line restatement of the cited Go source with the reference's RNG replaced
+ * by the counter-based RNG contract of SURVEY.md §8c (Philox4x32-10, pinned by the
+ * published Random123 known-answer vectors), plus known-answer tests derived from the
+ * source text (tests/test_oracle_kat.py).
+ *
+ * Every function cites the reference file:line it restates.  Float semantics: IEEE
+ * float32, no contraction (built with -ffp-contract=off), float64 exactly where the Go
+ * code widens to float64.
+ */
+#ifndef RTX_ORACLE_H
+#define RTX_ORACLE_H
+
+#include <stdint.h>
+
+#include "../include/rtx.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Colour evaluation order of Ray.GetColor.
+ *  REFERENCE: the recursion of ray.go:32-54, emit + att * GetColor(depth-1).
+ *  ITERATIVE: L += T*emit; T *= att (front to back) — same path decisions, the colour
+ *  product is rounded in the other order.  The HIP kernel uses this order, so it must
+ *  match the ITERATIVE oracle bit for bit and the REFERENCE oracle to ~1 ulp.       */
+enum { ORACLE_ORDER_REFERENCE = 0, ORACLE_ORDER_ITERATIVE = 1 };
+
+typedef struct oracle_counters {
+    uint64_t samples;
+    uint64_t segments;        /* world.Hit calls, ray.go:36                         */
+    uint64_t node_visits;     /* Aabb.Hit calls, bvh.go:221                         */
+    uint64_t prim_tests_ref;  /* Sphere.Hit calls as the reference makes them        */
+    uint64_t prim_tests;      /* ... minus the redundant second test of left==right  */
+    uint64_t hits;
+    uint64_t texel_fetches;
+    uint64_t rng_draws;
+} oracle_counters;
+
+/* Philox4x32-10 (Salmon et al., SC'11; Random123). */
+void oracle_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);
+
+/* The per-ray stream of the RNG contract: draw n of sample k of global pixel p. */
+float oracle_pixel_draw(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t n);
+
+/* Host streams (scene generation / BVH axis): word n of stream s. */
+uint32_t oracle_stream_u32(uint64_t seed, uint32_t stream, uint64_t n);
+
+/* Camera options as the reference's functional options leave them (camera.go:56-117). */
+typedef struct oracle_camera_opts {
+    int32_t samples_per_pixel;
+    int32_t max_depth;
+    float fov_radians;     /* default float32(PiO2)                     camera.go:108 */
+    float look_from[3];
+    float look_at[3];
+    float vup[3];
+    float defocus_radians;
+    float focus_dist;
+    float background[3];
+} oracle_camera_opts;
+
+void oracle_camera_defaults(oracle_camera_opts* o);               /* camera.go:105-117 */
+float oracle_to_radians(float degrees);                           /* math.go:50-52      */
+/* Camera.init restated (camera.go:128-165). */
+void oracle_camera_init(float aspect_ratio, int32_t image_width, const oracle_camera_opts* o, rtx_camera* out);
+
+/* Render a region (rtx.h semantics).  threads <= 0 -> 1.  out holds
+ * rtx_region_rows(region) * region->width * 3 floats.  counters may be NULL.
+ * Returns 0, or -1 on bad arguments / unsupported scene features.                */
+int oracle_render(const rtx_scene_desc* scene, const rtx_camera* cam, uint64_t seed, const rtx_region* region,
+                  int order, int threads, float* out, oracle_counters* counters);
+
+/* One sample of one pixel (GetRay + GetColor), for tracing individual paths. */
+int oracle_sample(const rtx_scene_desc* scene, const rtx_camera* cam, uint64_t seed, uint32_t px, uint32_t py,
+                  uint32_t k, int order, float rgb[3], oracle_counters* counters);
+
+/* Output path: ToGamma2 -> ToRGB -> String (vec3.go:141-166), into buf (>= 64 B).
+ * Returns the string length. */
+int oracle_ppm_pixel(const float rgb[3], char* buf);
+
+/* ---- scene builders (main.go restated with the seeded streams) ---------------- */
+typedef struct oracle_scene oracle_scene;
+/* randSpheres, main.go:227-289 (scene + NewBVHFromWorld, bvh.go:138-185). */
+oracle_scene* oracle_build_random_spheres(uint64_t seed);
+const rtx_scene_desc* oracle_scene_desc(const oracle_scene* s);
+void oracle_scene_free(oracle_scene* s);
+
+/* Independent recompute of rtx_region_rows. */
+uint32_t oracle_region_rows(const rtx_region* r);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,444 @@
+// rtx_capi.hip — the C-ABI of librtx.so (include/rtx.h).
+//
+// Host-side half of the drop-in boundary: validates the flattened Hittable tree the
+// caller hands over (what a cgo Render would pass), converts it once into the
+// threaded pre-order device layout (rtx_layout.h), keeps it resident in HBM per
+// device, and launches the megakernel.  Errors are returned as codes with a
+// thread-local message; nothing throws across the ABI.
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/rtx.h"
+#include "rtx_device.h"
+#include "rtx_kernel.h"
+#include "rtx_layout.h"
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_last_error = buf;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                             \
+    do {                                                                                          \
+        hipError_t e_ = (expr);                                                                   \
+        if (e_ != hipSuccess)                                                                     \
+            return fail(e_ == hipErrorOutOfMemory ? RTX_ERR_OOM : RTX_ERR_HIP, "%s failed: %s (%s:%d)", \
+                        #expr, hipGetErrorString(e_), __FILE__, __LINE__);                        \
+    } while (0)
+
+struct DeviceCopy {
+    int device = -1;
+    rtx_entry* entries = nullptr;
+    rtx_material* materials = nullptr;
+    rtx_texture* textures = nullptr;
+    uint32_t* texels = nullptr;
+    unsigned long long* counters = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+};
+
+}  // namespace
+
+struct rtx_scene {
+    std::vector<rtx_entry> entries;
+    std::vector<rtx_material> materials;
+    std::vector<rtx_texture> textures;
+    std::vector<uint32_t> texels;
+    std::map<int, DeviceCopy> copies;
+    std::mutex mu;
+};
+
+namespace {
+
+int check_ref(const rtx_scene_desc* d, int32_t ref) {
+    if (ref >= 0) {
+        if ((uint32_t)ref >= d->n_nodes) return fail(RTX_ERR_INVALID_ARG, "node ref %d out of range (%u nodes)", ref, d->n_nodes);
+        return RTX_OK;
+    }
+    const uint32_t p = (uint32_t)(~ref);
+    const uint32_t type = p >> 28, idx = p & 0x0FFFFFFFu;
+    if (type == RTX_PRIM_SPHERE) {
+        if (idx >= d->n_spheres) return fail(RTX_ERR_INVALID_ARG, "sphere ref %u out of range (%u spheres)", idx, d->n_spheres);
+        return RTX_OK;
+    }
+    if (type == RTX_PRIM_QUAD) return fail(RTX_ERR_UNSUPPORTED, "Quad primitives are not on the GPU path yet (hittables.go:138-216)");
+    return fail(RTX_ERR_INVALID_ARG, "unknown primitive type %u", type);
+}
+
+// Reject a node graph with a cycle (a Go BVH cannot have one, a hand-built table can).
+int check_acyclic(const rtx_scene_desc* d) {
+    std::vector<uint8_t> state(d->n_nodes, 0);  // 0 new, 1 on path, 2 done
+    struct F { int32_t node; int child; };
+    for (uint32_t r = 0; r < d->n_roots; ++r) {
+        if (int rc = check_ref(d, d->roots[r])) return rc;
+        if (d->roots[r] < 0 || state[d->roots[r]] == 2) continue;
+        std::vector<F> st{{d->roots[r], 0}};
+        state[d->roots[r]] = 1;
+        while (!st.empty()) {
+            F& f = st.back();
+            if (f.child == 2) { state[f.node] = 2; st.pop_back(); continue; }
+            const int32_t ref = f.child++ == 0 ? d->nodes[f.node].left : d->nodes[f.node].right;
+            if (int rc = check_ref(d, ref)) return rc;
+            if (ref < 0 || state[ref] == 2) continue;
+            if (state[ref] == 1) return fail(RTX_ERR_INVALID_ARG, "BVH node graph has a cycle through node %d", ref);
+            state[ref] = 1;
+            st.push_back({ref, 0});
+        }
+    }
+    return RTX_OK;
+}
+
+// Emit the reference's visit order (bvh.go:220-249) as threaded pre-order entries.
+int emit(const rtx_scene_desc* d, int32_t root, std::vector<rtx_entry>& out) {
+    struct Frame {
+        int32_t ref;
+        int64_t node_entry;  // >= 0: close this node's escape when popped
+    };
+    std::vector<Frame> stack;
+    stack.push_back({root, -1});
+    const size_t limit = (size_t)1 << 26;  // 2 GiB of entries
+    while (!stack.empty()) {
+        Frame f = stack.back();
+        stack.pop_back();
+        if (f.node_entry >= 0) {  // subtree finished
+            const int32_t esc = (int32_t)out.size();
+            std::memcpy(&out[(size_t)f.node_entry].a[3], &esc, 4);
+            continue;
+        }
+        if (int rc = check_ref(d, f.ref)) return rc;
+        if (out.size() >= limit) return fail(RTX_ERR_INVALID_ARG, "BVH expands to more than %zu entries", limit);
+        rtx_entry e;
+        std::memset(&e, 0, sizeof(e));
+        if (f.ref >= 0) {
+            const rtx_bvh_node& n = d->nodes[f.ref];
+            e.a[0] = n.bmin[0]; e.a[1] = n.bmin[1]; e.a[2] = n.bmin[2];
+            e.b[0] = n.bmax[0]; e.b[1] = n.bmax[1]; e.b[2] = n.bmax[2];
+            const int32_t tag = RTX_E_NODE;
+            std::memcpy(&e.b[3], &tag, 4);
+            const int64_t me = (int64_t)out.size();
+            out.push_back(e);
+            // visit order: left, then right (skipped when left == right, see rtx_layout.h)
+            stack.push_back({0, me});
+            if (n.right != n.left) stack.push_back({n.right, -1});
+            stack.push_back({n.left, -1});
+        } else {
+            const uint32_t idx = ((uint32_t)(~f.ref)) & 0x0FFFFFFFu;
+            const rtx_sphere& s = d->spheres[idx];
+            e.a[0] = s.center[0]; e.a[1] = s.center[1]; e.a[2] = s.center[2]; e.a[3] = s.radius;
+            e.b[0] = s.radius * s.radius;  // hittables.go:100
+            const int32_t si = (int32_t)idx, mi = (int32_t)s.material;
+            std::memcpy(&e.b[1], &si, 4);
+            std::memcpy(&e.b[3], &mi, 4);
+            out.push_back(e);
+        }
+    }
+    return RTX_OK;
+}
+
+int ensure_device(rtx_scene* s, int device, DeviceCopy** out) {
+    auto it = s->copies.find(device);
+    if (it != s->copies.end()) {
+        *out = &it->second;
+        return RTX_OK;
+    }
+    DeviceCopy c;
+    c.device = device;
+    HIP_TRY(hipSetDevice(device));
+    HIP_TRY(hipMalloc(&c.entries, s->entries.size() * sizeof(rtx_entry)));
+    HIP_TRY(hipMemcpy(c.entries, s->entries.data(), s->entries.size() * sizeof(rtx_entry), hipMemcpyHostToDevice));
+    HIP_TRY(hipMalloc(&c.materials, std::max<size_t>(1, s->materials.size()) * sizeof(rtx_material)));
+    if (!s->materials.empty())
+        HIP_TRY(hipMemcpy(c.materials, s->materials.data(), s->materials.size() * sizeof(rtx_material), hipMemcpyHostToDevice));
+    HIP_TRY(hipMalloc(&c.textures, std::max<size_t>(1, s->textures.size()) * sizeof(rtx_texture)));
+    if (!s->textures.empty())
+        HIP_TRY(hipMemcpy(c.textures, s->textures.data(), s->textures.size() * sizeof(rtx_texture), hipMemcpyHostToDevice));
+    HIP_TRY(hipMalloc(&c.texels, std::max<size_t>(1, s->texels.size()) * sizeof(uint32_t)));
+    if (!s->texels.empty())
+        HIP_TRY(hipMemcpy(c.texels, s->texels.data(), s->texels.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+    HIP_TRY(hipMalloc(&c.counters, 8 * sizeof(unsigned long long)));
+    HIP_TRY(hipEventCreate(&c.ev0));
+    HIP_TRY(hipEventCreate(&c.ev1));
+    auto res = s->copies.emplace(device, c);
+    *out = &res.first->second;
+    return RTX_OK;
+}
+
+void free_copy(DeviceCopy& c) {
+    if (hipSetDevice(c.device) != hipSuccess) return;
+    (void)hipFree(c.entries);
+    (void)hipFree(c.materials);
+    (void)hipFree(c.textures);
+    (void)hipFree(c.texels);
+    (void)hipFree(c.counters);
+    if (c.ev0) (void)hipEventDestroy(c.ev0);
+    if (c.ev1) (void)hipEventDestroy(c.ev1);
+}
+
+int check_camera(const rtx_camera* cam) {
+    if (!cam) return fail(RTX_ERR_INVALID_ARG, "camera is NULL");
+    if (cam->image_width == 0 || cam->image_height == 0) return fail(RTX_ERR_INVALID_ARG, "empty image");
+    if (cam->samples_per_pixel == 0) return fail(RTX_ERR_INVALID_ARG, "samples_per_pixel must be > 0");
+    if ((uint64_t)cam->image_width * cam->image_height > 0xFFFFFFFFull)
+        return fail(RTX_ERR_INVALID_ARG, "image has more than 2^32 pixels (RNG counter is 32-bit)");
+    return RTX_OK;
+}
+
+int check_region(const rtx_camera* cam, const rtx_region* r) {
+    if (!r) return fail(RTX_ERR_INVALID_ARG, "region is NULL");
+    if (r->world == 0 || r->rank >= r->world) return fail(RTX_ERR_INVALID_ARG, "bad shard %u/%u", r->rank, r->world);
+    if ((uint64_t)r->x0 + r->width > cam->image_width || (uint64_t)r->y0 + r->height > cam->image_height)
+        return fail(RTX_ERR_INVALID_ARG, "region [%u+%u, %u+%u] outside %ux%u image", r->x0, r->width, r->y0, r->height,
+                    cam->image_width, cam->image_height);
+    return RTX_OK;
+}
+
+uint32_t region_rows(const rtx_region* r) {
+    if (r->world == 0 || r->rank >= r->world || r->height <= r->rank) return 0;
+    return (r->height - r->rank + r->world - 1) / r->world;
+}
+
+rtxd::Params make_params(const rtx_scene* s, const DeviceCopy* c, const rtx_camera* cam, uint64_t seed,
+                         const rtx_region* r, float* d_out) {
+    rtxd::Params p;
+    std::memset(&p, 0, sizeof(p));
+    p.entries = reinterpret_cast<const float4*>(c->entries);
+    p.n_entries = (uint32_t)s->entries.size();
+    p.n_materials = (uint32_t)s->materials.size();
+    p.materials = c->materials;
+    p.textures = c->textures;
+    p.texels = c->texels;
+    p.cam = *cam;
+    p.seed = seed;
+    p.x0 = r->x0;
+    p.y0 = r->y0;
+    p.width = r->width;
+    p.rows = region_rows(r);
+    p.rank = r->rank;
+    p.world = r->world;
+    p.out = d_out;
+    p.counters = c->counters;
+    return p;
+}
+
+// Enqueue one region on the current device, bracketed by HIP events on `stream`.
+int enqueue_on(rtx_scene* s, DeviceCopy* c, const rtx_camera* cam, uint64_t seed, const rtx_region* r, float* d_out,
+               hipStream_t stream, bool count, bool timed) {
+    rtxd::Params p = make_params(s, c, cam, seed, r, d_out);
+    if (count) HIP_TRY(hipMemsetAsync(c->counters, 0, 8 * sizeof(unsigned long long), stream));
+    if (timed) HIP_TRY(hipEventRecord(c->ev0, stream));
+    HIP_TRY(rtxd::launch_render(p, count, stream));
+    if (timed) HIP_TRY(hipEventRecord(c->ev1, stream));
+    return RTX_OK;
+}
+
+// Wait for an enqueue_on(timed=true) and read its time and counters.
+int collect_on(DeviceCopy* c, bool count, uint64_t samples, rtx_stats* st) {
+    HIP_TRY(hipEventSynchronize(c->ev1));
+    float ms = 0.0f;
+    HIP_TRY(hipEventElapsedTime(&ms, c->ev0, c->ev1));
+    unsigned long long h[8] = {0};
+    if (count) HIP_TRY(hipMemcpy(h, c->counters, 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    std::memset(st, 0, sizeof(*st));
+    st->samples = count ? h[0] : samples;
+    st->segments = h[1];
+    st->node_visits = h[2];
+    st->prim_tests = h[3];
+    st->hits = h[4];
+    st->texel_fetches = h[5];
+    st->rng_draws = h[6];
+    st->kernel_ms = ms;
+    return RTX_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int rtx_version(void) { return RTX_ABI_VERSION; }
+
+const char* rtx_build_info(void) {
+    return "librtx gfx950 megakernel v0 (thread-per-pixel, threaded pre-order BVH); built " __DATE__ " " __TIME__;
+}
+
+const char* rtx_last_error(void) { return g_last_error.c_str(); }
+
+int rtx_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+uint32_t rtx_region_rows(const rtx_region* region) { return region ? region_rows(region) : 0; }
+
+int rtx_scene_create(const rtx_scene_desc* d, rtx_scene** out) {
+    g_last_error.clear();
+    if (!d || !out) return fail(RTX_ERR_INVALID_ARG, "NULL argument");
+    *out = nullptr;
+    if (d->n_roots == 0 || !d->roots) return fail(RTX_ERR_INVALID_ARG, "scene has no root");
+    if (d->n_nodes && !d->nodes) return fail(RTX_ERR_INVALID_ARG, "nodes is NULL");
+    if (d->n_spheres && !d->spheres) return fail(RTX_ERR_INVALID_ARG, "spheres is NULL");
+    if (d->n_materials && !d->materials) return fail(RTX_ERR_INVALID_ARG, "materials is NULL");
+    if (d->n_textures && !d->textures) return fail(RTX_ERR_INVALID_ARG, "textures is NULL");
+    if (d->n_texels && !d->texels) return fail(RTX_ERR_INVALID_ARG, "texels is NULL");
+    if (d->n_quads) return fail(RTX_ERR_UNSUPPORTED, "Quad primitives are not on the GPU path yet (hittables.go:138-216)");
+    for (uint32_t i = 0; i < d->n_spheres; ++i)
+        if (d->spheres[i].material >= d->n_materials)
+            return fail(RTX_ERR_INVALID_ARG, "sphere %u material %u out of range", i, d->spheres[i].material);
+    for (uint32_t i = 0; i < d->n_materials; ++i) {
+        const rtx_material& m = d->materials[i];
+        if (m.type > RTX_MAT_DIFFUSE_LIGHT) return fail(RTX_ERR_INVALID_ARG, "material %u: unknown type %u", i, m.type);
+        if ((m.type == RTX_MAT_LAMBERTIAN || m.type == RTX_MAT_DIFFUSE_LIGHT) && m.texture >= d->n_textures)
+            return fail(RTX_ERR_INVALID_ARG, "material %u texture %u out of range", i, m.texture);
+    }
+    for (uint32_t i = 0; i < d->n_textures; ++i) {
+        const rtx_texture& t = d->textures[i];
+        if (t.type == RTX_TEX_NOISE)
+            return fail(RTX_ERR_UNSUPPORTED, "NoiseTexture (Perlin, materials.go:195-295) is not on the GPU path");
+        if (t.type > RTX_TEX_NOISE) return fail(RTX_ERR_INVALID_ARG, "texture %u: unknown type %u", i, t.type);
+        if (t.type == RTX_TEX_IMAGE && (int32_t)t.height > 0 &&
+            (uint64_t)t.texel_offset + (uint64_t)t.width * t.height > d->n_texels)
+            return fail(RTX_ERR_INVALID_ARG, "texture %u texels out of range", i);
+    }
+    if (int rc = check_acyclic(d)) return rc;
+    rtx_scene* s = new rtx_scene();
+    for (uint32_t i = 0; i < d->n_roots; ++i) {
+        if (int rc = emit(d, d->roots[i], s->entries)) {
+            delete s;
+            return rc;
+        }
+    }
+    s->materials.assign(d->materials, d->materials + d->n_materials);
+    s->textures.assign(d->textures, d->textures + d->n_textures);
+    if (d->n_texels) s->texels.assign(d->texels, d->texels + d->n_texels);
+    int cur = 0;
+    if (hipGetDevice(&cur) != hipSuccess) {
+        delete s;
+        return fail(RTX_ERR_NO_DEVICE, "no HIP device");
+    }
+    DeviceCopy* c = nullptr;
+    if (int rc = ensure_device(s, cur, &c)) {
+        for (auto& kv : s->copies) free_copy(kv.second);
+        delete s;
+        return rc;
+    }
+    *out = s;
+    return RTX_OK;
+}
+
+void rtx_scene_destroy(rtx_scene* s) {
+    if (!s) return;
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    for (auto& kv : s->copies) free_copy(kv.second);
+    (void)hipSetDevice(cur);
+    delete s;
+}
+
+uint64_t rtx_scene_device_bytes(const rtx_scene* s) {
+    if (!s) return 0;
+    return s->entries.size() * sizeof(rtx_entry) + s->materials.size() * sizeof(rtx_material) +
+           s->textures.size() * sizeof(rtx_texture) + s->texels.size() * sizeof(uint32_t);
+}
+
+int rtx_render_region_device(rtx_scene* s, const rtx_camera* cam, uint64_t seed, const rtx_region* region,
+                             float* d_out, void* hip_stream, uint32_t flags, rtx_stats* stats) {
+    g_last_error.clear();
+    if (!s || !d_out) return fail(RTX_ERR_INVALID_ARG, "NULL argument");
+    if (int rc = check_camera(cam)) return rc;
+    if (int rc = check_region(cam, region)) return rc;
+    std::lock_guard<std::mutex> lk(s->mu);
+    int cur = 0;
+    HIP_TRY(hipGetDevice(&cur));
+    DeviceCopy* c = nullptr;
+    if (int rc = ensure_device(s, cur, &c)) return rc;
+    HIP_TRY(hipSetDevice(cur));
+    const bool count = (flags & RTX_FLAG_COUNTERS) != 0;
+    if (int rc = enqueue_on(s, c, cam, seed, region, d_out, (hipStream_t)hip_stream, count, stats != nullptr)) return rc;
+    if (!stats) return RTX_OK;
+    return collect_on(c, count, (uint64_t)region_rows(region) * region->width * cam->samples_per_pixel, stats);
+}
+
+int rtx_render(rtx_scene* s, const rtx_camera* cam, uint64_t seed, int n_gpus, float* out_rgb, rtx_stats* stats) {
+    g_last_error.clear();
+    if (!s || !out_rgb) return fail(RTX_ERR_INVALID_ARG, "NULL argument");
+    if (int rc = check_camera(cam)) return rc;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(RTX_ERR_NO_DEVICE, "no HIP device");
+    if (n_gpus <= 0) n_gpus = 1;
+    if (n_gpus > ndev) return fail(RTX_ERR_INVALID_ARG, "n_gpus=%d but %d devices visible", n_gpus, ndev);
+    if ((uint32_t)n_gpus > cam->image_height) n_gpus = (int)cam->image_height;
+    std::lock_guard<std::mutex> lk(s->mu);
+    int cur = 0;
+    HIP_TRY(hipGetDevice(&cur));
+    const uint32_t W = cam->image_width, H = cam->image_height;
+    std::vector<float*> bufs(n_gpus, nullptr);
+    std::vector<hipStream_t> streams(n_gpus, nullptr);
+    std::vector<rtx_region> regs(n_gpus);
+    std::vector<rtx_stats> sts(n_gpus);
+    int rc = RTX_OK;
+    // Each device renders a row-interleaved band (rows y % n == d) of the full image.
+    for (int d = 0; d < n_gpus && rc == RTX_OK; ++d) {
+        DeviceCopy* c = nullptr;
+        if ((rc = ensure_device(s, d, &c))) break;
+        if (hipSetDevice(d) != hipSuccess) { rc = fail(RTX_ERR_HIP, "hipSetDevice(%d)", d); break; }
+        regs[d] = rtx_region{0, 0, W, H, (uint32_t)d, (uint32_t)n_gpus};
+        const size_t bytes = (size_t)region_rows(&regs[d]) * W * 3 * sizeof(float);
+        if (hipStreamCreateWithFlags(&streams[d], hipStreamNonBlocking) != hipSuccess) { rc = fail(RTX_ERR_HIP, "stream"); break; }
+        if (hipMalloc(&bufs[d], std::max<size_t>(bytes, 4)) != hipSuccess) { rc = fail(RTX_ERR_OOM, "hipMalloc %zu", bytes); break; }
+        rc = enqueue_on(s, c, cam, seed, &regs[d], bufs[d], streams[d], stats != nullptr, true);
+    }
+    // All devices run concurrently; collect after every launch is enqueued.
+    for (int d = 0; d < n_gpus && rc == RTX_OK && stats; ++d) {
+        if (hipSetDevice(d) != hipSuccess) { rc = fail(RTX_ERR_HIP, "hipSetDevice(%d)", d); break; }
+        rc = collect_on(&s->copies[d], true, 0, &sts[d]);
+    }
+    // Bands -> host rows y = d + r * n (strided copy de-interleaves them).
+    for (int d = 0; d < n_gpus && rc == RTX_OK; ++d) {
+        if (hipSetDevice(d) != hipSuccess) { rc = fail(RTX_ERR_HIP, "hipSetDevice(%d)", d); break; }
+        const uint32_t rows = region_rows(&regs[d]);
+        if (rows == 0) continue;
+        hipError_t e = hipMemcpy2DAsync(out_rgb + (size_t)d * W * 3, (size_t)n_gpus * W * 3 * sizeof(float), bufs[d],
+                                        (size_t)W * 3 * sizeof(float), (size_t)W * 3 * sizeof(float), rows,
+                                        hipMemcpyDeviceToHost, streams[d]);
+        if (e == hipSuccess) e = hipStreamSynchronize(streams[d]);
+        if (e != hipSuccess) rc = fail(RTX_ERR_HIP, "copy band %d: %s", d, hipGetErrorString(e));
+    }
+    for (int d = 0; d < n_gpus; ++d) {
+        if (hipSetDevice(d) != hipSuccess) continue;
+        if (streams[d]) (void)hipStreamSynchronize(streams[d]);
+        if (bufs[d]) (void)hipFree(bufs[d]);
+        if (streams[d]) (void)hipStreamDestroy(streams[d]);
+    }
+    (void)hipSetDevice(cur);
+    if (rc == RTX_OK && stats) {
+        std::memset(stats, 0, sizeof(*stats));
+        for (int d = 0; d < n_gpus; ++d) {
+            stats->samples += sts[d].samples;
+            stats->segments += sts[d].segments;
+            stats->node_visits += sts[d].node_visits;
+            stats->prim_tests += sts[d].prim_tests;
+            stats->hits += sts[d].hits;
+            stats->texel_fetches += sts[d].texel_fetches;
+            stats->rng_draws += sts[d].rng_draws;
+            stats->kernel_ms = std::max(stats->kernel_ms, sts[d].kernel_ms);
+        }
+    }
+    return rc;
+}
+
+}  // extern "C"

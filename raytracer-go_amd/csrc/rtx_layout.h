@@ -1,0 +1,33 @@
+// rtx_layout.h — device layout of a scene (library-internal; not part of the ABI).
+//
+// The reference walks a pointer tree recursively on every ray (bvh.go:220-249):
+// box test, left child, right child clipped to the left hit.  That visit order is a
+// pre-order depth-first walk with a running "closest" bound.  On the device the tree
+// is stored as that walk, "threaded": one 32-B entry per node / primitive in
+// pre-order, and every node carries its escape index (the entry after its subtree).
+//
+//   node box hit  -> next = i + 1          (descend: first child in pre-order)
+//   node box miss -> next = escape         (skip the subtree)
+//   primitive     -> test, next = i + 1
+//
+// So traversal needs no stack at all and visits exactly the reference's sequence
+// of box and primitive tests with the same running bound — the results are
+// bit-identical to the recursion, including ties (left before right).  The one
+// deliberate difference: a one-element split stores left == right (bvh.go:162-165);
+// its second test can never succeed (open interval clipped to the first hit, or an
+// identical miss), so that primitive is emitted once.
+//
+// Entry (two float4 = 32 B, 16-B aligned; loads are 2 x global/ds 128-bit):
+//   node:   a = (bmin.x, bmin.y, bmin.z, int escape)   b = (bmax.x, bmax.y, bmax.z, int RTX_E_NODE)
+//   sphere: a = (c.x, c.y, c.z, radius)                b = (radius*radius, int sphere, 0, int material >= 0)
+// radius*radius is the float32 product hittables.go:100 computes, precomputed.
+#pragma once
+#include <stdint.h>
+
+#define RTX_E_NODE (-1)
+
+struct rtx_entry {
+    float a[4];
+    float b[4];
+};
+static_assert(sizeof(rtx_entry) == 32, "entry is 32 B");

@@ -1,0 +1,179 @@
+// flatten.cpp — walk the Hittable tree by type switch into the rtx.h tables.
+//
+// This is the step a cgo Render performs before crossing the boundary:
+// *BVH -> node (bBox, left, right), *Sphere -> sphere, materials and textures by
+// identity (a shared material/texture is stored once).  Nodes are numbered in
+// pre-order (a node before its children, left before right), the order NewBVH
+// creates them in.  A World passed to Render gives one root per item (its linear
+// scan order, hittables.go:55-72).
+#include <unordered_map>
+
+#include "internal.h"
+
+namespace internal {
+
+namespace {
+
+struct Flattener {
+    FlatScene& fs;
+    std::unordered_map<const Hittable*, int32_t> refs;
+    std::unordered_map<const Material*, uint32_t> mats;
+    std::unordered_map<const Texture*, uint32_t> texs;
+    Error err;
+
+    explicit Flattener(FlatScene& f) : fs(f) {}
+
+    bool fail(int code, const std::string& msg) {
+        if (!err) err = Error{code, msg};
+        return false;
+    }
+
+    bool texture(const TexturePtr& t, uint32_t& out) {
+        if (!t) return fail(RTX_ERR_INVALID_ARG, "nil Texture");
+        auto it = texs.find(t.get());
+        if (it != texs.end()) { out = it->second; return true; }
+        rtx_texture r{};
+        if (auto s = dynamic_cast<const SolidColor*>(t.get())) {
+            r.type = RTX_TEX_SOLID;
+            r.even[0] = s->albedo.X; r.even[1] = s->albedo.Y; r.even[2] = s->albedo.Z;
+        } else if (auto c = dynamic_cast<const Checkered*>(t.get())) {
+            r.type = RTX_TEX_CHECKERED;
+            r.scale = c->scale;
+            r.even[0] = c->even.X; r.even[1] = c->even.Y; r.even[2] = c->even.Z;
+            r.odd[0] = c->odd.X; r.odd[1] = c->odd.Y; r.odd[2] = c->odd.Z;
+        } else if (auto im = dynamic_cast<const ImageTexture*>(t.get())) {
+            r.type = RTX_TEX_IMAGE;
+            const Image* img = im->img.get();
+            r.width = img ? (uint32_t)std::max(img->W, 0) : 0u;
+            r.height = img ? (uint32_t)std::max(img->H, 0) : 0u;
+            r.texel_offset = (uint32_t)fs.texels.size();
+            if (img && img->W > 0 && img->H > 0) {
+                if (img->rgba.size() != (size_t)img->W * img->H) return fail(RTX_ERR_INVALID_ARG, "image size mismatch");
+                fs.texels.insert(fs.texels.end(), img->rgba.begin(), img->rgba.end());
+            }
+        } else if (dynamic_cast<const NoiseTexture*>(t.get())) {
+            return fail(RTX_ERR_UNSUPPORTED, "NoiseTexture (Perlin, materials.go:195-295) is not on the GPU path");
+        } else {
+            return fail(RTX_ERR_UNSUPPORTED, "unknown Texture type");
+        }
+        out = (uint32_t)fs.textures.size();
+        fs.textures.push_back(r);
+        texs[t.get()] = out;
+        return true;
+    }
+
+    bool material(const MaterialPtr& m, uint32_t& out) {
+        if (!m) return fail(RTX_ERR_INVALID_ARG, "nil Material");
+        auto it = mats.find(m.get());
+        if (it != mats.end()) { out = it->second; return true; }
+        rtx_material r{};
+        if (auto l = dynamic_cast<const Lambertian*>(m.get())) {
+            r.type = RTX_MAT_LAMBERTIAN;
+            if (!texture(l->albedo, r.texture)) return false;
+        } else if (auto me = dynamic_cast<const Metal*>(m.get())) {
+            r.type = RTX_MAT_METAL;
+            r.albedo[0] = me->albedo.X; r.albedo[1] = me->albedo.Y; r.albedo[2] = me->albedo.Z;
+            r.fuzz = me->fuzz;
+        } else if (auto d = dynamic_cast<const Dielectric*>(m.get())) {
+            r.type = RTX_MAT_DIELECTRIC;
+            r.ior = d->refractiveIndex;
+        } else if (auto dl = dynamic_cast<const DiffuseLight*>(m.get())) {
+            r.type = RTX_MAT_DIFFUSE_LIGHT;
+            if (!texture(dl->emit, r.texture)) return false;
+        } else {
+            return fail(RTX_ERR_UNSUPPORTED, "unknown Material type");
+        }
+        out = (uint32_t)fs.materials.size();
+        fs.materials.push_back(r);
+        mats[m.get()] = out;
+        return true;
+    }
+
+    // Iterative pre-order walk (trees of 1e5+ spheres are ~17 deep, but a hand-built
+    // chain could be deep).
+    bool ref(const HittablePtr& root, int32_t& out) {
+        // child slots live in fs.nodes, which may reallocate: patch through indices
+        struct Patch {
+            int32_t node;
+            int side;  // 0 left, 1 right, -1 external slot
+            int32_t* ext;
+        };
+        std::vector<std::pair<const Hittable*, Patch>> stack{{root.get(), Patch{-1, -1, &out}}};
+        while (!stack.empty()) {
+            auto [h, patch] = stack.back();
+            stack.pop_back();
+            int32_t r;
+            if (!h) return fail(RTX_ERR_INVALID_ARG, "nil Hittable");
+            auto it = refs.find(h);
+            if (it != refs.end()) {
+                r = it->second;
+            } else if (auto b = dynamic_cast<const BVH*>(h)) {
+                r = (int32_t)fs.nodes.size();
+                rtx_bvh_node n{};
+                n.bmin[0] = b->bBox.x.min; n.bmin[1] = b->bBox.y.min; n.bmin[2] = b->bBox.z.min;
+                n.bmax[0] = b->bBox.x.max; n.bmax[1] = b->bBox.y.max; n.bmax[2] = b->bBox.z.max;
+                fs.nodes.push_back(n);
+                refs[h] = r;
+                stack.push_back({b->right.get(), Patch{r, 1, nullptr}});
+                stack.push_back({b->left.get(), Patch{r, 0, nullptr}});
+            } else if (auto s = dynamic_cast<const Sphere*>(h)) {
+                rtx_sphere sp{};
+                sp.center[0] = s->Center.X; sp.center[1] = s->Center.Y; sp.center[2] = s->Center.Z;
+                sp.radius = s->Radius;
+                if (!material(s->Mat, sp.material)) return false;
+                r = RTX_REF_PRIM(RTX_PRIM_SPHERE, fs.spheres.size());
+                fs.spheres.push_back(sp);
+                refs[h] = r;
+            } else if (dynamic_cast<const Quad*>(h)) {
+                return fail(RTX_ERR_UNSUPPORTED, "Quad primitives are not on the GPU path yet (hittables.go:138-216)");
+            } else if (dynamic_cast<const World*>(h)) {
+                return fail(RTX_ERR_UNSUPPORTED, "a World nested inside a BVH is not on the GPU path");
+            } else {
+                return fail(RTX_ERR_UNSUPPORTED, "unknown Hittable type");
+            }
+            if (patch.side < 0) *patch.ext = r;
+            else if (patch.side == 0) fs.nodes[patch.node].left = r;
+            else fs.nodes[patch.node].right = r;
+        }
+        return true;
+    }
+};
+
+}  // namespace
+
+Error Flatten(const HittablePtr& world, FlatScene& fs) {
+    fs = FlatScene{};
+    if (!world) return Error{RTX_ERR_INVALID_ARG, "nil world"};
+    Flattener f(fs);
+    if (auto w = dynamic_cast<const World*>(world.get())) {
+        for (const auto& h : w->hittables) {
+            int32_t r = 0;
+            if (!f.ref(h, r)) return f.err;
+            fs.roots.push_back(r);
+        }
+        if (fs.roots.empty()) return Error{RTX_ERR_INVALID_ARG, "empty World"};
+    } else {
+        int32_t r = 0;
+        if (!f.ref(world, r)) return f.err;
+        fs.roots.push_back(r);
+    }
+    rtx_scene_desc& d = fs.desc;
+    d = rtx_scene_desc{};
+    d.nodes = fs.nodes.data();
+    d.n_nodes = (uint32_t)fs.nodes.size();
+    d.roots = fs.roots.data();
+    d.n_roots = (uint32_t)fs.roots.size();
+    d.spheres = fs.spheres.data();
+    d.n_spheres = (uint32_t)fs.spheres.size();
+    d.quads = fs.quads.data();
+    d.n_quads = (uint32_t)fs.quads.size();
+    d.materials = fs.materials.data();
+    d.n_materials = (uint32_t)fs.materials.size();
+    d.textures = fs.textures.data();
+    d.n_textures = (uint32_t)fs.textures.size();
+    d.texels = fs.texels.data();
+    d.n_texels = fs.texels.size();
+    return Error{};
+}
+
+}  // namespace internal

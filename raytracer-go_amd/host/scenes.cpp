@@ -1,0 +1,174 @@
+// scenes.cpp — main.go scene builders restated over the seeded streams.
+#include "scenes.h"
+
+#include <cmath>
+
+namespace internal {
+
+namespace {
+
+std::vector<CameraOpt> rand_spheres_camera() {  // main.go:228-239
+    return {WithSamplesPerPixel(500),
+            WithMaxRayDepth(50),
+            WithLookFrom(NewVec3(13, 2, 3)),
+            WithLookAt(NewVec3(0, 0, 0)),
+            WithFOVDegrees(20),
+            WithDefocusAngleDegrees(0.6f),
+            WithFocusDist(10),
+            WithBackgroundColor(NewVec3(0.7f, 0.8f, 1))};
+}
+
+MaterialPtr checkered_ground() {  // main.go:242-243
+    auto checkered = NewCheckered(0.32f, NewVec3(0.2f, 0.3f, 0.1f), NewVec3(0.9f, 0.9f, 0.9f));
+    return NewLambertian(checkered);
+}
+
+// The material draw of main.go:258-270 with configurable thresholds.
+MaterialPtr random_material(Rand& randCtx, float matPer, float lamb, float metal) {
+    if (matPer < lamb) {
+        const Vec3 a = NewVec3Rand32(randCtx);
+        const Vec3 b = NewVec3Rand32(randCtx);
+        const Vec3 randCol = Mul(a, b);
+        return NewLambertian(NewSolidColor(randCol.X, randCol.Y, randCol.Z));
+    }
+    if (matPer < metal) {
+        const Vec3 albedo = NewVec3RandRange32(randCtx, 0.5f, 1);
+        const float fuzz = RandF32N(randCtx, 0, 0.5f);
+        return NewMetal(albedo, fuzz);
+    }
+    return NewDielectric(1.5f);
+}
+
+void grid_spheres(World& world, Rand& randCtx, float lamb, float metal) {  // main.go:248-276
+    Rand& g = GlobalRand();
+    const Vec3 p = NewVec3(4, 0.2f, 0);
+    for (int i = -11; i < 11; ++i) {
+        for (int j = -11; j < 11; ++j) {
+            const float matPer = g.Float32();
+            const float cx = (float)i + 0.9f * g.Float32();
+            const float cz = (float)j + 0.9f * g.Float32();
+            const Vec3 center = NewVec3(cx, 0.2f, cz);
+            const Vec3 dist = Sub(center, p);
+            const float ln = dist.Len();
+            if (ln > 0.9f) world.Add(NewSphere(center, 0.2f, random_material(randCtx, matPer, lamb, metal)));
+        }
+    }
+}
+
+}  // namespace
+
+SceneSpec RandSpheres(uint64_t seed) {
+    SceneSpec s;
+    s.name = "random_spheres";
+    s.opts = rand_spheres_camera();
+    Seed(seed);                       // rand.Float32() / rand.Intn global source
+    auto randCtx = NewRand(seed);     // main.go:246-247
+    auto world = NewWorld();
+    world->Add(NewSphere(NewVec3(0, -1000, 0), 1000, checkered_ground()));  // :244
+    grid_spheres(*world, *randCtx, 0.8f, 0.95f);
+    world->Add(NewSphere(NewVec3(0, 1, 0), 1, NewDielectric(1.5f)));                         // :278-279
+    world->Add(NewSphere(NewVec3(-4, 1, 0), 1, NewLambertian(NewSolidColor(0.4f, 0.2f, 0.1f))));  // :281-282
+    world->Add(NewSphere(NewVec3(4, 1, 0), 1, NewMetal(NewVec3(0.7f, 0.6f, 0.5f), 0)));      // :284-285
+    s.world = NewBVHFromWorld(*world);                                                        // :287
+    return s;
+}
+
+SceneSpec StressSpheres(uint64_t seed, int n) {
+    SceneSpec s;
+    s.name = "stress_100k";
+    s.opts = rand_spheres_camera();
+    s.opts[0] = WithSamplesPerPixel(100);
+    Seed(seed);
+    auto randCtx = NewRand(seed);
+    auto world = NewWorld();
+    world->Add(NewSphere(NewVec3(0, -1000, 0), 1000, checkered_ground()));
+    Rand& g = GlobalRand();
+    for (int k = 0; k < n; ++k) {
+        const float matPer = g.Float32();
+        const float cx = -158.0f + 316.0f * g.Float32();
+        const float cz = -158.0f + 316.0f * g.Float32();
+        world->Add(NewSphere(NewVec3(cx, 0.2f, cz), 0.2f, random_material(*randCtx, matPer, 0.8f, 0.95f)));
+    }
+    s.world = NewBVHFromWorld(*world);
+    return s;
+}
+
+ImagePtr SyntheticEarth(uint64_t seed, int w, int h) {
+    auto img = std::make_shared<Image>();
+    img->W = w;
+    img->H = h;
+    img->rgba.resize((size_t)w * h);
+    Rand r(seed, kStreamTexture);
+    // A few seeded low-frequency waves decide land vs ocean; a per-texel draw adds grain.
+    float ph[6];
+    for (float& v : ph) v = 6.2831853f * r.Float32();
+    for (int y = 0; y < h; ++y) {
+        const float lat = ((float)y + 0.5f) / (float)h;  // 0 top .. 1 bottom
+        for (int x = 0; x < w; ++x) {
+            const float lon = ((float)x + 0.5f) / (float)w;
+            const float a = std::sin(6.2831853f * 2.0f * lon + ph[0]) * std::sin(3.1415927f * 3.0f * lat + ph[1]);
+            const float b = 0.5f * std::sin(6.2831853f * 5.0f * lon + ph[2]) * std::cos(3.1415927f * 4.0f * lat + ph[3]);
+            const float c = 0.25f * std::sin(6.2831853f * 11.0f * lon + ph[4] + 3.0f * lat + ph[5]);
+            const float land = a + b + c;
+            const uint32_t grain = r.Uint32() & 31u;
+            uint32_t R, G, B;
+            if (lat < 0.07f || lat > 0.93f) {  // ice caps
+                R = 225 + (grain & 15); G = 230 + (grain & 15); B = 240 + (grain & 15);
+            } else if (land > 0.35f) {         // land
+                R = 70 + grain * 2; G = 110 + grain; B = 40 + grain;
+            } else {                           // ocean
+                R = 10 + grain / 2; G = 40 + grain; B = 120 + grain * 2;
+            }
+            img->rgba[(size_t)y * w + x] = R | (G << 8) | (B << 16) | (255u << 24);
+        }
+    }
+    return img;
+}
+
+SceneSpec EarthDielectric(uint64_t seed, int tex_w, int tex_h) {
+    SceneSpec s;
+    s.name = "earth_dielectric";
+    s.opts = rand_spheres_camera();
+    s.opts[0] = WithSamplesPerPixel(1000);
+    s.width = 3840;
+    Seed(seed);
+    auto randCtx = NewRand(seed);
+    auto world = NewWorld();
+    world->Add(NewSphere(NewVec3(0, -1000, 0), 1000, checkered_ground()));
+    grid_spheres(*world, *randCtx, 0.45f, 0.65f);
+    auto earth = NewLambertian(NewImageTexture(SyntheticEarth(seed, tex_w, tex_h)));
+    world->Add(NewSphere(NewVec3(0, 1, 0), 1, earth));
+    world->Add(NewSphere(NewVec3(-4, 1, 0), 1, NewDielectric(1.5f)));
+    world->Add(NewSphere(NewVec3(4, 1, 0), 1, NewMetal(NewVec3(0.7f, 0.6f, 0.5f), 0)));
+    s.world = NewBVHFromWorld(*world);
+    return s;
+}
+
+SceneSpec Earth(uint64_t seed, int tex_w, int tex_h) {  // main.go:80-104
+    SceneSpec s;
+    s.name = "earth";
+    s.opts = {WithSamplesPerPixel(100),
+              WithMaxRayDepth(50),
+              WithLookFrom(NewVec3(0, 0, 12)),
+              WithLookAt(NewVec3(0, 0, 0)),
+              WithFOVDegrees(20),
+              WithDefocusAngleDegrees(0),
+              WithBackgroundColor(NewVec3(0.7f, 0.8f, 1))};
+    Seed(seed);
+    auto world = NewWorld();
+    auto mat = NewLambertian(NewImageTexture(SyntheticEarth(seed, tex_w, tex_h)));
+    world->Add(NewSphere(NewVec3(0, 0, 0), 2, mat));
+    s.world = NewBVHFromWorld(*world);
+    return s;
+}
+
+bool BuildScene(const std::string& name, uint64_t seed, SceneSpec& out) {
+    if (name == "random_spheres") out = RandSpheres(seed);
+    else if (name == "stress_100k") out = StressSpheres(seed, 100000);
+    else if (name == "earth_dielectric") out = EarthDielectric(seed, 2048, 1024);
+    else if (name == "earth") out = Earth(seed, 2048, 1024);
+    else return false;
+    return true;
+}
+
+}  // namespace internal

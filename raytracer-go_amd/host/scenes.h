@@ -1,0 +1,37 @@
+// scenes.h — the scene builders of main.go (and the BASELINE configs built from them),
+// restated with seeded streams instead of time-seeded math/rand.
+#pragma once
+#include <string>
+#include <vector>
+
+#include "internal.h"
+
+namespace internal {
+
+struct SceneSpec {
+    std::string name;
+    HittablePtr world;  // what main.go passes to camera.Render (a *BVH)
+    float aspect = 16.0f / 9.0f;
+    int width = 400;
+    std::vector<CameraOpt> opts;  // NewCamera options as main.go sets them
+};
+
+// randSpheres, main.go:227-289 — the north-star scene (configs 1-3).
+SceneSpec RandSpheres(uint64_t seed);
+// Config 4: 100 000 r=0.2 spheres, centres uniform on the y=0.2 plane over
+// [-158,158)^2 (the randSpheres grid density), materials 80/15/5 as main.go:258-270,
+// plus the checkered ground sphere; randSpheres camera.
+SceneSpec StressSpheres(uint64_t seed, int n);
+// Config 5: randSpheres layout with a Dielectric-heavy mix (45/20/35), the centre
+// sphere Lambertian(ImageTexture(synthetic 2048x1024 earth)), defocus 0.6 / focus 10.
+SceneSpec EarthDielectric(uint64_t seed, int tex_w, int tex_h);
+// earth, main.go:80-104, with a synthetic texture standing in for the missing
+// textures/earthmap.jpg (.MISSING_LARGE_BLOBS:2).
+SceneSpec Earth(uint64_t seed, int tex_w, int tex_h);
+// A seeded RGBA8 "earth-like" raster (oceans, continents, ice caps).
+ImagePtr SyntheticEarth(uint64_t seed, int w, int h);
+
+// By name: "random_spheres", "stress_100k", "earth_dielectric", "earth".
+bool BuildScene(const std::string& name, uint64_t seed, SceneSpec& out);
+
+}  // namespace internal

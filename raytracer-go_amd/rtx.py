@@ -1,0 +1,272 @@
+"""ctypes binding of librtx.so (include/rtx.h) and librtxhost.so (include/rtx_host.h).
+
+This is plumbing for the Python test driver and bench.py — the drop-in boundary
+itself is the C-ABI (a Go host binds it via cgo).  Loading fails
+loudly if the native libraries are missing: there is no CPU fallback for the product
+path.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, c_char_p, c_double, c_float, c_int, c_int32, c_uint32, c_uint64, c_void_p
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+RTX_OK = 0
+RTX_ERR_INVALID_ARG = -1
+RTX_ERR_HIP = -2
+RTX_ERR_RCCL = -3
+RTX_ERR_UNSUPPORTED = -4
+RTX_ERR_NO_DEVICE = -5
+RTX_ERR_OOM = -6
+
+RTX_PRIM_SPHERE = 0
+RTX_PRIM_QUAD = 1
+RTX_MAT_LAMBERTIAN, RTX_MAT_METAL, RTX_MAT_DIELECTRIC, RTX_MAT_DIFFUSE_LIGHT = 0, 1, 2, 3
+RTX_TEX_SOLID, RTX_TEX_CHECKERED, RTX_TEX_IMAGE, RTX_TEX_NOISE = 0, 1, 2, 3
+RTX_FLAG_COUNTERS = 1
+
+
+def ref_prim(ptype: int, index: int) -> int:
+    """RTX_REF_PRIM: ~((type << 28) | index) as int32."""
+    v = ((ptype << 28) | (index & 0x0FFFFFFF)) & 0xFFFFFFFF
+    return ~v if v < 0x80000000 else ~(v - (1 << 32))
+
+
+class BvhNode(ctypes.Structure):
+    _fields_ = [("bmin", c_float * 3), ("left", c_int32), ("bmax", c_float * 3), ("right", c_int32)]
+
+
+class Sphere(ctypes.Structure):
+    _fields_ = [("center", c_float * 3), ("radius", c_float), ("material", c_uint32), ("pad", c_uint32 * 3)]
+
+
+class Quad(ctypes.Structure):
+    _fields_ = [("q", c_float * 3), ("material", c_uint32), ("u", c_float * 3), ("d", c_float),
+                ("v", c_float * 3), ("pad0", c_float), ("w", c_float * 3), ("pad1", c_float),
+                ("normal", c_float * 3), ("pad2", c_float)]
+
+
+class Material(ctypes.Structure):
+    _fields_ = [("type", c_uint32), ("texture", c_uint32), ("fuzz", c_float), ("ior", c_float),
+                ("albedo", c_float * 3), ("pad", c_float)]
+
+
+class Texture(ctypes.Structure):
+    _fields_ = [("type", c_uint32), ("scale", c_float), ("width", c_uint32), ("height", c_uint32),
+                ("even", c_float * 3), ("texel_offset", c_uint32), ("odd", c_float * 3), ("pad", c_float)]
+
+
+class SceneDesc(ctypes.Structure):
+    _fields_ = [("nodes", POINTER(BvhNode)), ("n_nodes", c_uint32), ("n_roots", c_uint32),
+                ("roots", POINTER(c_int32)), ("spheres", POINTER(Sphere)), ("n_spheres", c_uint32),
+                ("n_quads", c_uint32), ("quads", POINTER(Quad)), ("materials", POINTER(Material)),
+                ("n_materials", c_uint32), ("n_textures", c_uint32), ("textures", POINTER(Texture)),
+                ("texels", POINTER(c_uint32)), ("n_texels", c_uint64)]
+
+
+class Camera(ctypes.Structure):
+    _fields_ = [("image_width", c_uint32), ("image_height", c_uint32), ("samples_per_pixel", c_uint32),
+                ("max_depth", c_uint32), ("center", c_float * 3), ("defocus_angle", c_float),
+                ("pixel00", c_float * 3), ("pad0", c_float), ("pixel_du", c_float * 3), ("pad1", c_float),
+                ("pixel_dv", c_float * 3), ("pad2", c_float), ("defocus_disk_u", c_float * 3), ("pad3", c_float),
+                ("defocus_disk_v", c_float * 3), ("pad4", c_float), ("background", c_float * 3), ("pad5", c_float)]
+
+
+class Region(ctypes.Structure):
+    _fields_ = [("x0", c_uint32), ("y0", c_uint32), ("width", c_uint32), ("height", c_uint32),
+                ("rank", c_uint32), ("world", c_uint32)]
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [("samples", c_uint64), ("segments", c_uint64), ("node_visits", c_uint64),
+                ("prim_tests", c_uint64), ("hits", c_uint64), ("texel_fetches", c_uint64),
+                ("rng_draws", c_uint64), ("kernel_ms", c_double), ("gather_ms", c_double)]
+
+    def as_dict(self) -> dict:
+        return {name: getattr(self, name) for name, _ in self._fields_}
+
+
+RTX_SYMBOLS = [
+    "rtx_version", "rtx_build_info", "rtx_last_error", "rtx_device_count", "rtx_scene_create",
+    "rtx_scene_destroy", "rtx_scene_device_bytes", "rtx_render", "rtx_render_region_device", "rtx_region_rows",
+]
+RTXHOST_SYMBOLS = [
+    "rtxhost_build_scene", "rtxhost_scene_free", "rtxhost_scene_desc", "rtxhost_scene_camera",
+    "rtxhost_render_ppm", "rtxhost_ppm_encode", "rtxhost_last_error",
+]
+
+_lib = None
+_host = None
+
+
+def lib_path(name: str) -> str:
+    return os.path.join(HERE, name)
+
+
+def load() -> ctypes.CDLL:
+    """Load librtx.so (raises OSError if it was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    path = lib_path("librtx.so")
+    if not os.path.exists(path):
+        raise OSError(f"librtx.so not built at {path}: run __graft_entry__.build() (no CPU fallback exists)")
+    L = ctypes.CDLL(path)
+    L.rtx_version.restype = c_int
+    L.rtx_build_info.restype = c_char_p
+    L.rtx_last_error.restype = c_char_p
+    L.rtx_device_count.restype = c_int
+    L.rtx_scene_create.argtypes = [POINTER(SceneDesc), POINTER(c_void_p)]
+    L.rtx_scene_create.restype = c_int
+    L.rtx_scene_destroy.argtypes = [c_void_p]
+    L.rtx_scene_destroy.restype = None
+    L.rtx_scene_device_bytes.argtypes = [c_void_p]
+    L.rtx_scene_device_bytes.restype = c_uint64
+    L.rtx_render.argtypes = [c_void_p, POINTER(Camera), c_uint64, c_int, c_void_p, POINTER(Stats)]
+    L.rtx_render.restype = c_int
+    L.rtx_render_region_device.argtypes = [c_void_p, POINTER(Camera), c_uint64, POINTER(Region), c_void_p,
+                                           c_void_p, c_uint32, POINTER(Stats)]
+    L.rtx_render_region_device.restype = c_int
+    L.rtx_region_rows.argtypes = [POINTER(Region)]
+    L.rtx_region_rows.restype = c_uint32
+    _lib = L
+    return L
+
+
+def load_host() -> ctypes.CDLL:
+    global _host
+    if _host is not None:
+        return _host
+    load()
+    path = lib_path("librtxhost.so")
+    if not os.path.exists(path):
+        raise OSError(f"librtxhost.so not built at {path}")
+    H = ctypes.CDLL(path)
+    H.rtxhost_build_scene.argtypes = [c_char_p, c_uint64, POINTER(c_void_p)]
+    H.rtxhost_build_scene.restype = c_int
+    H.rtxhost_scene_free.argtypes = [c_void_p]
+    H.rtxhost_scene_free.restype = None
+    H.rtxhost_scene_desc.argtypes = [c_void_p]
+    H.rtxhost_scene_desc.restype = POINTER(SceneDesc)
+    H.rtxhost_scene_camera.argtypes = [c_void_p, c_int32, c_int32, c_int32, POINTER(Camera)]
+    H.rtxhost_scene_camera.restype = c_int
+    H.rtxhost_render_ppm.argtypes = [c_char_p, c_uint64, c_int32, c_int32, c_int32, c_uint64, c_int32, c_char_p]
+    H.rtxhost_render_ppm.restype = c_int
+    H.rtxhost_ppm_encode.argtypes = [c_void_p, c_uint32, c_uint32, c_void_p, c_uint64]
+    H.rtxhost_ppm_encode.restype = c_uint64
+    H.rtxhost_last_error.restype = c_char_p
+    _host = H
+    return H
+
+
+class RtxError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"rtx error {code}: {msg}")
+        self.code = code
+
+
+def check(rc: int, where: str = "rtx") -> None:
+    if rc != RTX_OK:
+        msg = load().rtx_last_error().decode()
+        raise RtxError(rc, f"{where}: {msg}")
+
+
+class HostScene:
+    """A main.go scene built by the C++ mirror (NewBVH + flatten)."""
+
+    def __init__(self, name: str, seed: int = 1):
+        H = load_host()
+        h = c_void_p()
+        rc = H.rtxhost_build_scene(name.encode(), seed, ctypes.byref(h))
+        if rc != RTX_OK:
+            raise RtxError(rc, H.rtxhost_last_error().decode())
+        self._h = h
+        self.name = name
+        self.seed = seed
+
+    @property
+    def desc(self):
+        return load_host().rtxhost_scene_desc(self._h)
+
+    def camera(self, width: int = 0, spp: int = 0, depth: int = 0) -> Camera:
+        cam = Camera()
+        rc = load_host().rtxhost_scene_camera(self._h, width, spp, depth, ctypes.byref(cam))
+        if rc != RTX_OK:
+            raise RtxError(rc, load_host().rtxhost_last_error().decode())
+        return cam
+
+    def close(self) -> None:
+        if self._h:
+            load_host().rtxhost_scene_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class DeviceScene:
+    """rtx_scene_create: the tables uploaded once to the current HIP device."""
+
+    def __init__(self, desc_ptr):
+        L = load()
+        h = c_void_p()
+        check(L.rtx_scene_create(desc_ptr, ctypes.byref(h)), "rtx_scene_create")
+        self._h = h
+
+    @property
+    def handle(self):
+        return self._h
+
+    def device_bytes(self) -> int:
+        return load().rtx_scene_device_bytes(self._h)
+
+    def render_region(self, cam: Camera, seed: int, region: Region, out_ptr: int, stream: int = 0,
+                      counters: bool = False, timed: bool = False):
+        """Enqueue (and optionally wait/time) a region render into device memory at out_ptr."""
+        st = Stats() if (timed or counters) else None
+        rc = load().rtx_render_region_device(self._h, ctypes.byref(cam), seed, ctypes.byref(region),
+                                             c_void_p(out_ptr), c_void_p(stream),
+                                             RTX_FLAG_COUNTERS if counters else 0,
+                                             ctypes.byref(st) if st is not None else None)
+        check(rc, "rtx_render_region_device")
+        return st
+
+    def render_host(self, cam: Camera, seed: int, n_gpus: int = 1, stats: bool = False):
+        import numpy as np
+        out = np.zeros((cam.image_height, cam.image_width, 3), dtype=np.float32)
+        st = Stats() if stats else None
+        rc = load().rtx_render(self._h, ctypes.byref(cam), seed, n_gpus, out.ctypes.data_as(c_void_p),
+                               ctypes.byref(st) if st is not None else None)
+        check(rc, "rtx_render")
+        return out, st
+
+    def close(self) -> None:
+        if self._h:
+            load().rtx_scene_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def region_rows(region: Region) -> int:
+    return int(load().rtx_region_rows(ctypes.byref(region)))
+
+
+def ppm_encode(rgb) -> bytes:
+    import numpy as np
+    a = np.ascontiguousarray(rgb, dtype=np.float32)
+    h, w = a.shape[0], a.shape[1]
+    H = load_host()
+    n = H.rtxhost_ppm_encode(a.ctypes.data_as(c_void_p), w, h, None, 0)
+    buf = ctypes.create_string_buffer(int(n))
+    H.rtxhost_ppm_encode(a.ctypes.data_as(c_void_p), w, h, buf, n)
+    return buf.raw[: int(n)]
