@@ -74,7 +74,7 @@ typedef struct rtx_sphere {
 } rtx_sphere;
 
 /* internal/hittables.go:138-165 (NewQuad) — derived fields as the constructor
- * computes them.  Reserved for the Quad/Box row.                  64 B */
+ * computes them.  Reserved for the Quad/Box row.                  80 B */
 typedef struct rtx_quad {
     float q[3];
     uint32_t material;
@@ -190,9 +190,23 @@ typedef struct rtx_stats {
     uint64_t rng_draws;
     double kernel_ms;      /* device time of the render kernel(s), HIP events       */
     double gather_ms;      /* multi-GPU gather (rtx_render with n_gpus > 1)         */
+    /* scheduling counters of the persistent kernels (RTX_FLAG_COUNTERS):            */
+    uint64_t wave_iters;   /* traversal-loop iterations, summed over waves           */
+    uint64_t lane_steps;   /* lanes stepping a BVH entry, summed over iterations     */
+    uint64_t shade_phases; /* shading phases, summed over waves                      */
+    uint64_t shade_lanes;  /* lanes shaded or claiming, summed over shading phases   */
 } rtx_stats;
 
 #define RTX_FLAG_COUNTERS 1u /* count work units (separate kernel instantiation) */
+#define RTX_FLAG_KERNEL_V0 2u /* A/B: the first thread-per-pixel kernel instead of the
+                                 persistent wave kernel (identical output) */
+#define RTX_FLAG_NO_LDS 4u    /* A/B: read the scene from global memory even if it fits LDS */
+#define RTX_FLAG_KERNEL_POOL 8u /* A/B: the pixel-pool persistent kernel (v2) instead of
+                                   the default one-pixel-per-lane wave kernel (v1) */
+#define RTX_FLAG_POOL4 16u      /* A/B: v2 with 4 instead of 2 pixel chunks per wave */
+/* Tuning: lanes of a wave that must wait before it shades (1..64; 0 = default, or the
+ * RTX_SHADE_THRESH environment variable). */
+#define RTX_FLAG_SHADE_THRESH(n) (((uint32_t)(n)&0x7Fu) << 8)
 
 typedef struct rtx_scene rtx_scene;
 

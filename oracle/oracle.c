@@ -97,6 +97,67 @@ static double go_pow5(double x) {
     return ldexp(a1, ae);
 }
 
+/* Go math.Atan2 / math.Acos (Go 1.21 src/math/atan.go, asin.go, atan2.go; pure Go on
+ * amd64: Cephes rational approximations, restated operation for operation). */
+static double go_xatan(double x) {
+    const double P0 = -8.750608600031904122785e-01, P1 = -1.615753718733365076637e+01,
+                 P2 = -7.500855792314704667340e+01, P3 = -1.228866684490136173410e+02,
+                 P4 = -6.485021904942025371773e+01, Q0 = +2.485846490142306297962e+01,
+                 Q1 = +1.650270098316988542046e+02, Q2 = +4.328810604912902668951e+02,
+                 Q3 = +4.853903996359136964868e+02, Q4 = +1.945506571482613964425e+02;
+    double z = x * x;
+    z = z * ((((P0 * z + P1) * z + P2) * z + P3) * z + P4) / (((((z + Q0) * z + Q1) * z + Q2) * z + Q3) * z + Q4);
+    z = x * z + x;
+    return z;
+}
+static double go_satan(double x) {
+    const double Morebits = 6.123233995736765886130e-17; /* pi/2 = PIO2 + Morebits */
+    const double Tan3pio8 = 2.41421356237309504880;      /* tan(3*pi/8) */
+    if (x <= 0.66) return go_xatan(x);
+    if (x > Tan3pio8) return 1.57079632679489661923 - go_xatan(1.0 / x) + Morebits;
+    return 0.785398163397448309616 + go_xatan((x - 1.0) / (x + 1.0)) + 0.5 * Morebits;
+}
+static double go_atan(double x) {
+    if (x == 0.0) return x;
+    if (x > 0.0) return go_satan(x);
+    return -go_satan(-x);
+}
+double oracle_go_atan2(double y, double x) {
+    const double Pi = 3.14159265358979323846;
+    if (isnan(y) || isnan(x)) return NAN;
+    if (y == 0.0) {
+        if (x >= 0.0 && !signbit(x)) return copysign(0.0, y);
+        return copysign(Pi, y);
+    }
+    if (x == 0.0) return copysign(Pi / 2.0, y);
+    if (isinf(x)) {
+        if (x > 0.0) return isinf(y) ? copysign(Pi / 4.0, y) : copysign(0.0, y);
+        return isinf(y) ? copysign(3.0 * Pi / 4.0, y) : copysign(Pi, y);
+    }
+    if (isinf(y)) return copysign(Pi / 2.0, y);
+    double q = go_atan(y / x);
+    if (x < 0.0) {
+        if (q <= 0.0) return q + Pi;
+        return q - Pi;
+    }
+    return q;
+}
+static double go_asin(double x) {
+    if (x == 0.0) return x;
+    int sign = 0;
+    if (x < 0.0) {
+        x = -x;
+        sign = 1;
+    }
+    if (x > 1.0) return NAN;
+    double temp = sqrt(1.0 - x * x);
+    if (x > 0.7) temp = 1.57079632679489661923 - go_satan(temp / x);
+    else temp = go_satan(x / temp);
+    if (sign) temp = -temp;
+    return temp;
+}
+double oracle_go_acos(double x) { return 1.57079632679489661923 - go_asin(x); }
+
 /* ============================================================================
  * RNG contract: Philox4x32-10, key = seed, counter =
  * (global pixel index, sample index, draw block, stream); draw n is word n&3 of
@@ -123,35 +184,51 @@ void oracle_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t
 
 static inline float u32_to_unit(uint32_t x) { return (float)(x >> 8) * 0x1.0p-24f; }
 
+/* The per-sample stream of the contract (GPU-first form): one Philox
+ * block per (global pixel, sample, event, attempt).  Event 0 is GetRay; event s+1 the
+ * scatter after segment s.  Draws are taken in the reference's order: words of the
+ * current attempt's block in sequence; a rejected unit-sphere / unit-disk candidate
+ * moves to the next attempt's block (word 0).  GetRay's first block holds dx, dy and
+ * the first disk candidate. */
 typedef struct {
     uint32_t key[2];
-    uint32_t pixel, sample, n;
+    uint32_t pixel, sample, event, attempt, word;
     uint32_t buf[4];
     uint64_t* draws;
 } rng_t;
 
+static void rng_load(rng_t* r) {
+    uint32_t ctr[4] = {r->pixel, r->sample, r->event, r->attempt};
+    oracle_philox4x32_10(ctr, r->key, r->buf);
+    r->word = 0;
+}
+static void rng_event(rng_t* r, uint32_t event) {
+    r->event = event;
+    r->attempt = 0;
+    rng_load(r);
+}
+static void rng_next_attempt(rng_t* r) {
+    r->attempt++;
+    rng_load(r);
+}
 static inline float rng_float32(rng_t* r) {
-    if ((r->n & 3u) == 0) {
-        uint32_t ctr[4] = {r->pixel, r->sample, r->n >> 2, 0u};
-        oracle_philox4x32_10(ctr, r->key, r->buf);
-    }
-    uint32_t w = r->buf[r->n & 3u];
-    r->n++;
+    uint32_t w = r->buf[r->word++ & 3u];
     if (r->draws) (*r->draws)++;
     return u32_to_unit(w);
 }
 
-float oracle_pixel_draw(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t n) {
-    uint32_t ctr[4] = {pixel, sample, n >> 2, 0u};
+void oracle_pixel_block(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t event, uint32_t attempt,
+                        uint32_t out[4]) {
+    uint32_t ctr[4] = {pixel, sample, event, attempt};
     uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
-    uint32_t out[4];
     oracle_philox4x32_10(ctr, key, out);
-    return u32_to_unit(out[n & 3u]);
 }
 
+/* Host streams (scene generation, BVH axis): word n of stream s, counter
+ * (block lo, block hi, 0, 0x80000000 | s) — disjoint from every pixel counter. */
 uint32_t oracle_stream_u32(uint64_t seed, uint32_t stream, uint64_t n) {
     uint64_t blk = n >> 2;
-    uint32_t ctr[4] = {(uint32_t)blk, (uint32_t)(blk >> 32), 0u, stream};
+    uint32_t ctr[4] = {(uint32_t)blk, (uint32_t)(blk >> 32), 0u, 0x80000000u | stream};
     uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
     uint32_t out[4];
     oracle_philox4x32_10(ctr, key, out);
@@ -161,7 +238,8 @@ uint32_t oracle_stream_u32(uint64_t seed, uint32_t stream, uint64_t n) {
 /* RandF32N, math.go:30-32: min + Float32()*(max-min). */
 static inline float rand_f32n(rng_t* r, float mn, float mx) { return mn + rng_float32(r) * (mx - mn); }
 
-/* NewVec3UnitRandOnUnitSphere32, vec3.go:182-190 (arguments drawn x, y, z). */
+/* NewVec3UnitRandOnUnitSphere32, vec3.go:182-190 (arguments drawn x, y, z); the
+ * caller has opened the event. */
 static vec3 rand_unit_on_sphere(rng_t* r) {
     for (;;) {
         float x = rand_f32n(r, -1.0f, 1.0f);
@@ -169,16 +247,18 @@ static vec3 rand_unit_on_sphere(rng_t* r) {
         float z = rand_f32n(r, -1.0f, 1.0f);
         vec3 v = v3(x, y, z);
         if (v_lensq(v) < 1.0f) return v_unit(v);
+        rng_next_attempt(r);
     }
 }
 
-/* NewVec3RandInUnitDisk, vec3.go:203-210. */
+/* NewVec3RandInUnitDisk, vec3.go:203-210 (event 0, after dx and dy). */
 static vec3 rand_in_unit_disk(rng_t* r) {
     for (;;) {
         float x = rand_f32n(r, -1.0f, 1.0f);
         float y = rand_f32n(r, -1.0f, 1.0f);
         vec3 v = v3(x, y, 0.0f);
         if (v_lensq(v) < 1.0f) return v;
+        rng_next_attempt(r);
     }
 }
 
@@ -311,8 +391,8 @@ static int sphere_hit(const ctx_t* cx, const rtx_sphere* s, const ray_t* r, floa
     }
     vec3 point = ray_at(r, t);                                             /* :118 */
     vec3 norm = v_unit(v_scale(v_sub(point, c), s->radius));               /* :119-120 */
-    float theta = (float)acos(-(double)norm.y);                            /* :122 */
-    float phi = (float)(atan2(-(double)norm.z, (double)norm.x) + 3.14159265358979323846); /* :123 */
+    float theta = (float)oracle_go_acos(-(double)norm.y);                  /* :122 */
+    float phi = (float)(oracle_go_atan2(-(double)norm.z, (double)norm.x) + 3.14159265358979323846); /* :123 */
     float u = (phi + 5.0f * PI_F32 / 12.0f) / (2.0f * PI_F32);             /* :125 typed consts fold in float32 */
     float v = theta / PI_F32;                                              /* :126 */
     (void)cx;
@@ -509,6 +589,7 @@ static vec3 ray_color_ref(const ctx_t* cx, const ray_t* r, rng_t* rng, int depth
         vec3 emit = material_emit(cx, &h, &has_emit);
         vec3 att;
         ray_t scattered;
+        rng_event(rng, cx->cam->max_depth - (uint32_t)depth + 1u);  /* scatter after this segment */
         if (!material_scatter(cx, r, &h, rng, &att, &scattered)) return emit;
         vec3 col = v_mul(att, ray_color_ref(cx, &scattered, rng, depth - 1));
         return v_add(emit, col);
@@ -535,6 +616,7 @@ static vec3 ray_color_iter(const ctx_t* cx, ray_t r, rng_t* rng, int depth) {
         if (has_emit) acc = v_add(acc, v_mul(thr, emit));
         vec3 att;
         ray_t scattered;
+        rng_event(rng, cx->cam->max_depth - (uint32_t)depth + 1u);
         if (!material_scatter(cx, &r, &h, rng, &att, &scattered)) return acc;
         thr = v_mul(thr, att);
         r = scattered;
@@ -552,6 +634,7 @@ static ray_t get_ray(const ctx_t* cx, rng_t* rng, uint32_t i, uint32_t j) {
     vec3 pc = v3(c->pixel00[0], c->pixel00[1], c->pixel00[2]);              /* :272 */
     pc = v_add(pc, du_off);                                                 /* :273 */
     pc = v_add(pc, dv_off);                                                 /* :274 */
+    rng_event(rng, 0u);
     float dx = -0.5f + rng_float32(rng);                                    /* :290 */
     float dy = -0.5f + rng_float32(rng);                                    /* :291 */
     pc = v_add(pc, v_add(v_scale(du, dx), v_scale(dv, dy)));                /* :275, 293-298 */
@@ -575,7 +658,7 @@ static vec3 sample_color(const ctx_t* cx, uint32_t i, uint32_t j, uint32_t k) {
     rng.key[1] = (uint32_t)(cx->seed >> 32);
     rng.pixel = j * cx->cam->image_width + i;
     rng.sample = k;
-    rng.n = 0;
+    rng.event = rng.attempt = rng.word = 0;
     rng.draws = &cx->c->rng_draws;
     ray_t r = get_ray(cx, &rng, i, j);
     cx->c->samples++;

@@ -51,8 +51,9 @@ typedef struct oracle_counters {
 /* Philox4x32-10 (Salmon et al., SC'11; Random123). */
 void oracle_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);
 
-/* The per-ray stream of the RNG contract: draw n of sample k of global pixel p. */
-float oracle_pixel_draw(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t n);
+/* The per-sample RNG contract: Philox block of (global pixel, sample, event, attempt). */
+void oracle_pixel_block(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t event, uint32_t attempt,
+                        uint32_t out[4]);
 
 /* Host streams (scene generation / BVH axis): word n of stream s. */
 uint32_t oracle_stream_u32(uint64_t seed, uint32_t stream, uint64_t n);
@@ -95,6 +96,10 @@ typedef struct oracle_scene oracle_scene;
 oracle_scene* oracle_build_random_spheres(uint64_t seed);
 const rtx_scene_desc* oracle_scene_desc(const oracle_scene* s);
 void oracle_scene_free(oracle_scene* s);
+
+/* Go's math.Atan2 / math.Acos algorithms (the UV of hittables.go:122-123). */
+double oracle_go_atan2(double y, double x);
+double oracle_go_acos(double x);
 
 /* Independent recompute of rtx_region_rows. */
 uint32_t oracle_region_rows(const rtx_region* r);

@@ -9,6 +9,7 @@
 
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -60,6 +61,7 @@ struct rtx_scene {
     std::vector<rtx_texture> textures;
     std::vector<uint32_t> texels;
     std::map<int, DeviceCopy> copies;
+    bool has_image = false;  // some texture is an ImageTexture: hits need UV
     std::mutex mu;
 };
 
@@ -170,7 +172,7 @@ int ensure_device(rtx_scene* s, int device, DeviceCopy** out) {
     HIP_TRY(hipMalloc(&c.texels, std::max<size_t>(1, s->texels.size()) * sizeof(uint32_t)));
     if (!s->texels.empty())
         HIP_TRY(hipMemcpy(c.texels, s->texels.data(), s->texels.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
-    HIP_TRY(hipMalloc(&c.counters, 8 * sizeof(unsigned long long)));
+    HIP_TRY(hipMalloc(&c.counters, 16 * sizeof(unsigned long long)));
     HIP_TRY(hipEventCreate(&c.ev0));
     HIP_TRY(hipEventCreate(&c.ev1));
     auto res = s->copies.emplace(device, c);
@@ -212,6 +214,28 @@ uint32_t region_rows(const rtx_region* r) {
     return (r->height - r->rank + r->world - 1) / r->world;
 }
 
+// Tuning knob of the v1 kernel (lanes waiting before a wave shades); RTX_SHADE_THRESH.
+uint32_t shade_thresh() {
+    static const uint32_t v = [] {
+        const char* e = std::getenv("RTX_SHADE_THRESH");
+        const long x = e ? std::strtol(e, nullptr, 10) : 48;
+        return (uint32_t)(x < 1 ? 1 : (x > 64 ? 64 : x));
+    }();
+    return v;
+}
+
+// Per-wave time limit of the persistent kernel (RTX_WATCHDOG_S, default 300 s): a bug
+// can never keep the GPU busy forever; the launch then fails with RTX_ERR_HIP.
+uint64_t watchdog_ticks() {
+    static const uint64_t v = [] {
+        const char* e = std::getenv("RTX_WATCHDOG_S");
+        double s = e ? std::strtod(e, nullptr) : 300.0;
+        if (!(s > 0)) s = 300.0;
+        return (uint64_t)(s * 1.0e8);  // s_memrealtime runs at 100 MHz
+    }();
+    return v;
+}
+
 rtxd::Params make_params(const rtx_scene* s, const DeviceCopy* c, const rtx_camera* cam, uint64_t seed,
                          const rtx_region* r, float* d_out) {
     rtxd::Params p;
@@ -232,16 +256,23 @@ rtxd::Params make_params(const rtx_scene* s, const DeviceCopy* c, const rtx_came
     p.world = r->world;
     p.out = d_out;
     p.counters = c->counters;
+    p.tile_counter = reinterpret_cast<uint32_t*>(c->counters + 7);  // slot 7 low: v2 tile queue head
+    p.error_flag = reinterpret_cast<uint32_t*>(c->counters + 7) + 1;  // slot 7 high: watchdog flag
+    p.watchdog_ticks = watchdog_ticks();
+    p.shade_thresh = shade_thresh();
+    p.has_uv = s->has_image ? 1u : 0u;
     return p;
 }
 
 // Enqueue one region on the current device, bracketed by HIP events on `stream`.
 int enqueue_on(rtx_scene* s, DeviceCopy* c, const rtx_camera* cam, uint64_t seed, const rtx_region* r, float* d_out,
-               hipStream_t stream, bool count, bool timed) {
+               hipStream_t stream, uint32_t flags, bool timed) {
     rtxd::Params p = make_params(s, c, cam, seed, r, d_out);
-    if (count) HIP_TRY(hipMemsetAsync(c->counters, 0, 8 * sizeof(unsigned long long), stream));
+    const uint32_t th = (flags >> 8) & 0x7Fu;  // RTX_FLAG_SHADE_THRESH(n) override
+    if (th) p.shade_thresh = th > 64 ? 64 : th;
+    if (flags & RTX_FLAG_COUNTERS) HIP_TRY(hipMemsetAsync(c->counters, 0, 16 * sizeof(unsigned long long), stream));
     if (timed) HIP_TRY(hipEventRecord(c->ev0, stream));
-    HIP_TRY(rtxd::launch_render(p, count, stream));
+    HIP_TRY(rtxd::launch_render(p, flags, stream));
     if (timed) HIP_TRY(hipEventRecord(c->ev1, stream));
     return RTX_OK;
 }
@@ -251,8 +282,9 @@ int collect_on(DeviceCopy* c, bool count, uint64_t samples, rtx_stats* st) {
     HIP_TRY(hipEventSynchronize(c->ev1));
     float ms = 0.0f;
     HIP_TRY(hipEventElapsedTime(&ms, c->ev0, c->ev1));
-    unsigned long long h[8] = {0};
-    if (count) HIP_TRY(hipMemcpy(h, c->counters, 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    unsigned long long h[16] = {0};
+    HIP_TRY(hipMemcpy(h, c->counters, 16 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    if ((h[7] >> 32) != 0) return fail(RTX_ERR_HIP, "render kernel watchdog fired (RTX_WATCHDOG_S): output incomplete");
     std::memset(st, 0, sizeof(*st));
     st->samples = count ? h[0] : samples;
     st->segments = h[1];
@@ -261,6 +293,10 @@ int collect_on(DeviceCopy* c, bool count, uint64_t samples, rtx_stats* st) {
     st->hits = h[4];
     st->texel_fetches = h[5];
     st->rng_draws = h[6];
+    st->wave_iters = h[8];
+    st->lane_steps = h[9];
+    st->shade_phases = h[10];
+    st->shade_lanes = h[11];
     st->kernel_ms = ms;
     return RTX_OK;
 }
@@ -272,7 +308,7 @@ extern "C" {
 int rtx_version(void) { return RTX_ABI_VERSION; }
 
 const char* rtx_build_info(void) {
-    return "librtx gfx950 megakernel v0 (thread-per-pixel, threaded pre-order BVH); built " __DATE__ " " __TIME__;
+    return "librtx gfx950 megakernel v1 (persistent wave loop, LDS scene, threaded pre-order BVH); built " __DATE__ " " __TIME__;
 }
 
 const char* rtx_last_error(void) { return g_last_error.c_str(); }
@@ -324,6 +360,7 @@ int rtx_scene_create(const rtx_scene_desc* d, rtx_scene** out) {
     }
     s->materials.assign(d->materials, d->materials + d->n_materials);
     s->textures.assign(d->textures, d->textures + d->n_textures);
+    for (const rtx_texture& t : s->textures) s->has_image |= t.type == RTX_TEX_IMAGE;
     if (d->n_texels) s->texels.assign(d->texels, d->texels + d->n_texels);
     int cur = 0;
     if (hipGetDevice(&cur) != hipSuccess) {
@@ -368,7 +405,7 @@ int rtx_render_region_device(rtx_scene* s, const rtx_camera* cam, uint64_t seed,
     if (int rc = ensure_device(s, cur, &c)) return rc;
     HIP_TRY(hipSetDevice(cur));
     const bool count = (flags & RTX_FLAG_COUNTERS) != 0;
-    if (int rc = enqueue_on(s, c, cam, seed, region, d_out, (hipStream_t)hip_stream, count, stats != nullptr)) return rc;
+    if (int rc = enqueue_on(s, c, cam, seed, region, d_out, (hipStream_t)hip_stream, flags, stats != nullptr)) return rc;
     if (!stats) return RTX_OK;
     return collect_on(c, count, (uint64_t)region_rows(region) * region->width * cam->samples_per_pixel, stats);
 }
@@ -400,7 +437,7 @@ int rtx_render(rtx_scene* s, const rtx_camera* cam, uint64_t seed, int n_gpus, f
         const size_t bytes = (size_t)region_rows(&regs[d]) * W * 3 * sizeof(float);
         if (hipStreamCreateWithFlags(&streams[d], hipStreamNonBlocking) != hipSuccess) { rc = fail(RTX_ERR_HIP, "stream"); break; }
         if (hipMalloc(&bufs[d], std::max<size_t>(bytes, 4)) != hipSuccess) { rc = fail(RTX_ERR_OOM, "hipMalloc %zu", bytes); break; }
-        rc = enqueue_on(s, c, cam, seed, &regs[d], bufs[d], streams[d], stats != nullptr, true);
+        rc = enqueue_on(s, c, cam, seed, &regs[d], bufs[d], streams[d], stats ? RTX_FLAG_COUNTERS : 0u, true);
     }
     // All devices run concurrently; collect after every launch is enqueued.
     for (int d = 0; d < n_gpus && rc == RTX_OK && stats; ++d) {

@@ -5,8 +5,9 @@
 // float32 operations of the Go source, in the same association order, with no
 // contraction (built with -ffp-contract=off) and with the correctly rounded division
 // and square root hipcc emits by default for gfx950.  Where Go widens to float64
-// (Dielectric, materials.go:100, 118) the kernel does too.  The cited lines are the
-// reference's; the structure (iterative, stackless, branch-light) is the GPU's.
+// (Dielectric, materials.go:100, 118; sphere UV, hittables.go:122-123) the kernel does
+// too.  The cited lines are the reference's; the structure (iterative, stackless,
+// lockstep RNG) is the GPU's.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -51,12 +52,94 @@ __device__ __forceinline__ double go_pow5(double x) {
 }
 
 // ---------------------------------------------------------------------------------
-// RNG contract: Philox4x32-10 keyed by the seed; counter =
-// (global pixel index, sample index, draw block, stream 0); draw n = word n & 3 of
-// block n >> 2; u = float32(x >> 8) * 2^-24.
+// Go's math.Atan2 / math.Acos (Go 1.21 src/math/atan.go, asin.go, atan2.go — pure Go
+// on amd64, Cephes rational approximations).  Restated op for op in float64, so the
+// UV of hittables.go:122-123 is the same bits on the GPU, in the oracle and in Go.
 // ---------------------------------------------------------------------------------
-__device__ __forceinline__ void philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0,
-                                              uint32_t k1, uint32_t& o0, uint32_t& o1, uint32_t& o2, uint32_t& o3) {
+__device__ __forceinline__ double go_xatan(double x) {  // atan.go xatan: [0, 0.66]
+    const double P0 = -8.750608600031904122785e-01, P1 = -1.615753718733365076637e+01,
+                 P2 = -7.500855792314704667340e+01, P3 = -1.228866684490136173410e+02,
+                 P4 = -6.485021904942025371773e+01, Q0 = +2.485846490142306297962e+01,
+                 Q1 = +1.650270098316988542046e+02, Q2 = +4.328810604912902668951e+02,
+                 Q3 = +4.853903996359136964868e+02, Q4 = +1.945506571482613964425e+02;
+    double z = x * x;
+    z = z * ((((P0 * z + P1) * z + P2) * z + P3) * z + P4) / (((((z + Q0) * z + Q1) * z + Q2) * z + Q3) * z + Q4);
+    z = x * z + x;
+    return z;
+}
+__device__ __forceinline__ double go_satan(double x) {  // atan.go satan: x >= 0
+    const double Morebits = 6.123233995736765886130e-17, Tan3pio8 = 2.41421356237309504880;
+    const double PiO2 = 1.57079632679489661923, PiO4 = 0.785398163397448309616;
+    if (x <= 0.66) return go_xatan(x);
+    if (x > Tan3pio8) return PiO2 - go_xatan(1.0 / x) + Morebits;
+    return PiO4 + go_xatan((x - 1.0) / (x + 1.0)) + 0.5 * Morebits;
+}
+__device__ __forceinline__ double go_atan(double x) {
+    if (x == 0.0) return x;
+    return x > 0.0 ? go_satan(x) : -go_satan(-x);
+}
+__device__ __forceinline__ double go_atan2(double y, double x) {  // atan2.go
+    const double Pi = 3.14159265358979323846;
+    if (y != y || x != x) return __builtin_nan("");
+    if (y == 0.0) {
+        if (x >= 0.0 && !__builtin_signbit(x)) return __builtin_copysign(0.0, y);
+        return __builtin_copysign(Pi, y);
+    }
+    if (x == 0.0) return __builtin_copysign(Pi / 2.0, y);
+    if (__builtin_isinf(x)) {
+        if (x > 0.0) return __builtin_isinf(y) ? __builtin_copysign(Pi / 4.0, y) : __builtin_copysign(0.0, y);
+        return __builtin_isinf(y) ? __builtin_copysign(3.0 * Pi / 4.0, y) : __builtin_copysign(Pi, y);
+    }
+    if (__builtin_isinf(y)) return __builtin_copysign(Pi / 2.0, y);
+    const double q = go_atan(y / x);
+    if (x < 0.0) return q <= 0.0 ? q + Pi : q - Pi;
+    return q;
+}
+__device__ __forceinline__ double go_asin(double x) {  // asin.go
+    const double PiO2 = 1.57079632679489661923;
+    if (x == 0.0) return x;
+    bool sign = false;
+    if (x < 0.0) {
+        x = -x;
+        sign = true;
+    }
+    if (x > 1.0) return __builtin_nan("");
+    double temp = __builtin_sqrt(1.0 - x * x);
+    if (x > 0.7) temp = PiO2 - go_satan(temp / x);
+    else temp = go_satan(x / temp);
+    return sign ? -temp : temp;
+}
+__device__ __forceinline__ double go_acos(double x) { return 1.57079632679489661923 - go_asin(x); }
+
+// Spherical UV, hittables.go:122-126 (float64 Acos / Atan2; typed float32 constants).
+struct UV {
+    float u, v;
+};
+__device__ __noinline__ UV sphere_uv(float nx, float ny, float nz) {
+    const float pi32 = 3.14159274101257324f;
+    const float theta = (float)go_acos(-(double)ny);
+    const float phi = (float)(go_atan2(-(double)nz, (double)nx) + 3.14159265358979323846);
+    return UV{(phi + 5.0f * pi32 / 12.0f) / (2.0f * pi32), theta / pi32};
+}
+
+// ---------------------------------------------------------------------------------
+// RNG contract (GPU-first): Philox4x32-10 keyed by the seed, one block
+// of four 32-bit words per (global pixel, sample, event, attempt); u = float32(w >> 8)
+// * 2^-24 in [0, 1) (the range of rand.Float32).  The reference's draw ORDER is kept:
+//   event 0 = GetRay (camera.go:265-299): block (0,0) = dx, dy, disk x, disk y of the
+//             first unit-disk attempt; disk attempt a >= 1 uses words 0,1 of block (0,a);
+//   event s+1 = the scatter after segment s (ray.go:42):
+//             Lambertian / Metal unit-sphere attempt a (vec3.go:182-190) = words 0,1,2
+//             of block (s+1, a); Dielectric's uniform (materials.go:103) = word 0 of
+//             block (s+1, 0), drawn only when refraction is possible.
+// Every lane of a wave evaluates its block at the same program point, so Philox runs
+// in lockstep instead of at a per-lane word boundary inside divergent loops.
+// ---------------------------------------------------------------------------------
+struct U4 {
+    uint32_t x, y, z, w;
+};
+__device__ __forceinline__ U4 philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0,
+                                            uint32_t k1) {
 #pragma unroll
     for (int r = 0; r < 10; ++r) {
         if (r > 0) {
@@ -72,52 +155,27 @@ __device__ __forceinline__ void philox4x32_10(uint32_t c0, uint32_t c1, uint32_t
         c2 = n2;
         c3 = lo0;
     }
-    o0 = c0;
-    o1 = c1;
-    o2 = c2;
-    o3 = c3;
+    return U4{c0, c1, c2, c3};
 }
+__device__ __forceinline__ float unit_f32(uint32_t w) { return (float)(w >> 8) * 0x1.0p-24f; }
+// RandF32N(-1, 1), math.go:30-32: -1 + u * (1 - (-1)).
+__device__ __forceinline__ float signed_unit(uint32_t w) { return -1.0f + unit_f32(w) * 2.0f; }
 
-struct Rng {
-    uint32_t k0, k1, pixel, sample, n;
-    uint32_t w0, w1, w2, w3;
-    uint32_t draws;
-
-    __device__ __forceinline__ void init(uint64_t seed, uint32_t px, uint32_t k) {
-        k0 = (uint32_t)seed;
-        k1 = (uint32_t)(seed >> 32);
-        pixel = px;
-        sample = k;
-        n = 0;
+struct PathRng {
+    uint32_t k0, k1, pixel, sample;
+    __device__ __forceinline__ U4 block(uint32_t event, uint32_t attempt) const {
+        return philox4x32_10(pixel, sample, event, attempt, k0, k1);
     }
-    __device__ __forceinline__ float next() {
-        const uint32_t slot = n & 3u;
-        if (slot == 0u) philox4x32_10(pixel, sample, n >> 2, 0u, k0, k1, w0, w1, w2, w3);
-        const uint32_t w = slot == 0u ? w0 : (slot == 1u ? w1 : (slot == 2u ? w2 : w3));
-        ++n;
-        return (float)(w >> 8) * 0x1.0p-24f;
-    }
-    // RandF32N(-1, 1), math.go:30-32: -1 + u * (1 - (-1)).
-    __device__ __forceinline__ float signed_unit() { return -1.0f + next() * 2.0f; }
 };
 
-// NewVec3UnitRandOnUnitSphere32, vec3.go:182-190.
-__device__ __forceinline__ V3 rand_unit_on_sphere(Rng& rng) {
-    for (;;) {
-        const float x = rng.signed_unit();
-        const float y = rng.signed_unit();
-        const float z = rng.signed_unit();
+// NewVec3UnitRandOnUnitSphere32 (vec3.go:182-190) for event e, given its block 0.
+__device__ __forceinline__ V3 rand_unit_on_sphere(const PathRng& rng, uint32_t e, U4 b, uint32_t& draws) {
+    for (uint32_t a = 1;; ++a) {
+        const float x = signed_unit(b.x), y = signed_unit(b.y), z = signed_unit(b.z);
+        draws += 3;
         const V3 v = v3(x, y, z);
         if (lensq(v) < 1.0f) return unit(v);
-    }
-}
-
-// NewVec3RandInUnitDisk, vec3.go:203-210 (LenSq adds the z = 0 term: exact no-op).
-__device__ __forceinline__ void rand_in_unit_disk(Rng& rng, float& x, float& y) {
-    for (;;) {
-        x = rng.signed_unit();
-        y = rng.signed_unit();
-        if (x * x + y * y < 1.0f) return;
+        b = rng.block(e, a);
     }
 }
 
@@ -135,7 +193,12 @@ struct Params {
     uint64_t seed;
     uint32_t x0, y0, width, rows, rank, world;
     float* out;
-    unsigned long long* counters;  // 7 x u64 (rtx_stats order) when counting
+    unsigned long long* counters;  // rtx_stats order when counting (16 x u64)
+    uint32_t shade_thresh;         // v1/v2: shade once this many lanes of a wave wait (1..64)
+    uint32_t* tile_counter;        // v2: global tile queue head (zeroed before each launch)
+    uint32_t* error_flag;          // v2: set to 1 by a wave that hit the watchdog
+    uint64_t watchdog_ticks;       // v2: per-wave limit in s_memrealtime ticks (100 MHz)
+    uint32_t has_uv;               // scene has an image texture (UV needed at hits)
 };
 
 struct Ray {
@@ -143,68 +206,39 @@ struct Ray {
 };
 
 struct Counters {
-    uint32_t segments, node_visits, prim_tests, hits, texel_fetches;
+    uint32_t segments, node_visits, prim_tests, hits, texel_fetches, draws;
 };
 
-// Closest hit over the threaded pre-order layout (see rtx_layout.h): identical
-// sequence of Aabb.Hit (bvh.go:52-61, 84-102) and Sphere.Hit (hittables.go:96-116)
-// tests as the reference recursion, running bound = closest hit so far.
-template <bool COUNT>
-__device__ __forceinline__ int32_t closest_hit(const Params& p, const Ray& r, float& t_hit, Counters& cnt) {
-    // InBoundary computes 1/dir per node; hoisting it is bit-identical.
-    const float ix = 1.0f / r.d.x, iy = 1.0f / r.d.y, iz = 1.0f / r.d.z;
-    const bool nx = ix < 0.0f, ny = iy < 0.0f, nz = iz < 0.0f;
-    const float a = lensq(r.d);  // hittables.go:98, loop-invariant
-    const float tmin = 0.001f;   // ray.go:37
-    float closest = __builtin_inff();
-    int32_t hit = -1;
-    const float4* __restrict__ E = p.entries;
-    const uint32_t n = p.n_entries;
-    uint32_t i = 0;
-    while (i < n) {
-        const float4 ea = E[2 * i];
-        const float4 eb = E[2 * i + 1];
-        const int32_t tag = __float_as_int(eb.w);
-        if (tag == RTX_E_NODE) {
-            if (COUNT) ++cnt.node_visits;
-            // Per axis: t0 = (min - o) * invD, t1 = (max - o) * invD, swapped if invD < 0
-            // (selecting the operands first is the same two operations).
-            const float t0x = ((nx ? eb.x : ea.x) - r.o.x) * ix;
-            const float t1x = ((nx ? ea.x : eb.x) - r.o.x) * ix;
-            const float t0y = ((ny ? eb.y : ea.y) - r.o.y) * iy;
-            const float t1y = ((ny ? ea.y : eb.y) - r.o.y) * iy;
-            const float t0z = ((nz ? eb.z : ea.z) - r.o.z) * iz;
-            const float t1z = ((nz ? ea.z : eb.z) - r.o.z) * iz;
-            // `if t0 > min { min = t0 }` keeps min on NaN (0 * inf): fmaxf's NaN rule.
-            // The bound only shrinks, so testing min < max once after all three axes
-            // equals the reference's per-axis early exit.
-            const float lo = __builtin_fmaxf(__builtin_fmaxf(__builtin_fmaxf(tmin, t0x), t0y), t0z);
-            const float hi = __builtin_fminf(__builtin_fminf(__builtin_fminf(closest, t1x), t1y), t1z);
-            i = (lo < hi) ? i + 1 : (uint32_t)__float_as_int(ea.w);
-        } else {
-            if (COUNT) ++cnt.prim_tests;
-            const float ox = r.o.x - ea.x, oy = r.o.y - ea.y, oz = r.o.z - ea.z;       // :97
-            const float hb = r.d.x * ox + r.d.y * oy + r.d.z * oz;                     // :99
-            const float c = (ox * ox + oy * oy + oz * oz) - eb.x;                      // :100
-            const float disc = hb * hb - a * c;                                        // :102
-            if (disc >= 0.0f) {                                                        // :104 (NaN: miss either way)
-                const float sq = __builtin_sqrtf(disc);                                // :108
-                float t = (-hb - sq) / a;                                              // :110
-                bool ok = tmin < t && t < closest;
-                if (!ok) {
-                    t = (-hb + sq) / a;                                                // :112
-                    ok = tmin < t && t < closest;
-                }
-                if (ok) {
-                    closest = t;
-                    hit = (int32_t)i;
-                }
-            }
-            ++i;
-        }
+// GetRay + sampleUnitSquare, camera.go:265-299, event 0.  base = (pixel00 + du*i) + dv*j.
+__device__ __forceinline__ Ray camera_ray(const rtx_camera& c, V3 base, const PathRng& rng, uint32_t& draws) {
+    U4 b = rng.block(0, 0);
+    const V3 du = v3(c.pixel_du[0], c.pixel_du[1], c.pixel_du[2]);
+    const V3 dv = v3(c.pixel_dv[0], c.pixel_dv[1], c.pixel_dv[2]);
+    const float dx = -0.5f + unit_f32(b.x);                       // :290
+    const float dy = -0.5f + unit_f32(b.y);                       // :291
+    const V3 pc = add(base, add(scale(du, dx), scale(dv, dy)));   // :275
+    float x = signed_unit(b.z), y = signed_unit(b.w);             // :277 disk, always drawn
+    draws += 4;
+    for (uint32_t a = 1; !(x * x + y * y < 1.0f); ++a) {          // vec3.go:203-210
+        b = rng.block(0, a);
+        x = signed_unit(b.x);
+        y = signed_unit(b.y);
+        draws += 2;
     }
-    t_hit = closest;
-    return hit;
+    const V3 center = v3(c.center[0], c.center[1], c.center[2]);
+    V3 origin = center;
+    if (c.defocus_angle > 0.0f) {                                 // :279-281
+        const V3 ddu = v3(c.defocus_disk_u[0], c.defocus_disk_u[1], c.defocus_disk_u[2]);
+        const V3 ddv = v3(c.defocus_disk_v[0], c.defocus_disk_v[1], c.defocus_disk_v[2]);
+        origin = add(center, add(scale(ddu, x), scale(ddv, y)));
+    }
+    return Ray{origin, sub(pc, origin)};                          // :283-286
+}
+
+__device__ __forceinline__ V3 pixel_base(const rtx_camera& c, uint32_t x, uint32_t y) {  // camera.go:266-274
+    return add(add(v3(c.pixel00[0], c.pixel00[1], c.pixel00[2]),
+                   scale(v3(c.pixel_du[0], c.pixel_du[1], c.pixel_du[2]), (float)x)),
+               scale(v3(c.pixel_dv[0], c.pixel_dv[1], c.pixel_dv[2]), (float)y));
 }
 
 // Texture.GetTexture, materials.go:127-193.
@@ -236,103 +270,148 @@ __device__ __forceinline__ V3 texture_value(const Params& p, uint32_t ti, float 
               (float)(((px >> 16) & 0xFFu) * 257u) * cs);
 }
 
-__device__ __forceinline__ bool texture_needs_uv(const Params& p, uint32_t ti) {
-    return p.textures[ti].type == RTX_TEX_IMAGE;
+// One step of the closest-hit walk over the threaded pre-order layout (rtx_layout.h):
+// entry i is a node (Aabb.Hit, bvh.go:52-61, 84-102) or a sphere (Sphere.Hit,
+// hittables.go:96-116).  The sequence of steps is the reference recursion's, with
+// running bound `closest` = the closest hit so far (bvh.go:227-232).
+struct Trav {
+    uint32_t i;
+    int32_t hit;
+    float closest, ix, iy, iz, a;
+    bool nx, ny, nz;
+};
+
+__device__ __forceinline__ void trav_begin(Trav& t, const Ray& r) {
+    // InBoundary computes 1/dir per node; hoisting it is bit-identical.
+    t.ix = 1.0f / r.d.x;
+    t.iy = 1.0f / r.d.y;
+    t.iz = 1.0f / r.d.z;
+    t.nx = t.ix < 0.0f;
+    t.ny = t.iy < 0.0f;
+    t.nz = t.iz < 0.0f;
+    t.a = lensq(r.d);  // hittables.go:98, loop-invariant
+    t.closest = __builtin_inff();
+    t.hit = -1;
+    t.i = 0;
 }
 
-// Spherical UV, hittables.go:122-126 (float64 acos / atan2; typed float32 constants).
-__device__ __forceinline__ void sphere_uv(V3 n, float& u, float& v) {
-    const float pi32 = 3.14159274101257324f;
-    const float theta = (float)acos(-(double)n.y);
-    const float phi = (float)(atan2(-(double)n.z, (double)n.x) + 3.14159265358979323846);
-    u = (phi + 5.0f * pi32 / 12.0f) / (2.0f * pi32);
-    v = theta / pi32;
-}
-
-// GetRay + sampleUnitSquare, camera.go:265-299.  base = (pixel00 + du*i) + dv*j.
-__device__ __forceinline__ Ray camera_ray(const rtx_camera& c, V3 base, Rng& rng) {
-    const V3 du = v3(c.pixel_du[0], c.pixel_du[1], c.pixel_du[2]);
-    const V3 dv = v3(c.pixel_dv[0], c.pixel_dv[1], c.pixel_dv[2]);
-    const float dx = -0.5f + rng.next();                          // :290
-    const float dy = -0.5f + rng.next();                          // :291
-    const V3 pc = add(base, add(scale(du, dx), scale(dv, dy)));   // :275
-    float x, y;
-    rand_in_unit_disk(rng, x, y);                                 // :277, always drawn
-    const V3 center = v3(c.center[0], c.center[1], c.center[2]);
-    V3 origin = center;
-    if (c.defocus_angle > 0.0f) {                                 // :279-281
-        const V3 ddu = v3(c.defocus_disk_u[0], c.defocus_disk_u[1], c.defocus_disk_u[2]);
-        const V3 ddv = v3(c.defocus_disk_v[0], c.defocus_disk_v[1], c.defocus_disk_v[2]);
-        origin = add(center, add(scale(ddu, x), scale(ddv, y)));
-    }
-    return Ray{origin, sub(pc, origin)};                          // :283-286
-}
-
-// One path: GetColor (ray.go:32-54) as a bounded loop, colour accumulated front to
-// back (L += T*emit, T *= attenuation).  Path decisions are those of the recursion;
-// the colour product differs from it only in rounding (~1 ulp).
 template <bool COUNT>
-__device__ __forceinline__ V3 trace_path(const Params& p, Ray r, Rng& rng, Counters& cnt) {
-    V3 thr = v3(1.0f, 1.0f, 1.0f);
-    V3 acc = v3(0.0f, 0.0f, 0.0f);
-    for (uint32_t depth = p.cam.max_depth; depth > 0; --depth) {   // ray.go:33
-        if (COUNT) ++cnt.segments;
-        float t;
-        const int32_t e = closest_hit<COUNT>(p, r, t, cnt);
-        if (e < 0) {                                                // ray.go:52
-            const V3 bg = v3(p.cam.background[0], p.cam.background[1], p.cam.background[2]);
-            return add(acc, mul(thr, bg));
+__device__ __forceinline__ void trav_step(Trav& t, const Ray& r, const float4* __restrict__ E, Counters& cnt) {
+    const float tmin = 0.001f;  // ray.go:37
+    const float4 ea = E[2 * t.i];
+    const float4 eb = E[2 * t.i + 1];
+    if (__float_as_int(eb.w) == RTX_E_NODE) {
+        if (COUNT) ++cnt.node_visits;
+        // Per axis: t0 = (min - o) * invD, t1 = (max - o) * invD, swapped if invD < 0
+        // (selecting the operands first is the same two operations).
+        const float t0x = ((t.nx ? eb.x : ea.x) - r.o.x) * t.ix;
+        const float t1x = ((t.nx ? ea.x : eb.x) - r.o.x) * t.ix;
+        const float t0y = ((t.ny ? eb.y : ea.y) - r.o.y) * t.iy;
+        const float t1y = ((t.ny ? ea.y : eb.y) - r.o.y) * t.iy;
+        const float t0z = ((t.nz ? eb.z : ea.z) - r.o.z) * t.iz;
+        const float t1z = ((t.nz ? ea.z : eb.z) - r.o.z) * t.iz;
+        // `if t0 > min { min = t0 }` keeps min on NaN (0 * inf): fmaxf's NaN rule.  The
+        // bound only shrinks, so one min < max test after all three axes equals the
+        // reference's per-axis early exit.
+        const float lo = __builtin_fmaxf(__builtin_fmaxf(__builtin_fmaxf(tmin, t0x), t0y), t0z);
+        const float hi = __builtin_fminf(__builtin_fminf(__builtin_fminf(t.closest, t1x), t1y), t1z);
+        t.i = (lo < hi) ? t.i + 1 : (uint32_t)__float_as_int(ea.w);
+    } else {
+        if (COUNT) ++cnt.prim_tests;
+        const float ox = r.o.x - ea.x, oy = r.o.y - ea.y, oz = r.o.z - ea.z;  // :97
+        const float hb = r.d.x * ox + r.d.y * oy + r.d.z * oz;                 // :99
+        const float c = (ox * ox + oy * oy + oz * oz) - eb.x;                  // :100
+        const float disc = hb * hb - t.a * c;                                  // :102
+        if (disc >= 0.0f) {                                                    // :104 (NaN: miss either way)
+            const float sq = __builtin_sqrtf(disc);                            // :108
+            float tt = (-hb - sq) / t.a;                                       // :110
+            bool ok = tmin < tt && tt < t.closest;
+            if (!ok) {
+                tt = (-hb + sq) / t.a;                                         // :112
+                ok = tmin < tt && tt < t.closest;
+            }
+            if (ok) {
+                t.closest = tt;
+                t.hit = (int32_t)t.i;
+            }
         }
-        if (COUNT) ++cnt.hits;
-        const float4 sa = p.entries[2 * e];
-        const float4 sb = p.entries[2 * e + 1];
-        const V3 c = v3(sa.x, sa.y, sa.z);
-        const float radius = sa.w;
-        const uint32_t mi = (uint32_t)__float_as_int(sb.w);
-        const V3 pt = add(scale(r.d, t), r.o);                      // ray.go:25-30
-        V3 n = unit(scale(sub(pt, c), radius));                     // hittables.go:119-120
-        const bool front = dot(r.d, n) < 0.0f;                      // hittables.go:23
-        const rtx_material m = p.materials[mi];
-        float u = 0.0f, v = 0.0f;
-        if ((m.type == RTX_MAT_LAMBERTIAN || m.type == RTX_MAT_DIFFUSE_LIGHT) && texture_needs_uv(p, m.texture))
-            sphere_uv(n, u, v);                                     // only an image texture reads UV
-        if (!front) n = scale(n, -1.0f);                            // hittables.go:24-26
+        ++t.i;
+    }
+}
 
-        if (m.type == RTX_MAT_LAMBERTIAN) {                         // materials.go:33-42
-            V3 dir = add(n, rand_unit_on_sphere(rng));
+// Shade the result of segment `seg` (ray.go:36-53, materials.go:33-113).  Returns true
+// when the path ends, with its colour in `color`; otherwise r / thr hold the next
+// segment.  Lockstep RNG: every hitting lane evaluates block (seg+1, 0) first.
+template <bool COUNT>
+__device__ __forceinline__ bool shade(const Params& p, const float4* __restrict__ E, const Trav& t, uint32_t seg,
+                                      Ray& r, V3& thr, V3& acc, const PathRng& rng, Counters& cnt, V3& color) {
+    if (t.hit < 0) {  // miss: background (ray.go:52)
+        color = add(acc, mul(thr, v3(p.cam.background[0], p.cam.background[1], p.cam.background[2])));
+        return true;
+    }
+    if (COUNT) ++cnt.hits;
+    const uint32_t e = seg + 1;
+    const U4 b0 = rng.block(e, 0);
+    const float4 sa = E[2 * t.hit];
+    const float4 sb = E[2 * t.hit + 1];
+    const V3 c = v3(sa.x, sa.y, sa.z);
+    const uint32_t mi = (uint32_t)__float_as_int(sb.w);
+    const V3 pt = add(scale(r.d, t.closest), r.o);              // ray.go:25-30
+    V3 n = unit(scale(sub(pt, c), sa.w));                       // hittables.go:119-120
+    const bool front = dot(r.d, n) < 0.0f;                      // hittables.go:23
+    const rtx_material m = p.materials[mi];
+    float u = 0.0f, v = 0.0f;
+    if (p.has_uv && (m.type == RTX_MAT_LAMBERTIAN || m.type == RTX_MAT_DIFFUSE_LIGHT) &&
+        p.textures[m.texture].type == RTX_TEX_IMAGE) {           // only an image texture reads UV
+        const UV uv = sphere_uv(n.x, n.y, n.z);
+        u = uv.u;
+        v = uv.v;
+    }
+    if (!front) n = scale(n, -1.0f);                            // hittables.go:24-26
+
+    if (m.type == RTX_MAT_LAMBERTIAN || m.type == RTX_MAT_METAL) {
+        uint32_t draws = 0;
+        const V3 s = rand_unit_on_sphere(rng, e, b0, draws);    // shared by both materials
+        if (COUNT) cnt.draws += draws;
+        if (m.type == RTX_MAT_LAMBERTIAN) {                     // materials.go:33-42
+            V3 dir = add(n, s);
             if (near_zero(dir)) dir = n;
             const V3 att = texture_value<COUNT>(p, m.texture, u, v, pt, cnt);
             thr = mul(thr, att);
             r = Ray{pt, dir};
-        } else if (m.type == RTX_MAT_METAL) {                       // materials.go:60-75
-            const V3 ud = unit(r.d);
-            const V3 refl = reflect(ud, n);
-            const V3 fz = scale(rand_unit_on_sphere(rng), m.fuzz);
-            const V3 s = add(refl, fz);
-            if (!(dot(s, n) > 0.0f)) return acc;                    // absorbed: Emit() = 0
-            thr = mul(thr, v3(m.albedo[0], m.albedo[1], m.albedo[2]));
-            r = Ray{pt, s};
-        } else if (m.type == RTX_MAT_DIELECTRIC) {                  // materials.go:91-113
-            const float eta = front ? 1.0f / m.ior : m.ior;
-            const V3 ud = unit(r.d);
-            const float d = dot(scale(ud, -1.0f), n);
-            const float cos_t = d < 1.0f ? d : (d != d ? d : 1.0f); // float32(math.Min(float64(d), 1))
-            const float sin_t = (float)__builtin_sqrt(1.0 - (double)(cos_t * cos_t));
-            bool refl = sin_t * eta > 1.0f;
-            if (!refl) {                                            // short-circuit: draw only here
-                float r0 = (1.0f - eta) / (1.0f + eta);             // materials.go:116-118
-                r0 *= r0;
-                const float rf = r0 + (1.0f - r0) * (float)go_pow5(1.0 - (double)cos_t);
-                refl = rf > rng.next();
-            }
-            const V3 dir = refl ? reflect(ud, n) : refract(ud, n, eta);
-            r = Ray{pt, dir};                                       // attenuation (1,1,1)
-        } else {                                                    // DiffuseLight: emit, no scatter
-            const V3 em = texture_value<COUNT>(p, m.texture, u, v, pt, cnt);
-            return add(acc, mul(thr, em));
+            return false;
         }
+        const V3 refl = reflect(unit(r.d), n);                  // materials.go:60-75
+        const V3 sc = add(refl, scale(s, m.fuzz));
+        if (!(dot(sc, n) > 0.0f)) {                             // absorbed: Emit() = 0
+            color = acc;
+            return true;
+        }
+        thr = mul(thr, v3(m.albedo[0], m.albedo[1], m.albedo[2]));
+        r = Ray{pt, sc};
+        return false;
     }
-    return acc;  // depth exhausted: ray.go:33-35
+    if (m.type == RTX_MAT_DIELECTRIC) {                         // materials.go:91-113
+        const float eta = front ? 1.0f / m.ior : m.ior;
+        const V3 ud = unit(r.d);
+        const float d = dot(scale(ud, -1.0f), n);
+        const float cos_t = d < 1.0f ? d : (d != d ? d : 1.0f); // float32(math.Min(float64(d), 1))
+        const float sin_t = (float)__builtin_sqrt(1.0 - (double)(cos_t * cos_t));
+        bool refl = sin_t * eta > 1.0f;
+        if (!refl) {                                            // short-circuit: draw only here
+            float r0 = (1.0f - eta) / (1.0f + eta);             // materials.go:116-118
+            r0 *= r0;
+            const float rf = r0 + (1.0f - r0) * (float)go_pow5(1.0 - (double)cos_t);
+            refl = rf > unit_f32(b0.x);
+            if (COUNT) cnt.draws += 1;
+        }
+        r = Ray{pt, refl ? reflect(ud, n) : refract(ud, n, eta)};  // attenuation (1,1,1)
+        return false;
+    }
+    // DiffuseLight: emit, never scatters (materials.go:303-313)
+    const V3 em = texture_value<COUNT>(p, m.texture, u, v, pt, cnt);
+    color = add(acc, mul(thr, em));
+    return true;
 }
 
 }  // namespace rtxd

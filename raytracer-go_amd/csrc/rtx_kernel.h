@@ -4,7 +4,8 @@
 
 namespace rtxd {
 struct Params;
-// Enqueue a render of p's region on `stream`; `count` selects the instantiation that
-// accumulates the work counters into p.counters.
-hipError_t launch_render(const Params& p, bool count, hipStream_t stream);
+// Enqueue a render of p's region on `stream`.  flags: RTX_FLAG_COUNTERS selects the
+// instantiation that accumulates the work counters into p.counters; RTX_FLAG_KERNEL_V0
+// and RTX_FLAG_NO_LDS select A/B variants (identical output).
+hipError_t launch_render(const Params& p, uint32_t flags, hipStream_t stream);
 }  // namespace rtxd

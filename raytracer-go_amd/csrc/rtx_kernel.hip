@@ -2,11 +2,19 @@
 //
 // Replaces the per-pixel goroutine body of Camera.Render (camera.go:208-217):
 // GetPixelColor (camera.go:254-263) = for k < spp { sum += GetColor(GetRay()) },
-// then sum * (1/spp).  One work-item owns one pixel of a 16x16 tile (a 64-lane
-// wave = 16x4 pixels) and walks its samples in order k = 0..spp-1, so the float32
-// sum is accumulated in exactly the reference's order.  Each sample is independent
-// (counter-based RNG keyed by global pixel index and k), so the value of a pixel
-// does not depend on the tile, the region or the number of GPUs.
+// then sum * (1/spp).  Every pixel's samples are added in order k = 0..spp-1, so the
+// float32 sum is the reference's.  Every sample is independent (counter-based RNG
+// keyed by global pixel index and k), so a pixel's value does not depend on the tile,
+// the region, the scheduling or the number of GPUs.
+//
+// Three schedules of the same per-sample code (rtx_device.h), identical output:
+//  v2 render_pool   (default) persistent waves over a pool of pixels fed by a global
+//                   tile queue; lanes take any idle pixel of the pool.
+//  v1 render_wave   persistent loop, one pixel per lane, path regeneration.
+//  v0 render_pixels thread per pixel, samples in a plain loop (the first version).
+// v1 and v2 step every traversing lane through one BVH entry per iteration and shade
+// in batches: once `shade_thresh` lanes of the wave wait (or none traverses), all
+// waiting lanes shade together, so shading and its Philox blocks run in lockstep.
 #include <hip/hip_runtime.h>
 
 #include "rtx_device.h"
@@ -14,6 +22,26 @@
 
 namespace rtxd {
 
+__device__ __forceinline__ void flush_counters(const Params& p, uint64_t samples, const Counters& cnt) {
+    atomicAdd(&p.counters[0], (unsigned long long)samples);
+    atomicAdd(&p.counters[1], (unsigned long long)cnt.segments);
+    atomicAdd(&p.counters[2], (unsigned long long)cnt.node_visits);
+    atomicAdd(&p.counters[3], (unsigned long long)cnt.prim_tests);
+    atomicAdd(&p.counters[4], (unsigned long long)cnt.hits);
+    atomicAdd(&p.counters[5], (unsigned long long)cnt.texel_fetches);
+    atomicAdd(&p.counters[6], (unsigned long long)cnt.draws);
+}
+
+__device__ __forceinline__ void flush_sched(const Params& p, uint64_t wi, uint64_t ls, uint64_t sp, uint64_t sl) {
+    atomicAdd(&p.counters[8], (unsigned long long)wi);
+    atomicAdd(&p.counters[9], (unsigned long long)ls);
+    atomicAdd(&p.counters[10], (unsigned long long)sp);
+    atomicAdd(&p.counters[11], (unsigned long long)sl);
+}
+
+// ------------------------------------------------------------------------------------
+// v0: thread per pixel, samples in a loop, traversal from global memory.
+// ------------------------------------------------------------------------------------
 constexpr int TILE_W = 16;
 constexpr int TILE_H = 16;
 constexpr int BLOCK = TILE_W * TILE_H;
@@ -26,49 +54,422 @@ __global__ __launch_bounds__(BLOCK) void render_pixels(Params p) {
     const uint32_t x = p.x0 + lx;
     const uint32_t y = p.y0 + p.rank + lr * p.world;
     const rtx_camera& c = p.cam;
-
-    // camera.go:266-274: (pixel00 + du*i) + dv*j — the same for every sample.
-    const V3 base = add(add(v3(c.pixel00[0], c.pixel00[1], c.pixel00[2]),
-                            scale(v3(c.pixel_du[0], c.pixel_du[1], c.pixel_du[2]), (float)x)),
-                        scale(v3(c.pixel_dv[0], c.pixel_dv[1], c.pixel_dv[2]), (float)y));
-    const uint32_t pixel = y * c.image_width + x;
-
-    Counters cnt{0, 0, 0, 0, 0};
-    uint64_t draws = 0;
+    const V3 base = pixel_base(c, x, y);
+    PathRng rng{(uint32_t)p.seed, (uint32_t)(p.seed >> 32), y * c.image_width + x, 0};
+    Counters cnt{0, 0, 0, 0, 0, 0};
     V3 sum = v3(0.0f, 0.0f, 0.0f);
     for (uint32_t k = 0; k < c.samples_per_pixel; ++k) {
-        Rng rng;
-        rng.init(p.seed, pixel, k);
-        const Ray r = camera_ray(c, base, rng);
-        const V3 col = trace_path<COUNT>(p, r, rng, cnt);
-        sum = add(sum, col);  // camera.go:259
-        if (COUNT) draws += rng.n;
+        rng.sample = k;
+        Ray r = camera_ray(c, base, rng, cnt.draws);
+        V3 thr = v3(1.0f, 1.0f, 1.0f), acc = v3(0.0f, 0.0f, 0.0f), col = acc;
+        for (uint32_t seg = 0; seg < c.max_depth; ++seg) {  // ray.go:33 depth limit
+            if (COUNT) ++cnt.segments;
+            Trav t;
+            trav_begin(t, r);
+            while (t.i < p.n_entries) trav_step<COUNT>(t, r, p.entries, cnt);
+            if (shade<COUNT>(p, p.entries, t, seg, r, thr, acc, rng, cnt, col)) break;
+        }
+        sum = add(sum, col);  // camera.go:259 (col = 0 when the depth ran out)
     }
     const V3 avg = scale(sum, 1.0f / (float)c.samples_per_pixel);  // camera.go:261
     float* o = p.out + ((size_t)lr * p.width + lx) * 3;
     o[0] = avg.x;
     o[1] = avg.y;
     o[2] = avg.z;
+    if (COUNT) flush_counters(p, c.samples_per_pixel, cnt);
+}
 
+// ------------------------------------------------------------------------------------
+// v1: persistent wave loop, one pixel per lane, path regeneration, batched shading.
+// ------------------------------------------------------------------------------------
+constexpr int WAVE_BLOCK = 256;  // 4 waves, each an 8x8 pixel tile; block = 16x16 pixels
+enum : uint32_t { M_TRAV = 0, M_SHADE = 1, M_START = 2, M_DONE = 3 };
+
+template <bool COUNT, bool USE_LDS>
+__global__ __launch_bounds__(WAVE_BLOCK) void render_wave(Params p) {
+    extern __shared__ float4 lds_entries[];
+    const float4* __restrict__ E;
+    if constexpr (USE_LDS) {
+        const uint32_t n4 = 2 * p.n_entries;
+        for (uint32_t t = threadIdx.x; t < n4; t += WAVE_BLOCK) lds_entries[t] = p.entries[t];
+        __syncthreads();
+        E = lds_entries;
+    } else {
+        E = p.entries;
+    }
+    const uint32_t n_entries = p.n_entries;
+    const uint32_t thresh = p.shade_thresh;
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    const uint32_t lx = blockIdx.x * 16u + (wave & 1u) * 8u + (lane & 7u);
+    const uint32_t lr = blockIdx.y * 16u + (wave >> 1) * 8u + (lane >> 3);
+    const bool active = lx < p.width && lr < p.rows;
+    const uint32_t x = p.x0 + lx;
+    const uint32_t y = p.y0 + p.rank + lr * p.world;
+    const rtx_camera& c = p.cam;
+    const V3 base = pixel_base(c, x, y);
+    const uint32_t spp = c.samples_per_pixel;
+
+    uint32_t mode = active ? M_START : M_DONE;
+    uint32_t seg = 0;
+    V3 sum = v3(0.0f, 0.0f, 0.0f);
+    V3 thr = v3(1.0f, 1.0f, 1.0f), acc = v3(0.0f, 0.0f, 0.0f);
+    Ray r{v3(0, 0, 0), v3(0, 0, 0)};
+    PathRng rng{(uint32_t)p.seed, (uint32_t)(p.seed >> 32), y * c.image_width + x, 0};
+    Trav t{};
+    Counters cnt{0, 0, 0, 0, 0, 0};
+    uint64_t wave_iters = 0, lane_steps = 0, shade_phases = 0, shade_lanes = 0;
+
+    for (;;) {
+        for (;;) {  // traversal phase
+            if (mode == M_TRAV) {
+                trav_step<COUNT>(t, r, E, cnt);
+                if (t.i >= n_entries) mode = M_SHADE;
+            }
+            const uint64_t trav = __ballot(mode == M_TRAV);
+            const uint64_t pend = __ballot(mode == M_SHADE || mode == M_START);
+            if (COUNT) {
+                ++wave_iters;
+                lane_steps += (uint64_t)__popcll(trav);
+            }
+            if (trav == 0 || (uint32_t)__popcll(pend) >= thresh) {
+                if (COUNT) {
+                    ++shade_phases;
+                    shade_lanes += (uint64_t)__popcll(pend);
+                }
+                break;
+            }
+        }
+        if (__ballot(mode != M_DONE) == 0) break;
+
+        if (mode == M_SHADE || mode == M_START) {  // shading phase
+            bool new_sample = mode == M_START;
+            if (mode == M_SHADE) {
+                V3 color;
+                bool done = shade<COUNT>(p, E, t, seg, r, thr, acc, rng, cnt, color);
+                ++seg;
+                if (!done && seg == c.max_depth) {  // depth exhausted: GetColor(0) = 0 (ray.go:33)
+                    done = true;
+                    color = acc;
+                }
+                if (done) {
+                    sum = add(sum, color);  // camera.go:259
+                    ++rng.sample;
+                    new_sample = true;
+                }
+            }
+            if (new_sample) {
+                for (;;) {
+                    if (rng.sample >= spp) {
+                        mode = M_DONE;
+                        const V3 avg = scale(sum, 1.0f / (float)spp);  // camera.go:261
+                        float* o = p.out + ((size_t)lr * p.width + lx) * 3;
+                        o[0] = avg.x;
+                        o[1] = avg.y;
+                        o[2] = avg.z;
+                        break;
+                    }
+                    r = camera_ray(c, base, rng, cnt.draws);
+                    thr = v3(1.0f, 1.0f, 1.0f);
+                    acc = v3(0.0f, 0.0f, 0.0f);
+                    seg = 0;
+                    if (c.max_depth > 0) break;
+                    sum = add(sum, acc);  // max depth 0: GetColor returns black
+                    ++rng.sample;
+                }
+            }
+            if (mode != M_DONE) {  // begin a segment: world.Hit (ray.go:36)
+                if (COUNT) ++cnt.segments;
+                trav_begin(t, r);
+                mode = n_entries > 0 ? M_TRAV : M_SHADE;
+            }
+        }
+    }
     if (COUNT) {
-        atomicAdd(&p.counters[0], (unsigned long long)c.samples_per_pixel);
-        atomicAdd(&p.counters[1], (unsigned long long)cnt.segments);
-        atomicAdd(&p.counters[2], (unsigned long long)cnt.node_visits);
-        atomicAdd(&p.counters[3], (unsigned long long)cnt.prim_tests);
-        atomicAdd(&p.counters[4], (unsigned long long)cnt.hits);
-        atomicAdd(&p.counters[5], (unsigned long long)cnt.texel_fetches);
-        atomicAdd(&p.counters[6], (unsigned long long)draws);
+        flush_counters(p, active ? spp : 0, cnt);
+        if (lane == 0) flush_sched(p, wave_iters, lane_steps, shade_phases, shade_lanes);
     }
 }
 
-hipError_t launch_render(const Params& p, bool count, hipStream_t stream) {
-    if (p.width == 0 || p.rows == 0) return hipSuccess;
-    const dim3 grid((p.width + TILE_W - 1) / TILE_W, (p.rows + TILE_H - 1) / TILE_H);
-    if (count)
-        hipLaunchKernelGGL(render_pixels<true>, grid, dim3(BLOCK), 0, stream, p);
+// ------------------------------------------------------------------------------------
+// v2: persistent waves over a pool of pixels fed by a global tile queue.
+//
+// v1 keeps one pixel per lane, so a wave lasts as long as its most expensive pixel
+// (a sky pixel needs ~1 segment per sample, a glass one ~8).  v2 decouples lanes from
+// pixels: each wave owns CH chunks of 64 pixels (8x8 tiles of the region, taken from
+// a global atomic queue) = a pool of POOL_SLOTS pixels in LDS, each with its running
+// float32 sum and next sample index.  A free lane claims any idle pixel of the pool
+// and traces its next sample; a pixel has at most ONE sample in flight, so samples
+// still complete — and are summed — in order k = 0..spp-1 (camera.go:256-261).  When
+// all pixels of a chunk are done, the chunk is refilled from the queue.  The grid is
+// sized to the device's resident capacity; every wave exits once the queue is empty
+// and its chunks are finished, or when its watchdog fires.
+// ------------------------------------------------------------------------------------
+constexpr int POOL_BLOCK = 512;  // 8 waves share one LDS copy of the scene
+constexpr int POOL_WAVES = POOL_BLOCK / 64;
+enum : uint32_t { Q_TRAV = 0, Q_SHADE = 1, Q_FREE = 2, Q_IDLE = 3 };
+constexpr uint32_t ST_INFLIGHT = 0x80000000u, ST_INVALID = 0x40000000u, ST_K = 0x00FFFFFFu;
+
+template <int NCH>  // chunks (8x8 tiles) per wave
+struct WavePool {
+    static constexpr int SLOTS = NCH * 64;
+    float sx[SLOTS], sy[SLOTS], sz[SLOTS];
+    uint32_t st[SLOTS];        // next sample index | INFLIGHT | INVALID
+    int32_t tile[NCH];         // tile of the region held by chunk c, -1 = empty
+    uint32_t remaining[NCH];   // pixels of chunk c not finished yet
+    uint32_t origin[NCH];      // region x0 | y0 << 16 of the tile
+    uint32_t pad[NCH];
+};
+static_assert(sizeof(WavePool<2>) % 16 == 0 && sizeof(WavePool<4>) % 16 == 0, "keep the scene copy 16-B aligned");
+
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <bool COUNT, bool USE_LDS, int NCH>
+__global__ __launch_bounds__(POOL_BLOCK) void render_pool(Params p) {
+    using Pool = WavePool<NCH>;
+    constexpr uint32_t CH = NCH, POOL_SLOTS = Pool::SLOTS;
+    extern __shared__ float4 lds_dyn[];
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    Pool* wp = reinterpret_cast<Pool*>(lds_dyn) + wave;
+    const float4* __restrict__ E;
+    if constexpr (USE_LDS) {
+        float4* scene = lds_dyn + (POOL_WAVES * sizeof(Pool)) / 16;
+        const uint32_t n4 = 2 * p.n_entries;
+        for (uint32_t t = threadIdx.x; t < n4; t += POOL_BLOCK) scene[t] = p.entries[t];
+        E = scene;
+    } else {
+        E = p.entries;
+    }
+    const uint32_t n_entries = p.n_entries;
+    const uint32_t thresh = p.shade_thresh;
+    const rtx_camera& c = p.cam;
+    const uint32_t spp = c.samples_per_pixel;
+    const uint32_t tiles_x = (p.width + 7) / 8;
+    const uint32_t n_tiles = tiles_x * ((p.rows + 7) / 8);
+
+    // Take the next 8x8 tile of the region into chunk ch (wave-uniform call).
+    auto load_chunk = [&](uint32_t ch) {
+        uint32_t tl = 0;
+        if (lane == 0) tl = atomicAdd(p.tile_counter, 1u);
+        tl = __shfl(tl, 0);
+        const bool has = tl < n_tiles;
+        const uint32_t ox = (tl % tiles_x) * 8, oy = (tl / tiles_x) * 8;
+        const uint32_t lx = ox + (lane & 7u), lr = oy + (lane >> 3);
+        const bool valid = has && lx < p.width && lr < p.rows;
+        const uint32_t s = ch * 64 + lane;
+        wp->sx[s] = 0.0f;
+        wp->sy[s] = 0.0f;
+        wp->sz[s] = 0.0f;
+        wp->st[s] = valid ? 0u : ST_INVALID;
+        const uint32_t nvalid = (uint32_t)__popcll(__ballot(valid));
+        if (lane == 0) {
+            wp->tile[ch] = has ? (int32_t)tl : -1;
+            wp->remaining[ch] = nvalid;
+            wp->origin[ch] = ox | (oy << 16);
+        }
+    };
+    for (uint32_t ch = 0; ch < CH; ++ch) load_chunk(ch);
+    __syncthreads();  // scene copy + pool init visible
+
+    uint32_t mode = Q_FREE;
+    bool begin = false;  // set up a new segment at the end of this shading phase
+    uint32_t slot = 0, px = 0, py = 0, seg = 0;
+    uint32_t cursor = 0;  // wave-uniform claim cursor over the pool
+    V3 thr = v3(1.0f, 1.0f, 1.0f), acc = v3(0.0f, 0.0f, 0.0f);
+    Ray r{v3(0, 0, 0), v3(0, 0, 0)};
+    PathRng rng{(uint32_t)p.seed, (uint32_t)(p.seed >> 32), 0, 0};
+    Trav t{};
+    Counters cnt{0, 0, 0, 0, 0, 0};
+    uint64_t samples = 0;
+    uint64_t wave_iters = 0, lane_steps = 0, shade_phases = 0, shade_lanes = 0;
+    const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+    uint32_t iter = 0;
+
+    for (;;) {
+        // Watchdog: a wave never outlives p.watchdog_ticks (the grid always drains).
+        if ((++iter & 255u) == 0 && __builtin_amdgcn_s_memrealtime() - t_start > p.watchdog_ticks) {
+            if (lane == 0) atomicOr(p.error_flag, 1u);
+            break;
+        }
+        for (;;) {  // traversal phase
+            if (mode == Q_TRAV) {
+                trav_step<COUNT>(t, r, E, cnt);
+                if (t.i >= n_entries) mode = Q_SHADE;
+            }
+            const uint64_t trav = __ballot(mode == Q_TRAV);
+            const uint64_t pend = __ballot(mode == Q_SHADE || mode == Q_FREE);
+            if (COUNT) {
+                ++wave_iters;
+                lane_steps += (uint64_t)__popcll(trav);
+            }
+            if (trav == 0 || (uint32_t)__popcll(pend) >= thresh) {
+                if (COUNT) {
+                    ++shade_phases;
+                    shade_lanes += (uint64_t)__popcll(pend);
+                }
+                break;
+            }
+        }
+
+        // ---- shading phase: finish or continue paths ---------------------------------------
+        if (mode == Q_SHADE) {
+            V3 color = acc;
+            bool done = c.max_depth == 0;  // GetColor(0) returns black (ray.go:33-35)
+            if (!done) {
+                done = shade<COUNT>(p, E, t, seg, r, thr, acc, rng, cnt, color);
+                ++seg;
+                if (!done && seg == c.max_depth) {  // depth exhausted
+                    done = true;
+                    color = acc;
+                }
+            }
+            if (done) {  // sum += sample, in sample order (camera.go:259)
+                wp->sx[slot] = wp->sx[slot] + color.x;
+                wp->sy[slot] = wp->sy[slot] + color.y;
+                wp->sz[slot] = wp->sz[slot] + color.z;
+                const uint32_t kn = (wp->st[slot] & ST_K) + 1;
+                wp->st[slot] = kn;  // clears INFLIGHT
+                if (COUNT) ++samples;
+                if (kn == spp) {  // pixel complete: sum * (1/spp), camera.go:261
+                    const float inv = 1.0f / (float)spp;
+                    float* o = p.out + ((size_t)py * p.width + px) * 3;
+                    o[0] = wp->sx[slot] * inv;
+                    o[1] = wp->sy[slot] * inv;
+                    o[2] = wp->sz[slot] * inv;
+                    atomicSub(&wp->remaining[slot >> 6], 1u);
+                }
+                mode = Q_FREE;
+            } else {
+                mode = Q_TRAV;
+                begin = true;
+            }
+        }
+        wave_sync();
+
+        // ---- refill finished chunks from the global queue (wave-uniform) -------------------
+        bool any_chunk = false;
+        for (uint32_t ch = 0; ch < CH; ++ch) {
+            if (wp->tile[ch] >= 0 && wp->remaining[ch] == 0) {
+                load_chunk(ch);
+                wave_sync();
+            }
+            any_chunk |= wp->tile[ch] >= 0;
+        }
+        if (!any_chunk && __ballot(mode == Q_TRAV || mode == Q_SHADE) == 0) break;
+
+        // ---- claim idle pixels for free lanes ------------------------------------------------
+        const uint64_t freem = __ballot(mode == Q_FREE || mode == Q_IDLE);
+        if (mode == Q_FREE || mode == Q_IDLE) {
+            const uint32_t rank = (uint32_t)__popcll(freem & ((1ull << lane) - 1ull));
+            const uint32_t cand = (cursor + rank) % POOL_SLOTS;
+            const uint32_t st = wp->st[cand];
+            if ((st & (ST_INFLIGHT | ST_INVALID)) == 0 && (st & ST_K) < spp) {
+                wp->st[cand] = st | ST_INFLIGHT;
+                slot = cand;
+                const uint32_t org = wp->origin[cand >> 6];
+                const uint32_t j = cand & 63u;
+                px = (org & 0xFFFFu) + (j & 7u);
+                py = (org >> 16) + (j >> 3);
+                const uint32_t x = p.x0 + px, y = p.y0 + p.rank + py * p.world;
+                rng.pixel = y * c.image_width + x;
+                rng.sample = st & ST_K;
+                r = camera_ray(c, pixel_base(c, x, y), rng, cnt.draws);
+                thr = v3(1.0f, 1.0f, 1.0f);
+                acc = v3(0.0f, 0.0f, 0.0f);
+                seg = 0;
+                mode = Q_TRAV;
+                begin = true;
+                if (c.max_depth == 0) {
+                    mode = Q_SHADE;  // finishes black at the next shading phase
+                    begin = false;
+                }
+            } else {
+                mode = Q_IDLE;
+            }
+        }
+        cursor = (cursor + (uint32_t)__popcll(freem)) % POOL_SLOTS;
+
+        // ---- begin the next segment (world.Hit, ray.go:36) for lanes that just scattered
+        // or claimed a sample; lanes still mid-traversal keep their state ----------------------
+        if (begin) {
+            begin = false;
+            if (COUNT) ++cnt.segments;
+            trav_begin(t, r);
+            if (n_entries == 0) mode = Q_SHADE;
+        }
+    }
+
+    if (COUNT) {
+        flush_counters(p, samples, cnt);
+        if (lane == 0) flush_sched(p, wave_iters, lane_steps, shade_phases, shade_lanes);
+    }
+}
+
+// ------------------------------------------------------------------------------------
+// launches
+// ------------------------------------------------------------------------------------
+constexpr uint32_t LDS_MAX_BYTES = 64 * 1024;
+
+template <bool COUNT, int NCH>
+hipError_t launch_pool(const Params& p, bool use_lds, hipStream_t stream) {
+    const size_t shmem = POOL_WAVES * sizeof(WavePool<NCH>) + (use_lds ? (size_t)p.n_entries * 32 : 0);
+    int dev = 0, cus = 0, per_cu = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (e != hipSuccess) return e;
+    e = use_lds
+            ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, render_pool<COUNT, true, NCH>, POOL_BLOCK, shmem)
+            : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, render_pool<COUNT, false, NCH>, POOL_BLOCK, shmem);
+    if (e != hipSuccess) return e;
+    if (per_cu < 1) per_cu = 1;
+    const uint32_t tiles = ((p.width + 7) / 8) * ((p.rows + 7) / 8);
+    uint32_t blocks = (uint32_t)(per_cu * cus);
+    const uint32_t need = (tiles + POOL_WAVES * NCH - 1) / (POOL_WAVES * NCH);  // no wave starts empty-handed
+    if (blocks > need) blocks = need;
+    if (blocks == 0) blocks = 1;
+    e = hipMemsetAsync(p.tile_counter, 0, 2 * sizeof(uint32_t), stream);  // queue head + watchdog flag
+    if (e != hipSuccess) return e;
+    if (use_lds)
+        hipLaunchKernelGGL((render_pool<COUNT, true, NCH>), dim3(blocks), dim3(POOL_BLOCK), shmem, stream, p);
     else
-        hipLaunchKernelGGL(render_pixels<false>, grid, dim3(BLOCK), 0, stream, p);
+        hipLaunchKernelGGL((render_pool<COUNT, false, NCH>), dim3(blocks), dim3(POOL_BLOCK), shmem, stream, p);
     return hipGetLastError();
+}
+
+template <bool COUNT>
+hipError_t launch_wave(const Params& p, bool use_lds, hipStream_t stream) {
+    const dim3 grid((p.width + 15) / 16, (p.rows + 15) / 16);
+    if (use_lds) {
+        const size_t shmem = (size_t)p.n_entries * 32;
+        hipLaunchKernelGGL((render_wave<COUNT, true>), grid, dim3(WAVE_BLOCK), shmem, stream, p);
+    } else {
+        hipLaunchKernelGGL((render_wave<COUNT, false>), grid, dim3(WAVE_BLOCK), 0, stream, p);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_render(const Params& p, uint32_t flags, hipStream_t stream) {
+    if (p.width == 0 || p.rows == 0) return hipSuccess;
+    const bool count = (flags & RTX_FLAG_COUNTERS) != 0;
+    if (flags & RTX_FLAG_KERNEL_V0) {
+        const dim3 grid((p.width + TILE_W - 1) / TILE_W, (p.rows + TILE_H - 1) / TILE_H);
+        if (count)
+            hipLaunchKernelGGL(render_pixels<true>, grid, dim3(BLOCK), 0, stream, p);
+        else
+            hipLaunchKernelGGL(render_pixels<false>, grid, dim3(BLOCK), 0, stream, p);
+        return hipGetLastError();
+    }
+    const bool use_lds = !(flags & RTX_FLAG_NO_LDS) && (uint64_t)p.n_entries * 32 <= LDS_MAX_BYTES;
+    // v2 keeps tile origins in 16 bits: regions wider or taller than 65535 use v1.
+    if ((flags & RTX_FLAG_KERNEL_POOL) && p.width <= 0xFFFFu && p.rows <= 0xFFFFu) {
+        if (flags & RTX_FLAG_POOL4)
+            return count ? launch_pool<true, 4>(p, use_lds, stream) : launch_pool<false, 4>(p, use_lds, stream);
+        return count ? launch_pool<true, 2>(p, use_lds, stream) : launch_pool<false, 2>(p, use_lds, stream);
+    }
+    return count ? launch_wave<true>(p, use_lds, stream) : launch_wave<false>(p, use_lds, stream);
 }
 
 }  // namespace rtxd

@@ -97,7 +97,7 @@ static void philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1) {
 
 uint32_t Rand::Uint32() {
     const uint64_t blk = n_ >> 2;
-    uint32_t c[4] = {(uint32_t)blk, (uint32_t)(blk >> 32), 0u, stream_};
+    uint32_t c[4] = {(uint32_t)blk, (uint32_t)(blk >> 32), 0u, 0x80000000u | stream_};  // disjoint from pixel counters
     philox4x32_10(c, (uint32_t)seed_, (uint32_t)(seed_ >> 32));
     return c[n_++ & 3u];
 }

@@ -26,6 +26,14 @@ RTX_PRIM_QUAD = 1
 RTX_MAT_LAMBERTIAN, RTX_MAT_METAL, RTX_MAT_DIELECTRIC, RTX_MAT_DIFFUSE_LIGHT = 0, 1, 2, 3
 RTX_TEX_SOLID, RTX_TEX_CHECKERED, RTX_TEX_IMAGE, RTX_TEX_NOISE = 0, 1, 2, 3
 RTX_FLAG_COUNTERS = 1
+RTX_FLAG_KERNEL_V0 = 2
+RTX_FLAG_NO_LDS = 4
+RTX_FLAG_KERNEL_POOL = 8
+RTX_FLAG_POOL4 = 16
+
+
+def RTX_FLAG_SHADE_THRESH(n: int) -> int:
+    return (n & 0x7F) << 8
 
 
 def ref_prim(ptype: int, index: int) -> int:
@@ -82,7 +90,9 @@ class Region(ctypes.Structure):
 class Stats(ctypes.Structure):
     _fields_ = [("samples", c_uint64), ("segments", c_uint64), ("node_visits", c_uint64),
                 ("prim_tests", c_uint64), ("hits", c_uint64), ("texel_fetches", c_uint64),
-                ("rng_draws", c_uint64), ("kernel_ms", c_double), ("gather_ms", c_double)]
+                ("rng_draws", c_uint64), ("kernel_ms", c_double), ("gather_ms", c_double),
+                ("wave_iters", c_uint64), ("lane_steps", c_uint64), ("shade_phases", c_uint64),
+                ("shade_lanes", c_uint64)]
 
     def as_dict(self) -> dict:
         return {name: getattr(self, name) for name, _ in self._fields_}
@@ -226,12 +236,12 @@ class DeviceScene:
         return load().rtx_scene_device_bytes(self._h)
 
     def render_region(self, cam: Camera, seed: int, region: Region, out_ptr: int, stream: int = 0,
-                      counters: bool = False, timed: bool = False):
+                      counters: bool = False, timed: bool = False, flags: int = 0):
         """Enqueue (and optionally wait/time) a region render into device memory at out_ptr."""
         st = Stats() if (timed or counters) else None
         rc = load().rtx_render_region_device(self._h, ctypes.byref(cam), seed, ctypes.byref(region),
                                              c_void_p(out_ptr), c_void_p(stream),
-                                             RTX_FLAG_COUNTERS if counters else 0,
+                                             flags | (RTX_FLAG_COUNTERS if counters else 0),
                                              ctypes.byref(st) if st is not None else None)
         check(rc, "rtx_render_region_device")
         return st

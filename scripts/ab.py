@@ -1,0 +1,59 @@
+#!/usr/bin/env python3
+"""A/B kernel variants on one device, interleaved rounds in one process (guide §5.4 rule 24).
+
+  python scripts/ab.py [--width 1920] [--spp 100] [--rounds 3] [--variants v1,v0,nolds]
+Checks that every variant's image is bit-identical to the first one."""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "raytracer-go_amd"))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import rtx  # noqa: E402
+
+POOL = 8  # RTX_FLAG_KERNEL_POOL
+VARIANTS = {"v1": 0, "v2": POOL, "v0": rtx.RTX_FLAG_KERNEL_V0, "nolds": rtx.RTX_FLAG_NO_LDS, "p4": POOL | 16}
+for _t in (1, 4, 8, 12, 16, 20, 24, 32, 40, 48, 56, 64):
+    VARIANTS[f"t{_t}"] = _t << 8  # RTX_FLAG_SHADE_THRESH (v1)
+    VARIANTS[f"v2t{_t}"] = (_t << 8) | POOL
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--scene", default="random_spheres")
+ap.add_argument("--width", type=int, default=1920)
+ap.add_argument("--spp", type=int, default=100)
+ap.add_argument("--rounds", type=int, default=3)
+ap.add_argument("--variants", default="v1,v0")
+args = ap.parse_args()
+
+torch.cuda.set_device(0)
+scene = rtx.HostScene(args.scene, 1)
+cam = scene.camera(width=args.width, spp=args.spp)
+dev = rtx.DeviceScene(scene.desc)
+reg = rtx.Region(0, 0, cam.image_width, cam.image_height, 0, 1)
+names = args.variants.split(",")
+outs = {n: torch.zeros((cam.image_height, cam.image_width, 3), device="cuda") for n in names}
+stream = torch.cuda.current_stream().cuda_stream
+st = dev.render_region(cam, 1, reg, outs[names[0]].data_ptr(), stream, counters=True, timed=True)
+times = {n: [] for n in names}
+for rnd in range(args.rounds + 1):
+    for n in names:
+        s = dev.render_region(cam, 1, reg, outs[n].data_ptr(), stream, timed=True, flags=VARIANTS[n])
+        if rnd > 0:
+            times[n].append(s.kernel_ms)
+ref = outs[names[0]].cpu().numpy()
+for n in names:
+    same = np.array_equal(ref, outs[n].cpu().numpy())
+    med = float(np.median(times[n]))
+    print(f"{n:8s} median {med:9.2f} ms  min {min(times[n]):9.2f}  Gsamples/s {st.samples / med / 1e6:7.3f}  "
+          f"Mray/s {st.segments / med / 1e3:9.1f}  identical={same}", flush=True)
+# scheduling counters of each variant (a separate counting launch)
+for n in names:
+    c = dev.render_region(cam, 1, reg, outs[n].data_ptr(), stream, counters=True, timed=True, flags=VARIANTS[n])
+    if c.wave_iters:
+        print(f"{n:8s} trav-lane util {c.lane_steps / (64 * c.wave_iters):.3f}  iters/segment(wave) "
+              f"{c.wave_iters * 64 / c.segments:.1f}  entries/segment {(c.node_visits + c.prim_tests) / c.segments:.1f}"
+              f"  shade lanes/phase {c.shade_lanes / max(c.shade_phases, 1):.1f}  phases/wave-iter "
+              f"{c.shade_phases / c.wave_iters:.3f}", flush=True)

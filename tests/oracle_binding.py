@@ -50,8 +50,8 @@ def load():
     L = ctypes.CDLL(path)
     L.oracle_philox4x32_10.argtypes = [POINTER(c_uint32), POINTER(c_uint32), POINTER(c_uint32)]
     L.oracle_philox4x32_10.restype = None
-    L.oracle_pixel_draw.argtypes = [c_uint64, c_uint32, c_uint32, c_uint32]
-    L.oracle_pixel_draw.restype = c_float
+    L.oracle_pixel_block.argtypes = [c_uint64, c_uint32, c_uint32, c_uint32, c_uint32, POINTER(c_uint32)]
+    L.oracle_pixel_block.restype = None
     L.oracle_stream_u32.argtypes = [c_uint64, c_uint32, c_uint64]
     L.oracle_stream_u32.restype = c_uint32
     L.oracle_camera_defaults.argtypes = [POINTER(CameraOpts)]

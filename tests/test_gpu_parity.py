@@ -5,6 +5,8 @@ Stronger internal bar: bit-identical to the oracle's iterative colour order, and
 identical work counters (segments, node visits, primitive tests, hits, RNG draws),
 which pins every path decision.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -35,11 +37,11 @@ def dev_spheres(spheres, torch_cuda):
     return rtx.DeviceScene(spheres.desc)
 
 
-def gpu_region(torch, dev, cam, seed, reg, counters=True):
+def gpu_region(torch, dev, cam, seed, reg, counters=True, flags=0):
     rows = rtx.region_rows(reg)
     out = torch.full((max(rows, 1), max(reg.width, 1), 3), float("nan"), dtype=torch.float32, device="cuda")
     st = dev.render_region(cam, seed, reg, out.data_ptr(), torch.cuda.current_stream().cuda_stream,
-                           counters=counters, timed=True)
+                           counters=counters, timed=True, flags=flags)
     torch.cuda.synchronize()
     return out[:rows, : reg.width].cpu().numpy(), st
 
@@ -159,3 +161,94 @@ def test_full_c2_properties(torch_cuda, spheres, dev_spheres):
     assert np.array_equal(a, b)
     assert st.samples == 1920 * 1080 * 500
     assert 2.0 < st.segments / st.samples < 4.0
+
+
+KERNELS = {
+    "v1-wave": 0,
+    "v2-pool": rtx.RTX_FLAG_KERNEL_POOL,
+    "v2-pool4": rtx.RTX_FLAG_KERNEL_POOL | rtx.RTX_FLAG_POOL4,
+    "v0-pixels": rtx.RTX_FLAG_KERNEL_V0,
+    "v1-global-scene": rtx.RTX_FLAG_NO_LDS,
+    "v2-global-scene": rtx.RTX_FLAG_KERNEL_POOL | rtx.RTX_FLAG_NO_LDS,
+    "v1-thresh1": rtx.RTX_FLAG_SHADE_THRESH(1),
+    "v2-thresh64": rtx.RTX_FLAG_KERNEL_POOL | rtx.RTX_FLAG_SHADE_THRESH(64),
+}
+
+
+@pytest.mark.parametrize("name", list(KERNELS))
+def test_every_kernel_variant_is_bit_exact(torch_cuda, spheres, dev_spheres, name):
+    """All schedules (v0/v1/v2, LDS or global scene, any shading threshold) produce the
+    same bits and the same work counters as the oracle."""
+    cam = spheres.camera(width=120, spp=6, depth=50)
+    reg = rtx.Region(3, 2, 101, 53, 0, 1)
+    gpu, st = gpu_region(torch_cuda, dev_spheres, cam, 17, reg, flags=KERNELS[name])
+    check_parity(gpu, spheres.desc, cam, 17, reg, st)
+
+
+@pytest.mark.parametrize("name", ["v1-wave", "v2-pool"])
+def test_variant_shards(torch_cuda, spheres, dev_spheres, name):
+    cam = spheres.camera(width=96, spp=3)
+    full, _ = gpu_region(torch_cuda, dev_spheres, cam, 2, rtx.Region(0, 0, 96, cam.image_height, 0, 1),
+                         counters=False, flags=KERNELS[name])
+    reg = rtx.Region(0, 0, 96, cam.image_height, 1, 3)
+    part, _ = gpu_region(torch_cuda, dev_spheres, cam, 2, reg, counters=False, flags=KERNELS[name])
+    assert np.array_equal(full[1::3], part)
+
+
+def test_earth_image_texture_and_defocus(torch_cuda, built):
+    """Config 5 scene (synthetic 2048x1024 earth texture on a Lambertian sphere, 35 %
+    Dielectric, defocus 0.6): UV via Go's Acos/Atan2 restatement, texel fetch, edge
+    sentinel — bit-exact, texel fetches counted."""
+    scene = rtx.HostScene("earth_dielectric", 1)
+    dev = rtx.DeviceScene(scene.desc)
+    cam = scene.camera(width=384, spp=8, depth=50)
+    reg = rtx.Region(150, 70, 90, 60, 0, 1)  # the textured sphere is in the centre
+    gpu, st = gpu_region(torch_cuda, dev, cam, 5, reg)
+    check_parity(gpu, scene.desc, cam, 5, reg, st)
+    assert st.texel_fetches > 0
+
+
+def test_earth_scene_main_go(torch_cuda, built):
+    """main.go:80-104 earth scene (image texture only, no defocus)."""
+    scene = rtx.HostScene("earth", 1)
+    dev = rtx.DeviceScene(scene.desc)
+    cam = scene.camera(width=96, spp=4, depth=50)
+    reg = rtx.Region(0, 0, cam.image_width, cam.image_height, 0, 1)
+    gpu, st = gpu_region(torch_cuda, dev, cam, 1, reg)
+    check_parity(gpu, scene.desc, cam, 1, reg, st)
+    assert st.texel_fetches > 0
+
+
+def test_stress_100k_crop(torch_cuda, built):
+    """Config 4: 100k-sphere deep BVH (too big for LDS: global-memory traversal)."""
+    scene = rtx.HostScene("stress_100k", 1)
+    dev = rtx.DeviceScene(scene.desc)
+    assert dev.device_bytes() > 64 * 1024
+    cam = scene.camera(width=1920, spp=2, depth=50)
+    reg = rtx.Region(900, 500, 48, 24, 0, 1)
+    gpu, st = gpu_region(torch_cuda, dev, cam, 3, reg)
+    check_parity(gpu, scene.desc, cam, 3, reg, st)
+
+
+def test_watchdog_reports_error(torch_cuda, spheres):
+    """A persistent (v2) launch whose per-wave time limit is exceeded reports an error
+    instead of hanging (the limit is read once per process; exercised via a subprocess)."""
+    import subprocess
+    import sys
+
+    code = (
+        "import sys, torch; sys.path.insert(0, 'raytracer-go_amd'); import rtx\n"
+        "s = rtx.HostScene('random_spheres', 1); d = rtx.DeviceScene(s.desc); c = s.camera(width=400, spp=2000)\n"
+        "o = torch.empty((225, 400, 3), device='cuda')\n"
+        "try:\n"
+        "    d.render_region(c, 1, rtx.Region(0, 0, 400, 225, 0, 1), o.data_ptr(), 0, timed=True,"
+        " flags=rtx.RTX_FLAG_KERNEL_POOL)\n"
+        "    print('NOERROR')\n"
+        "except rtx.RtxError as e:\n"
+        "    print('ERR', e.code)\n"
+    )
+    env = dict(os.environ, RTX_WATCHDOG_S="0.02")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    res = subprocess.run([sys.executable, "-c", code], cwd=root, env=env, capture_output=True, text=True,
+                         timeout=120)
+    assert f"ERR {rtx.RTX_ERR_HIP}" in res.stdout, res.stdout + res.stderr

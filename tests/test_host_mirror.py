@@ -1,0 +1,146 @@
+"""The C++ mirror of the Go `internal` API (librtxhost.so): scene builders, NewBVH,
+flattening and the PPM writer, checked against the oracle's independent restatement."""
+import ctypes
+
+import numpy as np
+import pytest
+
+import oracle_binding as ob
+import rtx
+
+
+def tables(desc_ptr):
+    d = desc_ptr.contents
+    nodes = [(tuple(n.bmin), tuple(n.bmax), n.left, n.right) for n in d.nodes[: d.n_nodes]]
+    spheres = [(tuple(s.center), s.radius, s.material) for s in d.spheres[: d.n_spheres]]
+    mats = [(m.type, m.texture, m.fuzz, m.ior, tuple(m.albedo)) for m in d.materials[: d.n_materials]]
+    texs = [(t.type, t.scale, t.width, t.height, tuple(t.even), tuple(t.odd)) for t in d.textures[: d.n_textures]]
+    roots = list(d.roots[: d.n_roots])
+    return nodes, spheres, mats, texs, roots
+
+
+def preorder(desc_ptr):
+    """Walk the tree as bvh.go:220 does; yield node boxes and sphere payloads in visit order."""
+    nodes, spheres, mats, texs, roots = tables(desc_ptr)
+
+    def mat_payload(mi):
+        m = mats[mi]
+        tex = texs[m[1]] if m[0] in (rtx.RTX_MAT_LAMBERTIAN, rtx.RTX_MAT_DIFFUSE_LIGHT) else None
+        return (m[0], m[2], m[3], m[4], tex)
+
+    out = []
+    stack = list(reversed(roots))
+    while stack:
+        r = stack.pop()
+        if r >= 0:
+            bmin, bmax, left, right = nodes[r]
+            out.append(("node", bmin, bmax, left == right))
+            stack.append(right)
+            stack.append(left)
+        else:
+            c, rad, mi = spheres[(~r) & 0x0FFFFFFF]
+            out.append(("sphere", c, rad, mat_payload(mi)))
+    return out
+
+
+def test_random_spheres_matches_oracle_builder(built):
+    """main.go:227-289 + NewBVH (bvh.go:142-185): two independent restatements (C++
+    mirror, C oracle) agree on every box, sphere and material in traversal order."""
+    host = rtx.HostScene("random_spheres", 1)
+    orc = ob.OracleScene(1)
+    a, b = preorder(host.desc), preorder(orc.desc)
+    assert len(a) == len(b) > 900
+    assert a == b
+
+
+@pytest.mark.parametrize("seed", [2, 99])
+def test_random_spheres_other_seeds(built, seed):
+    assert preorder(rtx.HostScene("random_spheres", seed).desc) == preorder(ob.OracleScene(seed).desc)
+
+
+def go_min(a, b):
+    return min(a, b)
+
+
+def test_bvh_invariants(built):
+    host = rtx.HostScene("random_spheres", 1)
+    nodes, spheres, mats, texs, roots = tables(host.desc)
+    assert len(roots) == 1 and roots[0] == 0
+    seen = set()
+
+    def box(ref):
+        if ref >= 0:
+            return nodes[ref][0], nodes[ref][1]
+        c, r, _ = spheres[(~ref) & 0x0FFFFFFF]
+        cf = np.array(c, dtype=np.float32)
+        rf = np.float32(r)
+        return tuple(cf + (-rf)), tuple(cf + rf)
+
+    for i, (bmin, bmax, left, right) in enumerate(nodes):
+        for ref in (left, right):
+            if ref < 0:
+                seen.add((~ref) & 0x0FFFFFFF)
+        if left == right:
+            assert left < 0, "only a one-element split repeats its child (bvh.go:162-165)"
+        lb, rb = box(left), box(right)
+        for k in range(3):  # NewAabbFromBoxes, bvh.go:44-50
+            assert bmin[k] == min(lb[0][k], rb[0][k])
+            assert bmax[k] == max(lb[1][k], rb[1][k])
+    assert seen == set(range(len(spheres)))
+    # 485 spheres: a binary tree with n leaves plus the singleton splits.
+    assert len(nodes) >= len(spheres) - 1
+
+
+def test_materials_and_textures_deduplicated(built):
+    host = rtx.HostScene("random_spheres", 1)
+    nodes, spheres, mats, texs, roots = tables(host.desc)
+    assert len(mats) == len(spheres)  # every main.go sphere gets its own material
+    checkers = [t for t in texs if t[0] == rtx.RTX_TEX_CHECKERED]
+    assert len(checkers) == 1 and abs(checkers[0][1] - 0.32) < 1e-7
+
+
+def test_stress_and_earth_scenes_build(built):
+    s = rtx.HostScene("stress_100k", 1).desc.contents
+    assert s.n_spheres == 100001
+    e = rtx.HostScene("earth_dielectric", 1).desc.contents
+    imgs = [t for t in e.textures[: e.n_textures] if t.type == rtx.RTX_TEX_IMAGE]
+    assert len(imgs) == 1 and (imgs[0].width, imgs[0].height) == (2048, 1024)
+    assert e.n_texels == 2048 * 1024
+    diel = sum(1 for m in e.materials[: e.n_materials] if m.type == rtx.RTX_MAT_DIELECTRIC)
+    assert diel >= 0.3 * e.n_spheres - 2
+
+
+def test_camera_overrides(built):
+    host = rtx.HostScene("random_spheres", 1)
+    c = host.camera(width=1920, spp=500, depth=50)
+    assert (c.image_width, c.image_height, c.samples_per_pixel, c.max_depth) == (1920, 1080, 500, 50)
+    c2 = host.camera()
+    assert (c2.image_width, c2.samples_per_pixel) == (400, 500)  # main.go:228-231
+
+
+def test_ppm_encode_matches_oracle(built):
+    rng = np.random.default_rng(1)
+    img = rng.uniform(-0.1, 1.3, size=(3, 5, 3)).astype(np.float32)
+    img[0, 0] = [0.0, 1.0, 0.5]
+    img[1, 2] = [float("nan"), 4.0, 1e-12]
+    body = rtx.ppm_encode(img).decode()
+    lines = body.split("\n")
+    assert lines[-1] == "" and len(lines) == 16
+    for k, px in enumerate(img.reshape(-1, 3)):
+        assert lines[k] == ob.ppm_pixel(px)
+
+
+def test_render_ppm_without_gpu_fails_cleanly(built, tmp_path):
+    if rtx.load().rtx_device_count() > 0:
+        pytest.skip("a GPU is visible")
+    H = rtx.load_host()
+    out = tmp_path / "img.ppm"
+    rc = H.rtxhost_render_ppm(b"random_spheres", 1, 32, 2, 5, 1, 1, str(out).encode())
+    assert rc != 0 and H.rtxhost_last_error()
+    # the header was written before the device call failed, as camera.go:183-191 does
+    assert out.read_bytes().startswith(b"P3\n32 18\n255\n")
+
+
+def test_unknown_scene(built):
+    with pytest.raises(rtx.RtxError):
+        rtx.HostScene("cornell_box_unknown", 1)
