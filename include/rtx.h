@@ -207,6 +207,10 @@ typedef struct rtx_stats {
 /* Tuning: lanes of a wave that must wait before it shades (1..64; 0 = default, or the
  * RTX_SHADE_THRESH environment variable). */
 #define RTX_FLAG_SHADE_THRESH(n) (((uint32_t)(n)&0x7Fu) << 8)
+/* Tuning: geometry of the wave kernel: waves per block and BVH steps per lane between
+ * two wave votes (0 = 4 waves/3 steps (default), 1 = 4/1, 2 = 4/2, 3 = 4/4, 4 = 8/3,
+ * 5 = 8/3 with a >= 8 waves/SIMD register budget, 6 = 16/3). */
+#define RTX_FLAG_WAVE_GEOM(n) (((uint32_t)(n)&7u) << 24)
 
 typedef struct rtx_scene rtx_scene;
 

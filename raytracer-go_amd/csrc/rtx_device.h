@@ -300,6 +300,10 @@ __device__ __forceinline__ void trav_step(Trav& t, const Ray& r, const float4* _
     const float tmin = 0.001f;  // ray.go:37
     const float4 ea = E[2 * t.i];
     const float4 eb = E[2 * t.i + 1];
+    // Both halves are consumed here, so the whole entry arrives in one round trip (two
+    // ds_read_b128); otherwise the compiler sinks the node-only dwords into the box branch
+    // behind a second, dependent LDS read.
+    asm volatile("" ::"v"(ea.x), "v"(ea.y), "v"(ea.z), "v"(ea.w), "v"(eb.x), "v"(eb.y), "v"(eb.z), "v"(eb.w));
     if (__float_as_int(eb.w) == RTX_E_NODE) {
         if (COUNT) ++cnt.node_visits;
         // Per axis: t0 = (min - o) * invD, t1 = (max - o) * invD, swapped if invD < 0

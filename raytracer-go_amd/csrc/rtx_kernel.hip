@@ -8,9 +8,9 @@
 // the region, the scheduling or the number of GPUs.
 //
 // Three schedules of the same per-sample code (rtx_device.h), identical output:
-//  v2 render_pool   (default) persistent waves over a pool of pixels fed by a global
-//                   tile queue; lanes take any idle pixel of the pool.
-//  v1 render_wave   persistent loop, one pixel per lane, path regeneration.
+//  v1 render_wave   (default) persistent loop, one pixel per lane, path regeneration.
+//  v2 render_pool   persistent waves over a pool of pixels fed by a global tile queue;
+//                   lanes take any idle pixel of the pool (RTX_FLAG_KERNEL_POOL).
 //  v0 render_pixels thread per pixel, samples in a plain loop (the first version).
 // v1 and v2 step every traversing lane through one BVH entry per iteration and shade
 // in batches: once `shade_thresh` lanes of the wave wait (or none traverses), all
@@ -80,13 +80,54 @@ __global__ __launch_bounds__(BLOCK) void render_pixels(Params p) {
 }
 
 // ------------------------------------------------------------------------------------
+// Traversal phase shared by v1 and v2.  Lane modes: 0 = traversing, 1 and 2 = waiting
+// for the shading phase, 3 = neither.  Runs BVH steps until at least `thresh` lanes
+// wait or none traverses.  Each traversing lane takes one entry (box or sphere, by its
+// tag) per iteration.  (Separate box and sphere batches, steered by link-type bits in
+// the entries, were measured: the extra decode per step cost more than the reduced
+// divergence saved, DESIGN.md.)
+// ------------------------------------------------------------------------------------
+// STEPS > 1 takes up to STEPS entries per lane between two wave votes.
+template <bool COUNT, int STEPS = 1>
+__device__ __forceinline__ void traverse_phase(uint32_t& mode, Trav& t, const Ray& r, const float4* __restrict__ E,
+                                               uint32_t n_entries, uint32_t thresh, Counters& cnt,
+                                               uint64_t& wave_iters, uint64_t& lane_steps, uint64_t& shade_phases,
+                                               uint64_t& shade_lanes) {
+    for (;;) {
+#pragma unroll
+        for (int s = 0; s < STEPS; ++s) {
+            if (mode == 0) {
+                trav_step<COUNT>(t, r, E, cnt);
+                if (t.i >= n_entries) mode = 1;
+            }
+        }
+        const uint64_t trav = __ballot(mode == 0);
+        const uint64_t pend = __ballot(mode == 1 || mode == 2);
+        if (COUNT) {
+            ++wave_iters;
+            lane_steps += (uint64_t)__popcll(trav);
+        }
+        if (trav == 0 || (uint32_t)__popcll(pend) >= thresh) {
+            if (COUNT) {
+                ++shade_phases;
+                shade_lanes += (uint64_t)__popcll(pend);
+            }
+            return;
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------
 // v1: persistent wave loop, one pixel per lane, path regeneration, batched shading.
 // ------------------------------------------------------------------------------------
-constexpr int WAVE_BLOCK = 256;  // 4 waves, each an 8x8 pixel tile; block = 16x16 pixels
 enum : uint32_t { M_TRAV = 0, M_SHADE = 1, M_START = 2, M_DONE = 3 };
 
-template <bool COUNT, bool USE_LDS>
-__global__ __launch_bounds__(WAVE_BLOCK) void render_wave(Params p) {
+// BLOCK = 64 * WX * WY threads: a WX x WY grid of waves, each an 8x8 pixel tile; one LDS
+// copy of the scene per block.  MINW = minimum waves per SIMD requested from the
+// register allocator (0 = compiler's choice).  STEPS: entries per lane between votes.
+template <bool COUNT, bool USE_LDS, int WX, int WY, int MINW, int STEPS>
+__global__ __launch_bounds__(64 * WX * WY, MINW) void render_wave(Params p) {
+    constexpr uint32_t WAVE_BLOCK = 64 * WX * WY;
     extern __shared__ float4 lds_entries[];
     const float4* __restrict__ E;
     if constexpr (USE_LDS) {
@@ -100,8 +141,8 @@ __global__ __launch_bounds__(WAVE_BLOCK) void render_wave(Params p) {
     const uint32_t n_entries = p.n_entries;
     const uint32_t thresh = p.shade_thresh;
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-    const uint32_t lx = blockIdx.x * 16u + (wave & 1u) * 8u + (lane & 7u);
-    const uint32_t lr = blockIdx.y * 16u + (wave >> 1) * 8u + (lane >> 3);
+    const uint32_t lx = blockIdx.x * (8u * WX) + (wave % WX) * 8u + (lane & 7u);
+    const uint32_t lr = blockIdx.y * (8u * WY) + (wave / WX) * 8u + (lane >> 3);
     const bool active = lx < p.width && lr < p.rows;
     const uint32_t x = p.x0 + lx;
     const uint32_t y = p.y0 + p.rank + lr * p.world;
@@ -120,25 +161,8 @@ __global__ __launch_bounds__(WAVE_BLOCK) void render_wave(Params p) {
     uint64_t wave_iters = 0, lane_steps = 0, shade_phases = 0, shade_lanes = 0;
 
     for (;;) {
-        for (;;) {  // traversal phase
-            if (mode == M_TRAV) {
-                trav_step<COUNT>(t, r, E, cnt);
-                if (t.i >= n_entries) mode = M_SHADE;
-            }
-            const uint64_t trav = __ballot(mode == M_TRAV);
-            const uint64_t pend = __ballot(mode == M_SHADE || mode == M_START);
-            if (COUNT) {
-                ++wave_iters;
-                lane_steps += (uint64_t)__popcll(trav);
-            }
-            if (trav == 0 || (uint32_t)__popcll(pend) >= thresh) {
-                if (COUNT) {
-                    ++shade_phases;
-                    shade_lanes += (uint64_t)__popcll(pend);
-                }
-                break;
-            }
-        }
+        traverse_phase<COUNT, STEPS>(mode, t, r, E, n_entries, thresh, cnt, wave_iters, lane_steps, shade_phases,
+                                     shade_lanes);
         if (__ballot(mode != M_DONE) == 0) break;
 
         if (mode == M_SHADE || mode == M_START) {  // shading phase
@@ -294,25 +318,8 @@ __global__ __launch_bounds__(POOL_BLOCK) void render_pool(Params p) {
             if (lane == 0) atomicOr(p.error_flag, 1u);
             break;
         }
-        for (;;) {  // traversal phase
-            if (mode == Q_TRAV) {
-                trav_step<COUNT>(t, r, E, cnt);
-                if (t.i >= n_entries) mode = Q_SHADE;
-            }
-            const uint64_t trav = __ballot(mode == Q_TRAV);
-            const uint64_t pend = __ballot(mode == Q_SHADE || mode == Q_FREE);
-            if (COUNT) {
-                ++wave_iters;
-                lane_steps += (uint64_t)__popcll(trav);
-            }
-            if (trav == 0 || (uint32_t)__popcll(pend) >= thresh) {
-                if (COUNT) {
-                    ++shade_phases;
-                    shade_lanes += (uint64_t)__popcll(pend);
-                }
-                break;
-            }
-        }
+        traverse_phase<COUNT, 3>(mode, t, r, E, n_entries, thresh, cnt, wave_iters, lane_steps, shade_phases,
+                                 shade_lanes);
 
         // ---- shading phase: finish or continue paths ---------------------------------------
         if (mode == Q_SHADE) {
@@ -439,16 +446,30 @@ hipError_t launch_pool(const Params& p, bool use_lds, hipStream_t stream) {
     return hipGetLastError();
 }
 
-template <bool COUNT>
-hipError_t launch_wave(const Params& p, bool use_lds, hipStream_t stream) {
-    const dim3 grid((p.width + 15) / 16, (p.rows + 15) / 16);
+template <bool COUNT, int WX, int WY, int MINW, int STEPS = 1>
+hipError_t launch_wave_geom(const Params& p, bool use_lds, hipStream_t stream) {
+    const dim3 grid((p.width + 8 * WX - 1) / (8 * WX), (p.rows + 8 * WY - 1) / (8 * WY));
     if (use_lds) {
         const size_t shmem = (size_t)p.n_entries * 32;
-        hipLaunchKernelGGL((render_wave<COUNT, true>), grid, dim3(WAVE_BLOCK), shmem, stream, p);
+        hipLaunchKernelGGL((render_wave<COUNT, true, WX, WY, MINW, STEPS>), grid, dim3(64 * WX * WY), shmem, stream, p);
     } else {
-        hipLaunchKernelGGL((render_wave<COUNT, false>), grid, dim3(WAVE_BLOCK), 0, stream, p);
+        hipLaunchKernelGGL((render_wave<COUNT, false, WX, WY, MINW, STEPS>), grid, dim3(64 * WX * WY), 0, stream, p);
     }
     return hipGetLastError();
+}
+
+// Block geometry of v1 (RTX_FLAG_WAVE_GEOM): waves per block and the register budget.
+template <bool COUNT>
+hipError_t launch_wave(const Params& p, uint32_t geom, bool use_lds, hipStream_t stream) {
+    switch (geom) {
+    case 1: return launch_wave_geom<COUNT, 2, 2, 0, 1>(p, use_lds, stream);  // 256 threads, 1 step per vote
+    case 2: return launch_wave_geom<COUNT, 2, 2, 0, 2>(p, use_lds, stream);  // 256, 2 steps
+    case 3: return launch_wave_geom<COUNT, 2, 2, 0, 4>(p, use_lds, stream);  // 256, 4 steps
+    case 4: return launch_wave_geom<COUNT, 4, 2, 0, 3>(p, use_lds, stream);  // 512, 3 steps
+    case 5: return launch_wave_geom<COUNT, 4, 2, 8, 3>(p, use_lds, stream);  // 512, >= 8 waves/SIMD, 3 steps
+    case 6: return launch_wave_geom<COUNT, 4, 4, 0, 3>(p, use_lds, stream);  // 1024, 3 steps
+    default: return launch_wave_geom<COUNT, 2, 2, 0, 3>(p, use_lds, stream); // 256, 3 steps
+    }
 }
 
 hipError_t launch_render(const Params& p, uint32_t flags, hipStream_t stream) {
@@ -469,7 +490,8 @@ hipError_t launch_render(const Params& p, uint32_t flags, hipStream_t stream) {
             return count ? launch_pool<true, 4>(p, use_lds, stream) : launch_pool<false, 4>(p, use_lds, stream);
         return count ? launch_pool<true, 2>(p, use_lds, stream) : launch_pool<false, 2>(p, use_lds, stream);
     }
-    return count ? launch_wave<true>(p, use_lds, stream) : launch_wave<false>(p, use_lds, stream);
+    const uint32_t geom = (flags >> 24) & 7u;
+    return count ? launch_wave<true>(p, geom, use_lds, stream) : launch_wave<false>(p, geom, use_lds, stream);
 }
 
 }  // namespace rtxd

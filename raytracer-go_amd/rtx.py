@@ -36,6 +36,10 @@ def RTX_FLAG_SHADE_THRESH(n: int) -> int:
     return (n & 0x7F) << 8
 
 
+def RTX_FLAG_WAVE_GEOM(n: int) -> int:
+    return (n & 7) << 24
+
+
 def ref_prim(ptype: int, index: int) -> int:
     """RTX_REF_PRIM: ~((type << 28) | index) as int32."""
     v = ((ptype << 28) | (index & 0x0FFFFFFF)) & 0xFFFFFFFF
@@ -120,7 +124,7 @@ def load() -> ctypes.CDLL:
     global _lib
     if _lib is not None:
         return _lib
-    path = lib_path("librtx.so")
+    path = os.environ.get("RTX_LIB") or lib_path("librtx.so")  # RTX_LIB: A/B against another build
     if not os.path.exists(path):
         raise OSError(f"librtx.so not built at {path}: run __graft_entry__.build() (no CPU fallback exists)")
     L = ctypes.CDLL(path)

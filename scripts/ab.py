@@ -16,6 +16,8 @@ import rtx  # noqa: E402
 
 POOL = 8  # RTX_FLAG_KERNEL_POOL
 VARIANTS = {"v1": 0, "v2": POOL, "v0": rtx.RTX_FLAG_KERNEL_V0, "nolds": rtx.RTX_FLAG_NO_LDS, "p4": POOL | 16}
+for _g in range(8):
+    VARIANTS[f"g{_g}"] = rtx.RTX_FLAG_WAVE_GEOM(_g)
 for _t in (1, 4, 8, 12, 16, 20, 24, 32, 40, 48, 56, 64):
     VARIANTS[f"t{_t}"] = _t << 8  # RTX_FLAG_SHADE_THRESH (v1)
     VARIANTS[f"v2t{_t}"] = (_t << 8) | POOL
@@ -34,6 +36,11 @@ cam = scene.camera(width=args.width, spp=args.spp)
 dev = rtx.DeviceScene(scene.desc)
 reg = rtx.Region(0, 0, cam.image_width, cam.image_height, 0, 1)
 names = args.variants.split(",")
+for n in names:  # "a+b" = the flags of a and b together
+    if "+" in n:
+        VARIANTS[n] = 0
+        for part in n.split("+"):
+            VARIANTS[n] |= VARIANTS[part]
 outs = {n: torch.zeros((cam.image_height, cam.image_width, 3), device="cuda") for n in names}
 stream = torch.cuda.current_stream().cuda_stream
 st = dev.render_region(cam, 1, reg, outs[names[0]].data_ptr(), stream, counters=True, timed=True)
