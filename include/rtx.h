@@ -195,6 +195,8 @@ typedef struct rtx_stats {
     uint64_t lane_steps;   /* lanes stepping a BVH entry, summed over iterations     */
     uint64_t shade_phases; /* shading phases, summed over waves                      */
     uint64_t shade_lanes;  /* lanes shaded or claiming, summed over shading phases   */
+    uint64_t trav_cycles;  /* v1: shader cycles (s_memtime) in traversal, summed over waves */
+    uint64_t shade_cycles; /* v1: shader cycles in shading phases, summed over waves  */
 } rtx_stats;
 
 #define RTX_FLAG_COUNTERS 1u /* count work units (separate kernel instantiation) */

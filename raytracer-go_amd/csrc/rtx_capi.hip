@@ -297,6 +297,8 @@ int collect_on(DeviceCopy* c, bool count, uint64_t samples, rtx_stats* st) {
     st->lane_steps = h[9];
     st->shade_phases = h[10];
     st->shade_lanes = h[11];
+    st->trav_cycles = h[12];
+    st->shade_cycles = h[13];
     st->kernel_ms = ms;
     return RTX_OK;
 }

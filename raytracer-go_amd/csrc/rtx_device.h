@@ -146,14 +146,16 @@ __device__ __forceinline__ U4 philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c
             k0 += 0x9E3779B9u;
             k1 += 0xBB67AE85u;
         }
-        const uint32_t lo0 = 0xD2511F53u * c0, hi0 = __umulhi(0xD2511F53u, c0);
-        const uint32_t lo1 = 0xCD9E8D57u * c2, hi1 = __umulhi(0xCD9E8D57u, c2);
-        const uint32_t n0 = hi1 ^ c1 ^ k0;
-        const uint32_t n2 = hi0 ^ c3 ^ k1;
+        // One 32x32->64 product per word pair: a single v_mad_u64_u32 (quarter rate)
+        // instead of v_mul_lo_u32 + v_mul_hi_u32 (two quarter-rate instructions).
+        const uint64_t p0 = (uint64_t)0xD2511F53u * c0;
+        const uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
+        const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
+        const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
         c0 = n0;
-        c1 = lo1;
+        c1 = (uint32_t)p1;
         c2 = n2;
-        c3 = lo0;
+        c3 = (uint32_t)p0;
     }
     return U4{c0, c1, c2, c3};
 }
@@ -177,6 +179,17 @@ __device__ __forceinline__ V3 rand_unit_on_sphere(const PathRng& rng, uint32_t e
         if (lensq(v) < 1.0f) return unit(v);
         b = rng.block(e, a);
     }
+}
+
+// The scatter sample of one shading phase, drawn by the whole wave (coop_scatter).
+struct Scatter {
+    V3 s;            // unit vector on the sphere (Lambertian / Metal lanes)
+    uint32_t u0;     // word 0 of block (e, 0): Dielectric's uniform
+    uint32_t draws;  // rand draws NewVec3UnitRandOnUnitSphere32 made (3 per attempt)
+};
+
+__device__ __forceinline__ uint32_t lane_pull(uint32_t src_lane, uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src_lane * 4u), (int)v);
 }
 
 // ---------------------------------------------------------------------------------
@@ -270,6 +283,73 @@ __device__ __forceinline__ V3 texture_value(const Params& p, uint32_t ti, float 
               (float)(((px >> 16) & 0xFFu) * 257u) * cs);
 }
 
+// Wave-cooperative rejection sampling for NewVec3UnitRandOnUnitSphere32 (vec3.go:182-190).
+// Must be called by the whole wave (converged).  A lane with hit >= 0 draws block (e, 0);
+// its words 0-2 are attempt 0 of the unit-sphere loop.  The loop's result is the FIRST
+// accepted attempt a, attempt a being words 0-2 of block (e, a) — a pure function of the
+// counter, so any lane can evaluate any lane's attempt.  Instead of every lane looping
+// until the unluckiest one accepts (acceptance pi/6 per attempt: ~6-7 rounds for 40
+// lanes), the n lanes still rejecting get 64/n consecutive lanes each, which evaluate
+// attempts base .. base+64/n-1 of that owner in one round; the owner takes the first
+// accepted one.  Same attempt, same bits, about 3 Philox rounds per phase.
+__device__ __forceinline__ Scatter coop_scatter(const Params& p, const float4* __restrict__ E, const PathRng& rng,
+                                                uint32_t e, int32_t hit) {
+    Scatter out{v3(0.0f, 0.0f, 0.0f), 0u, 0u};
+    bool need = false;
+    float x = 0.0f, y = 0.0f, z = 0.0f;
+    if (hit >= 0) {
+        const U4 b0 = rng.block(e, 0);
+        const uint32_t mi = (uint32_t)__float_as_int(E[2 * hit + 1].w);
+        const uint32_t ty = p.materials[mi].type;
+        need = ty == RTX_MAT_LAMBERTIAN || ty == RTX_MAT_METAL;
+        out.u0 = b0.x;
+        x = signed_unit(b0.x);
+        y = signed_unit(b0.y);
+        z = signed_unit(b0.z);
+    }
+    uint32_t att = 0;
+    uint64_t pend = __ballot(need && !(x * x + y * y + z * z < 1.0f));  // lensq(v) < 1
+    const uint32_t lane = __lane_id();
+    const uint64_t below_mask = (1ull << lane) - 1ull;
+    for (uint32_t base = 1; pend != 0;) {
+        const uint32_t np = (uint32_t)__popcll(pend);
+        const uint32_t K = 64u / np;  // attempts per owner this round
+        const bool mine = (pend >> lane) & 1ull;
+        const uint32_t below = (uint32_t)__popcll(pend & below_mask);
+        // Lane q (< np) learns the lane id of the q-th pending lane (a permutation push).
+        const uint32_t dst = mine ? below : np + (lane - below);
+        const uint32_t owner_of = (uint32_t)__builtin_amdgcn_ds_permute((int)(dst * 4u), (int)lane);
+        const uint32_t q = lane / K, k = lane - q * K;
+        const bool slot = q < np;
+        const uint32_t owner = lane_pull(slot ? q : 0u, owner_of);
+        const uint32_t opix = lane_pull(owner, rng.pixel), osmp = lane_pull(owner, rng.sample);
+        const uint32_t oe = lane_pull(owner, e);
+        const U4 b = philox4x32_10(opix, osmp, oe, base + k, rng.k0, rng.k1);
+        const float bx = signed_unit(b.x), by = signed_unit(b.y), bz = signed_unit(b.z);
+        const uint64_t good = __ballot(slot && bx * bx + by * by + bz * bz < 1.0f);
+        const uint64_t kmask = K >= 64u ? ~0ull : ((1ull << K) - 1ull);
+        const uint64_t mine_good = mine ? ((good >> (below * K)) & kmask) : 0ull;
+        const uint32_t kk = mine_good ? (uint32_t)__builtin_ctzll(mine_good) : 0u;
+        const uint32_t src = mine_good ? below * K + kk : lane;
+        const float fx = __int_as_float((int)lane_pull(src, __float_as_uint(bx)));
+        const float fy = __int_as_float((int)lane_pull(src, __float_as_uint(by)));
+        const float fz = __int_as_float((int)lane_pull(src, __float_as_uint(bz)));
+        if (mine_good) {
+            x = fx;
+            y = fy;
+            z = fz;
+            att = base + kk;
+        }
+        pend = __ballot(mine && !mine_good);
+        base += K;
+    }
+    if (need) {
+        out.s = unit(v3(x, y, z));
+        out.draws = 3u * (att + 1u);
+    }
+    return out;
+}
+
 // One step of the closest-hit walk over the threaded pre-order layout (rtx_layout.h):
 // entry i is a node (Aabb.Hit, bvh.go:52-61, 84-102) or a sphere (Sphere.Hit,
 // hittables.go:96-116).  The sequence of steps is the reference recursion's, with
@@ -348,14 +428,17 @@ __device__ __forceinline__ void trav_step(Trav& t, const Ray& r, const float4* _
 // segment.  Lockstep RNG: every hitting lane evaluates block (seg+1, 0) first.
 template <bool COUNT>
 __device__ __forceinline__ bool shade(const Params& p, const float4* __restrict__ E, const Trav& t, uint32_t seg,
-                                      Ray& r, V3& thr, V3& acc, const PathRng& rng, Counters& cnt, V3& color) {
+                                      Ray& r, V3& thr, V3& acc, const PathRng& rng, Counters& cnt, V3& color,
+                                      const Scatter* pre = nullptr) {
     if (t.hit < 0) {  // miss: background (ray.go:52)
         color = add(acc, mul(thr, v3(p.cam.background[0], p.cam.background[1], p.cam.background[2])));
         return true;
     }
     if (COUNT) ++cnt.hits;
     const uint32_t e = seg + 1;
-    const U4 b0 = rng.block(e, 0);
+    U4 b0{0u, 0u, 0u, 0u};
+    if (pre) b0.x = pre->u0;  // drawn by coop_scatter
+    else b0 = rng.block(e, 0);
     const float4 sa = E[2 * t.hit];
     const float4 sb = E[2 * t.hit + 1];
     const V3 c = v3(sa.x, sa.y, sa.z);
@@ -375,7 +458,13 @@ __device__ __forceinline__ bool shade(const Params& p, const float4* __restrict_
 
     if (m.type == RTX_MAT_LAMBERTIAN || m.type == RTX_MAT_METAL) {
         uint32_t draws = 0;
-        const V3 s = rand_unit_on_sphere(rng, e, b0, draws);    // shared by both materials
+        V3 s;                                                   // shared by both materials
+        if (pre) {
+            s = pre->s;
+            draws = pre->draws;
+        } else {
+            s = rand_unit_on_sphere(rng, e, b0, draws);
+        }
         if (COUNT) cnt.draws += draws;
         if (m.type == RTX_MAT_LAMBERTIAN) {                     // materials.go:33-42
             V3 dir = add(n, s);

@@ -87,7 +87,9 @@ __global__ __launch_bounds__(BLOCK) void render_pixels(Params p) {
 // the entries, were measured: the extra decode per step cost more than the reduced
 // divergence saved, DESIGN.md.)
 // ------------------------------------------------------------------------------------
-// STEPS > 1 takes up to STEPS entries per lane between two wave votes.
+// STEPS > 1 takes up to STEPS entries per lane between two wave votes.  (A branch-free
+// step that evaluates the box and the sphere test on every lane measured 8 % slower:
+// most waves hold only box entries at a step, and the branch skips the sphere test.)
 template <bool COUNT, int STEPS = 1>
 __device__ __forceinline__ void traverse_phase(uint32_t& mode, Trav& t, const Ray& r, const float4* __restrict__ E,
                                                uint32_t n_entries, uint32_t thresh, Counters& cnt,
@@ -159,17 +161,26 @@ __global__ __launch_bounds__(64 * WX * WY, MINW) void render_wave(Params p) {
     Trav t{};
     Counters cnt{0, 0, 0, 0, 0, 0};
     uint64_t wave_iters = 0, lane_steps = 0, shade_phases = 0, shade_lanes = 0;
+    uint64_t trav_cycles = 0, shade_cycles = 0, clk = 0;  // COUNT only: s_memtime per phase
 
     for (;;) {
+        if (COUNT) clk = __builtin_amdgcn_s_memtime();
         traverse_phase<COUNT, STEPS>(mode, t, r, E, n_entries, thresh, cnt, wave_iters, lane_steps, shade_phases,
                                      shade_lanes);
+        if (COUNT) {
+            const uint64_t now = __builtin_amdgcn_s_memtime();
+            trav_cycles += now - clk;
+            clk = now;
+        }
         if (__ballot(mode != M_DONE) == 0) break;
 
+        // The scatter samples of this phase, drawn by the whole wave together.
+        const Scatter sc = coop_scatter(p, E, rng, seg + 1, mode == M_SHADE ? t.hit : -1);
         if (mode == M_SHADE || mode == M_START) {  // shading phase
             bool new_sample = mode == M_START;
             if (mode == M_SHADE) {
                 V3 color;
-                bool done = shade<COUNT>(p, E, t, seg, r, thr, acc, rng, cnt, color);
+                bool done = shade<COUNT>(p, E, t, seg, r, thr, acc, rng, cnt, color, &sc);
                 ++seg;
                 if (!done && seg == c.max_depth) {  // depth exhausted: GetColor(0) = 0 (ray.go:33)
                     done = true;
@@ -207,10 +218,15 @@ __global__ __launch_bounds__(64 * WX * WY, MINW) void render_wave(Params p) {
                 mode = n_entries > 0 ? M_TRAV : M_SHADE;
             }
         }
+        if (COUNT) shade_cycles += __builtin_amdgcn_s_memtime() - clk;
     }
     if (COUNT) {
         flush_counters(p, active ? spp : 0, cnt);
-        if (lane == 0) flush_sched(p, wave_iters, lane_steps, shade_phases, shade_lanes);
+        if (lane == 0) {
+            flush_sched(p, wave_iters, lane_steps, shade_phases, shade_lanes);
+            atomicAdd(&p.counters[12], (unsigned long long)trav_cycles);
+            atomicAdd(&p.counters[13], (unsigned long long)shade_cycles);
+        }
     }
 }
 

@@ -1,0 +1,48 @@
+#!/usr/bin/env python3
+"""HBM traffic per launch of the bench kernel from rocprofv3 --pmc passes.
+
+  python scripts/pmc_traffic.py <pmc_dir> <out.json> --workload random_spheres:1920x1080x500
+
+Reads FETCH_SIZE and WRITE_SIZE (separate passes, MI355X_MICROARCH.md §HBM) for the
+production kernel (render_wave<false, ...>, the non-counting instantiation the timed
+steps launch) and writes the per-launch byte count bench.py reports as roofline.traffic.
+Units: both counters are KiB (calibrated on this box: a 24,883,200-byte torch fill reads
+WRITE_SIZE 24300).  gfx950 correction: FETCH_SIZE counts half the bytes of 16-B-per-lane
+reads (the scene copy into LDS is exactly that), so it is doubled.
+"""
+import argparse
+import csv
+import glob
+import json
+import os
+import statistics
+
+ap = argparse.ArgumentParser()
+ap.add_argument("pmc_dir")
+ap.add_argument("out")
+ap.add_argument("--workload", required=True)
+ap.add_argument("--kernel", default="render_wave<false")
+args = ap.parse_args()
+
+vals = {"FETCH_SIZE": [], "WRITE_SIZE": []}
+for f in glob.glob(os.path.join(args.pmc_dir, "**", "*counter_collection.csv"), recursive=True):
+    with open(f) as fh:
+        for r in csv.DictReader(fh):
+            if args.kernel in r["Kernel_Name"] and r["Counter_Name"] in vals:
+                vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
+assert vals["FETCH_SIZE"] and vals["WRITE_SIZE"], f"no {args.kernel} rows with FETCH_SIZE/WRITE_SIZE under {args.pmc_dir}"
+fetch = statistics.median(vals["FETCH_SIZE"]) * 1024 * 2  # KiB -> B, x2 gfx950 correction
+write = statistics.median(vals["WRITE_SIZE"]) * 1024
+out = {
+    "workload": args.workload,
+    "kernel": args.kernel,
+    "launches": {k: len(v) for k, v in vals.items()},
+    "fetch_bytes_per_launch": fetch,
+    "write_bytes_per_launch": write,
+    "hbm_bytes_per_launch": fetch + write,
+    "method": "rocprofv3 --kernel-trace --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes); "
+              "KiB units; FETCH_SIZE x2 (gfx950 16-B/lane read correction)",
+}
+with open(args.out, "w") as fh:
+    json.dump(out, fh, indent=1)
+print(json.dumps(out))
