@@ -197,6 +197,7 @@ typedef struct rtx_stats {
     uint64_t shade_lanes;  /* lanes shaded or claiming, summed over shading phases   */
     uint64_t trav_cycles;  /* v1: shader cycles (s_memtime) in traversal, summed over waves */
     uint64_t shade_cycles; /* v1: shader cycles in shading phases, summed over waves  */
+    uint64_t idle_lanes;   /* v1: lanes whose pixel is finished, summed over iterations */
 } rtx_stats;
 
 #define RTX_FLAG_COUNTERS 1u /* count work units (separate kernel instantiation) */
@@ -209,9 +210,11 @@ typedef struct rtx_stats {
 /* Tuning: lanes of a wave that must wait before it shades (1..64; 0 = default, or the
  * RTX_SHADE_THRESH environment variable). */
 #define RTX_FLAG_SHADE_THRESH(n) (((uint32_t)(n)&0x7Fu) << 8)
-/* Tuning: geometry of the wave kernel: waves per block and BVH steps per lane between
- * two wave votes (0 = 4 waves/3 steps (default), 1 = 4/1, 2 = 4/2, 3 = 4/4, 4 = 8/3,
- * 5 = 8/3 with a >= 8 waves/SIMD register budget, 6 = 16/3). */
+/* Tuning: variant of the wave kernel (identical output): 0 = one 8x8 tile per wave,
+ * 4 waves per block, 3 BVH steps per wave vote (default); 1 = persistent waves that
+ * claim tiles; 2 = persistent, 1 step per vote; 3 = persistent, 4 steps; 4 = persistent,
+ * 8 waves per block; 5 = as 4 with a >= 8 waves/SIMD register budget; 6 = persistent,
+ * 1 wave per block. */
 #define RTX_FLAG_WAVE_GEOM(n) (((uint32_t)(n)&7u) << 24)
 
 typedef struct rtx_scene rtx_scene;

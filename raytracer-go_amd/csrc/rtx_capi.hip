@@ -162,7 +162,15 @@ int ensure_device(rtx_scene* s, int device, DeviceCopy** out) {
     c.device = device;
     HIP_TRY(hipSetDevice(device));
     HIP_TRY(hipMalloc(&c.entries, s->entries.size() * sizeof(rtx_entry)));
-    HIP_TRY(hipMemcpy(c.entries, s->entries.data(), s->entries.size() * sizeof(rtx_entry), hipMemcpyHostToDevice));
+    {  // device layout: all 'a' halves, then all 'b' halves (rtxd::SceneRef)
+        const size_t n = s->entries.size();
+        std::vector<float> soa(n * 8);
+        for (size_t i = 0; i < n; ++i) {
+            std::memcpy(&soa[4 * i], s->entries[i].a, 16);
+            std::memcpy(&soa[4 * (n + i)], s->entries[i].b, 16);
+        }
+        HIP_TRY(hipMemcpy(c.entries, soa.data(), n * sizeof(rtx_entry), hipMemcpyHostToDevice));
+    }
     HIP_TRY(hipMalloc(&c.materials, std::max<size_t>(1, s->materials.size()) * sizeof(rtx_material)));
     if (!s->materials.empty())
         HIP_TRY(hipMemcpy(c.materials, s->materials.data(), s->materials.size() * sizeof(rtx_material), hipMemcpyHostToDevice));
@@ -299,6 +307,7 @@ int collect_on(DeviceCopy* c, bool count, uint64_t samples, rtx_stats* st) {
     st->shade_lanes = h[11];
     st->trav_cycles = h[12];
     st->shade_cycles = h[13];
+    st->idle_lanes = h[14];
     st->kernel_ms = ms;
     return RTX_OK;
 }

@@ -192,11 +192,19 @@ __device__ __forceinline__ uint32_t lane_pull(uint32_t src_lane, uint32_t v) {
     return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src_lane * 4u), (int)v);
 }
 
+// The scene's entries (rtx_layout.h) as two arrays of half-entries: a[i] and b[i].  An
+// entry split this way spreads a wave's random reads over all 16 four-bank slots of
+// the LDS (a 32-B-strided array of whole entries reaches only 8 with each 16-B read).
+struct SceneRef {
+    const float4* __restrict__ a;
+    const float4* __restrict__ b;
+};
+
 // ---------------------------------------------------------------------------------
 // Kernel parameters
 // ---------------------------------------------------------------------------------
 struct Params {
-    const float4* entries;   // 2 float4 per rtx_entry
+    const float4* entries;   // n_entries 'a' halves, then n_entries 'b' halves (SceneRef)
     uint32_t n_entries;
     uint32_t n_materials;
     const rtx_material* materials;
@@ -292,14 +300,14 @@ __device__ __forceinline__ V3 texture_value(const Params& p, uint32_t ti, float 
 // lanes), the n lanes still rejecting get 64/n consecutive lanes each, which evaluate
 // attempts base .. base+64/n-1 of that owner in one round; the owner takes the first
 // accepted one.  Same attempt, same bits, about 3 Philox rounds per phase.
-__device__ __forceinline__ Scatter coop_scatter(const Params& p, const float4* __restrict__ E, const PathRng& rng,
+__device__ __forceinline__ Scatter coop_scatter(const Params& p, const SceneRef E, const PathRng& rng,
                                                 uint32_t e, int32_t hit) {
     Scatter out{v3(0.0f, 0.0f, 0.0f), 0u, 0u};
     bool need = false;
     float x = 0.0f, y = 0.0f, z = 0.0f;
     if (hit >= 0) {
         const U4 b0 = rng.block(e, 0);
-        const uint32_t mi = (uint32_t)__float_as_int(E[2 * hit + 1].w);
+        const uint32_t mi = (uint32_t)__float_as_int(E.b[hit].w);
         const uint32_t ty = p.materials[mi].type;
         need = ty == RTX_MAT_LAMBERTIAN || ty == RTX_MAT_METAL;
         out.u0 = b0.x;
@@ -376,10 +384,10 @@ __device__ __forceinline__ void trav_begin(Trav& t, const Ray& r) {
 }
 
 template <bool COUNT>
-__device__ __forceinline__ void trav_step(Trav& t, const Ray& r, const float4* __restrict__ E, Counters& cnt) {
+__device__ __forceinline__ void trav_step(Trav& t, const Ray& r, const SceneRef E, Counters& cnt) {
     const float tmin = 0.001f;  // ray.go:37
-    const float4 ea = E[2 * t.i];
-    const float4 eb = E[2 * t.i + 1];
+    const float4 ea = E.a[t.i];
+    const float4 eb = E.b[t.i];
     // Both halves are consumed here, so the whole entry arrives in one round trip (two
     // ds_read_b128); otherwise the compiler sinks the node-only dwords into the box branch
     // behind a second, dependent LDS read.
@@ -427,7 +435,7 @@ __device__ __forceinline__ void trav_step(Trav& t, const Ray& r, const float4* _
 // when the path ends, with its colour in `color`; otherwise r / thr hold the next
 // segment.  Lockstep RNG: every hitting lane evaluates block (seg+1, 0) first.
 template <bool COUNT>
-__device__ __forceinline__ bool shade(const Params& p, const float4* __restrict__ E, const Trav& t, uint32_t seg,
+__device__ __forceinline__ bool shade(const Params& p, const SceneRef E, const Trav& t, uint32_t seg,
                                       Ray& r, V3& thr, V3& acc, const PathRng& rng, Counters& cnt, V3& color,
                                       const Scatter* pre = nullptr) {
     if (t.hit < 0) {  // miss: background (ray.go:52)
@@ -439,8 +447,8 @@ __device__ __forceinline__ bool shade(const Params& p, const float4* __restrict_
     U4 b0{0u, 0u, 0u, 0u};
     if (pre) b0.x = pre->u0;  // drawn by coop_scatter
     else b0 = rng.block(e, 0);
-    const float4 sa = E[2 * t.hit];
-    const float4 sb = E[2 * t.hit + 1];
+    const float4 sa = E.a[t.hit];
+    const float4 sb = E.b[t.hit];
     const V3 c = v3(sa.x, sa.y, sa.z);
     const uint32_t mi = (uint32_t)__float_as_int(sb.w);
     const V3 pt = add(scale(r.d, t.closest), r.o);              // ray.go:25-30

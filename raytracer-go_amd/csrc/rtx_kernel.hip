@@ -57,6 +57,7 @@ __global__ __launch_bounds__(BLOCK) void render_pixels(Params p) {
     const V3 base = pixel_base(c, x, y);
     PathRng rng{(uint32_t)p.seed, (uint32_t)(p.seed >> 32), y * c.image_width + x, 0};
     Counters cnt{0, 0, 0, 0, 0, 0};
+    const SceneRef E{p.entries, p.entries + p.n_entries};
     V3 sum = v3(0.0f, 0.0f, 0.0f);
     for (uint32_t k = 0; k < c.samples_per_pixel; ++k) {
         rng.sample = k;
@@ -66,8 +67,8 @@ __global__ __launch_bounds__(BLOCK) void render_pixels(Params p) {
             if (COUNT) ++cnt.segments;
             Trav t;
             trav_begin(t, r);
-            while (t.i < p.n_entries) trav_step<COUNT>(t, r, p.entries, cnt);
-            if (shade<COUNT>(p, p.entries, t, seg, r, thr, acc, rng, cnt, col)) break;
+            while (t.i < p.n_entries) trav_step<COUNT>(t, r, E, cnt);
+            if (shade<COUNT>(p, E, t, seg, r, thr, acc, rng, cnt, col)) break;
         }
         sum = add(sum, col);  // camera.go:259 (col = 0 when the depth ran out)
     }
@@ -91,10 +92,10 @@ __global__ __launch_bounds__(BLOCK) void render_pixels(Params p) {
 // step that evaluates the box and the sphere test on every lane measured 8 % slower:
 // most waves hold only box entries at a step, and the branch skips the sphere test.)
 template <bool COUNT, int STEPS = 1>
-__device__ __forceinline__ void traverse_phase(uint32_t& mode, Trav& t, const Ray& r, const float4* __restrict__ E,
+__device__ __forceinline__ void traverse_phase(uint32_t& mode, Trav& t, const Ray& r, const SceneRef E,
                                                uint32_t n_entries, uint32_t thresh, Counters& cnt,
                                                uint64_t& wave_iters, uint64_t& lane_steps, uint64_t& shade_phases,
-                                               uint64_t& shade_lanes) {
+                                               uint64_t& shade_lanes, uint64_t& idle_lanes) {
     for (;;) {
 #pragma unroll
         for (int s = 0; s < STEPS; ++s) {
@@ -108,6 +109,7 @@ __device__ __forceinline__ void traverse_phase(uint32_t& mode, Trav& t, const Ra
         if (COUNT) {
             ++wave_iters;
             lane_steps += (uint64_t)__popcll(trav);
+            idle_lanes += (uint64_t)__popcll(__ballot(mode == 3));
         }
         if (trav == 0 || (uint32_t)__popcll(pend) >= thresh) {
             if (COUNT) {
@@ -120,53 +122,67 @@ __device__ __forceinline__ void traverse_phase(uint32_t& mode, Trav& t, const Ra
 }
 
 // ------------------------------------------------------------------------------------
-// v1: persistent wave loop, one pixel per lane, path regeneration, batched shading.
+// v1: wave loop, one pixel per lane, path regeneration, batched shading.
+//
+// PERSIST = false (default): one wave per 8x8 tile; a lane idles once its pixel is finished
+// until the wave's slowest pixel is (measured: 26 % of lane slots at the headline
+// config).  PERSIST = true: the grid is the device's resident capacity; a wave claims
+// 8x8 tiles from a global counter and hands their pixels, in order, to its lanes as
+// they finish, so its lanes stay on one or two neighbouring tiles (per-lane claims from
+// the global counter scattered a wave over the whole claim frontier and lost 24 % per
+// iteration to incoherence).  A pixel is still traced by one lane, samples
+// k = 0..spp-1 in order, so its float32 sum is the reference's whatever the schedule.
+// Measured at 100 spp: PERSIST raises traversal lane use from 0.50 to 0.62 but costs
+// 15 % more cycles per iteration (divergence grows with the active lanes), a net loss.
 // ------------------------------------------------------------------------------------
-enum : uint32_t { M_TRAV = 0, M_SHADE = 1, M_START = 2, M_DONE = 3 };
+enum : uint32_t { M_TRAV = 0, M_SHADE = 1, M_START = 2, M_DONE = 3, M_CLAIM = 4 };
 
 // BLOCK = 64 * WX * WY threads: a WX x WY grid of waves, each an 8x8 pixel tile; one LDS
 // copy of the scene per block.  MINW = minimum waves per SIMD requested from the
 // register allocator (0 = compiler's choice).  STEPS: entries per lane between votes.
-template <bool COUNT, bool USE_LDS, int WX, int WY, int MINW, int STEPS>
+template <bool COUNT, bool USE_LDS, int WX, int WY, int MINW, int STEPS, bool PERSIST>
 __global__ __launch_bounds__(64 * WX * WY, MINW) void render_wave(Params p) {
     constexpr uint32_t WAVE_BLOCK = 64 * WX * WY;
     extern __shared__ float4 lds_entries[];
-    const float4* __restrict__ E;
+    SceneRef E;
     if constexpr (USE_LDS) {
         const uint32_t n4 = 2 * p.n_entries;
         for (uint32_t t = threadIdx.x; t < n4; t += WAVE_BLOCK) lds_entries[t] = p.entries[t];
         __syncthreads();
-        E = lds_entries;
+        E = SceneRef{lds_entries, lds_entries + p.n_entries};
     } else {
-        E = p.entries;
+        E = SceneRef{p.entries, p.entries + p.n_entries};
     }
     const uint32_t n_entries = p.n_entries;
     const uint32_t thresh = p.shade_thresh;
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-    const uint32_t lx = blockIdx.x * (8u * WX) + (wave % WX) * 8u + (lane & 7u);
-    const uint32_t lr = blockIdx.y * (8u * WY) + (wave / WX) * 8u + (lane >> 3);
-    const bool active = lx < p.width && lr < p.rows;
-    const uint32_t x = p.x0 + lx;
-    const uint32_t y = p.y0 + p.rank + lr * p.world;
     const rtx_camera& c = p.cam;
-    const V3 base = pixel_base(c, x, y);
     const uint32_t spp = c.samples_per_pixel;
+    const uint32_t tiles_x = (p.width + 7u) / 8u;
+    const uint32_t n_tiles = tiles_x * ((p.rows + 7u) / 8u);
+    uint32_t cur_tile = 0, cursor = 64u;  // PERSIST: the wave's tile and its next pixel (uniform)
+    bool exhausted = false;
 
-    uint32_t mode = active ? M_START : M_DONE;
-    uint32_t seg = 0;
+    uint32_t lx = blockIdx.x * (8u * WX) + (wave % WX) * 8u + (lane & 7u);
+    uint32_t lr = blockIdx.y * (8u * WY) + (wave / WX) * 8u + (lane >> 3);
+    const bool active = !PERSIST && lx < p.width && lr < p.rows;
+    V3 base = pixel_base(c, p.x0 + lx, p.y0 + p.rank + lr * p.world);
+    uint32_t mode = PERSIST ? M_CLAIM : (active ? M_START : M_DONE);
+    uint32_t seg = 0, pixels_done = 0;
     V3 sum = v3(0.0f, 0.0f, 0.0f);
     V3 thr = v3(1.0f, 1.0f, 1.0f), acc = v3(0.0f, 0.0f, 0.0f);
     Ray r{v3(0, 0, 0), v3(0, 0, 0)};
-    PathRng rng{(uint32_t)p.seed, (uint32_t)(p.seed >> 32), y * c.image_width + x, 0};
+    PathRng rng{(uint32_t)p.seed, (uint32_t)(p.seed >> 32),
+                (p.y0 + p.rank + lr * p.world) * c.image_width + p.x0 + lx, 0};
     Trav t{};
     Counters cnt{0, 0, 0, 0, 0, 0};
     uint64_t wave_iters = 0, lane_steps = 0, shade_phases = 0, shade_lanes = 0;
-    uint64_t trav_cycles = 0, shade_cycles = 0, clk = 0;  // COUNT only: s_memtime per phase
+    uint64_t trav_cycles = 0, shade_cycles = 0, clk = 0, idle_lanes = 0;  // COUNT only
 
     for (;;) {
         if (COUNT) clk = __builtin_amdgcn_s_memtime();
         traverse_phase<COUNT, STEPS>(mode, t, r, E, n_entries, thresh, cnt, wave_iters, lane_steps, shade_phases,
-                                     shade_lanes);
+                                     shade_lanes, idle_lanes);
         if (COUNT) {
             const uint64_t now = __builtin_amdgcn_s_memtime();
             trav_cycles += now - clk;
@@ -174,58 +190,103 @@ __global__ __launch_bounds__(64 * WX * WY, MINW) void render_wave(Params p) {
         }
         if (__ballot(mode != M_DONE) == 0) break;
 
+        // ---- shading phase ----------------------------------------------------------
         // The scatter samples of this phase, drawn by the whole wave together.
         const Scatter sc = coop_scatter(p, E, rng, seg + 1, mode == M_SHADE ? t.hit : -1);
-        if (mode == M_SHADE || mode == M_START) {  // shading phase
-            bool new_sample = mode == M_START;
-            if (mode == M_SHADE) {
-                V3 color;
-                bool done = shade<COUNT>(p, E, t, seg, r, thr, acc, rng, cnt, color, &sc);
-                ++seg;
-                if (!done && seg == c.max_depth) {  // depth exhausted: GetColor(0) = 0 (ray.go:33)
-                    done = true;
-                    color = acc;
-                }
-                if (done) {
-                    sum = add(sum, color);  // camera.go:259
-                    ++rng.sample;
-                    new_sample = true;
-                }
+        bool ready = false;                // a ray to trace (continued path or new sample)
+        bool fresh = mode == M_START;      // the lane needs its pixel's next sample
+        if (mode == M_SHADE) {
+            V3 color;
+            bool done = shade<COUNT>(p, E, t, seg, r, thr, acc, rng, cnt, color, &sc);
+            ++seg;
+            if (!done && seg == c.max_depth) {  // depth exhausted: GetColor(0) = 0 (ray.go:33)
+                done = true;
+                color = acc;
             }
-            if (new_sample) {
+            if (done) {
+                sum = add(sum, color);  // camera.go:259
+                ++rng.sample;
+                fresh = true;
+            } else {
+                ready = true;
+            }
+        }
+        // New samples, at one program point for the whole wave (camera_ray's Philox runs
+        // in lockstep).  Loops only for max depth 0 (every sample black) and ragged claims.
+        for (;;) {
+            if (fresh && rng.sample >= spp) {  // pixel finished (camera.go:261)
+                const V3 avg = scale(sum, 1.0f / (float)spp);
+                float* o = p.out + ((size_t)lr * p.width + lx) * 3;
+                o[0] = avg.x;
+                o[1] = avg.y;
+                o[2] = avg.z;
+                ++pixels_done;
+                fresh = false;
+                mode = PERSIST ? M_CLAIM : M_DONE;
+            }
+            if constexpr (PERSIST) {  // lanes without a pixel take the next ones of the wave's tile
                 for (;;) {
-                    if (rng.sample >= spp) {
-                        mode = M_DONE;
-                        const V3 avg = scale(sum, 1.0f / (float)spp);  // camera.go:261
-                        float* o = p.out + ((size_t)lr * p.width + lx) * 3;
-                        o[0] = avg.x;
-                        o[1] = avg.y;
-                        o[2] = avg.z;
+                    const uint64_t wm = __ballot(mode == M_CLAIM);
+                    if (wm == 0) break;
+                    if (cursor >= 64u && !exhausted) {  // claim the next 8x8 tile (wave-uniform)
+                        uint32_t tl = 0;
+                        if (lane == 0) tl = atomicAdd(p.tile_counter, 1u);
+                        cur_tile = (uint32_t)__shfl((int)tl, 0);
+                        cursor = 0;
+                        exhausted = cur_tile >= n_tiles;
+                    }
+                    if (exhausted) {
+                        if (mode == M_CLAIM) mode = M_DONE;
                         break;
                     }
-                    r = camera_ray(c, base, rng, cnt.draws);
-                    thr = v3(1.0f, 1.0f, 1.0f);
-                    acc = v3(0.0f, 0.0f, 0.0f);
-                    seg = 0;
-                    if (c.max_depth > 0) break;
+                    const uint32_t rank = (uint32_t)__popcll(wm & ((1ull << lane) - 1ull));
+                    if (mode == M_CLAIM && rank < 64u - cursor) {
+                        const uint32_t l = cursor + rank;
+                        lx = (cur_tile % tiles_x) * 8u + (l & 7u);
+                        lr = (cur_tile / tiles_x) * 8u + (l >> 3);
+                        if (lx < p.width && lr < p.rows) {  // else: outside a ragged tile, claim again
+                            const uint32_t x = p.x0 + lx, y = p.y0 + p.rank + lr * p.world;
+                            base = pixel_base(c, x, y);
+                            rng.pixel = y * c.image_width + x;
+                            rng.sample = 0;
+                            sum = v3(0.0f, 0.0f, 0.0f);
+                            fresh = true;
+                            mode = M_START;
+                        }
+                    }
+                    const uint32_t taken = (uint32_t)__popcll(wm);
+                    cursor = cursor + taken > 64u ? 64u : cursor + taken;
+                }
+            }
+            if (fresh && rng.sample < spp) {
+                r = camera_ray(c, base, rng, cnt.draws);  // GetRay, camera.go:257
+                thr = v3(1.0f, 1.0f, 1.0f);
+                acc = v3(0.0f, 0.0f, 0.0f);
+                seg = 0;
+                if (c.max_depth > 0) {
+                    fresh = false;
+                    ready = true;
+                } else {
                     sum = add(sum, acc);  // max depth 0: GetColor returns black
                     ++rng.sample;
                 }
             }
-            if (mode != M_DONE) {  // begin a segment: world.Hit (ray.go:36)
-                if (COUNT) ++cnt.segments;
-                trav_begin(t, r);
-                mode = n_entries > 0 ? M_TRAV : M_SHADE;
-            }
+            if (__ballot(fresh) == 0) break;
+        }
+        if (ready) {  // begin a segment: world.Hit (ray.go:36)
+            if (COUNT) ++cnt.segments;
+            trav_begin(t, r);
+            mode = n_entries > 0 ? M_TRAV : M_SHADE;
         }
         if (COUNT) shade_cycles += __builtin_amdgcn_s_memtime() - clk;
     }
     if (COUNT) {
-        flush_counters(p, active ? spp : 0, cnt);
+        flush_counters(p, (uint64_t)pixels_done * spp, cnt);
         if (lane == 0) {
             flush_sched(p, wave_iters, lane_steps, shade_phases, shade_lanes);
             atomicAdd(&p.counters[12], (unsigned long long)trav_cycles);
             atomicAdd(&p.counters[13], (unsigned long long)shade_cycles);
+            atomicAdd(&p.counters[14], (unsigned long long)idle_lanes);
         }
     }
 }
@@ -274,14 +335,14 @@ __global__ __launch_bounds__(POOL_BLOCK) void render_pool(Params p) {
     extern __shared__ float4 lds_dyn[];
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
     Pool* wp = reinterpret_cast<Pool*>(lds_dyn) + wave;
-    const float4* __restrict__ E;
+    SceneRef E;
     if constexpr (USE_LDS) {
         float4* scene = lds_dyn + (POOL_WAVES * sizeof(Pool)) / 16;
         const uint32_t n4 = 2 * p.n_entries;
         for (uint32_t t = threadIdx.x; t < n4; t += POOL_BLOCK) scene[t] = p.entries[t];
-        E = scene;
+        E = SceneRef{scene, scene + p.n_entries};
     } else {
-        E = p.entries;
+        E = SceneRef{p.entries, p.entries + p.n_entries};
     }
     const uint32_t n_entries = p.n_entries;
     const uint32_t thresh = p.shade_thresh;
@@ -325,6 +386,7 @@ __global__ __launch_bounds__(POOL_BLOCK) void render_pool(Params p) {
     Counters cnt{0, 0, 0, 0, 0, 0};
     uint64_t samples = 0;
     uint64_t wave_iters = 0, lane_steps = 0, shade_phases = 0, shade_lanes = 0;
+    uint64_t idle_lanes = 0;  // (v2: Q_IDLE lanes; not reported)
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
     uint32_t iter = 0;
 
@@ -335,7 +397,7 @@ __global__ __launch_bounds__(POOL_BLOCK) void render_pool(Params p) {
             break;
         }
         traverse_phase<COUNT, 3>(mode, t, r, E, n_entries, thresh, cnt, wave_iters, lane_steps, shade_phases,
-                                 shade_lanes);
+                                 shade_lanes, idle_lanes);
 
         // ---- shading phase: finish or continue paths ---------------------------------------
         if (mode == Q_SHADE) {
@@ -462,14 +524,30 @@ hipError_t launch_pool(const Params& p, bool use_lds, hipStream_t stream) {
     return hipGetLastError();
 }
 
-template <bool COUNT, int WX, int WY, int MINW, int STEPS = 1>
+template <bool COUNT, int WX, int WY, int MINW, int STEPS = 1, bool PERSIST = false>
 hipError_t launch_wave_geom(const Params& p, bool use_lds, hipStream_t stream) {
-    const dim3 grid((p.width + 8 * WX - 1) / (8 * WX), (p.rows + 8 * WY - 1) / (8 * WY));
-    if (use_lds) {
-        const size_t shmem = (size_t)p.n_entries * 32;
-        hipLaunchKernelGGL((render_wave<COUNT, true, WX, WY, MINW, STEPS>), grid, dim3(64 * WX * WY), shmem, stream, p);
+    const size_t shmem = use_lds ? (size_t)p.n_entries * 32 : 0;
+    const auto kern = use_lds ? render_wave<COUNT, true, WX, WY, MINW, STEPS, PERSIST>
+                              : render_wave<COUNT, false, WX, WY, MINW, STEPS, PERSIST>;
+    constexpr int block = 64 * WX * WY;
+    if constexpr (PERSIST) {
+        int dev = 0, cus = 0, per_cu = 0;
+        hipError_t e = hipGetDevice(&dev);
+        if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, block, shmem);
+        if (e != hipSuccess) return e;
+        if (per_cu < 1) per_cu = 1;
+        const uint64_t tiles = (uint64_t)((p.width + 7) / 8) * ((p.rows + 7) / 8);
+        uint64_t blocks = (uint64_t)per_cu * cus;
+        const uint64_t need = (tiles + WX * WY - 1) / (WX * WY);  // no wave starts without a tile
+        if (blocks > need) blocks = need;
+        if (blocks == 0) blocks = 1;
+        e = hipMemsetAsync(p.tile_counter, 0, 2 * sizeof(uint32_t), stream);  // claim counter + flag
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(kern, dim3((uint32_t)blocks), dim3(block), shmem, stream, p);
     } else {
-        hipLaunchKernelGGL((render_wave<COUNT, false, WX, WY, MINW, STEPS>), grid, dim3(64 * WX * WY), 0, stream, p);
+        const dim3 grid((p.width + 8 * WX - 1) / (8 * WX), (p.rows + 8 * WY - 1) / (8 * WY));
+        hipLaunchKernelGGL(kern, grid, dim3(block), shmem, stream, p);
     }
     return hipGetLastError();
 }
@@ -478,13 +556,13 @@ hipError_t launch_wave_geom(const Params& p, bool use_lds, hipStream_t stream) {
 template <bool COUNT>
 hipError_t launch_wave(const Params& p, uint32_t geom, bool use_lds, hipStream_t stream) {
     switch (geom) {
-    case 1: return launch_wave_geom<COUNT, 2, 2, 0, 1>(p, use_lds, stream);  // 256 threads, 1 step per vote
-    case 2: return launch_wave_geom<COUNT, 2, 2, 0, 2>(p, use_lds, stream);  // 256, 2 steps
-    case 3: return launch_wave_geom<COUNT, 2, 2, 0, 4>(p, use_lds, stream);  // 256, 4 steps
-    case 4: return launch_wave_geom<COUNT, 4, 2, 0, 3>(p, use_lds, stream);  // 512, 3 steps
-    case 5: return launch_wave_geom<COUNT, 4, 2, 8, 3>(p, use_lds, stream);  // 512, >= 8 waves/SIMD, 3 steps
-    case 6: return launch_wave_geom<COUNT, 4, 4, 0, 3>(p, use_lds, stream);  // 1024, 3 steps
-    default: return launch_wave_geom<COUNT, 2, 2, 0, 3>(p, use_lds, stream); // 256, 3 steps
+    case 1: return launch_wave_geom<COUNT, 2, 2, 0, 3, true>(p, use_lds, stream);   // persistent, claims tiles
+    case 2: return launch_wave_geom<COUNT, 2, 2, 0, 1, true>(p, use_lds, stream);   // 1 step per vote
+    case 3: return launch_wave_geom<COUNT, 2, 2, 0, 4, true>(p, use_lds, stream);   // 4 steps per vote
+    case 4: return launch_wave_geom<COUNT, 4, 2, 0, 3, true>(p, use_lds, stream);   // 8 waves per block
+    case 5: return launch_wave_geom<COUNT, 4, 2, 8, 3, true>(p, use_lds, stream);   // 8 waves, >= 8/SIMD
+    case 6: return launch_wave_geom<COUNT, 1, 1, 0, 3, true>(p, use_lds, stream);   // 1 wave per block
+    default: return launch_wave_geom<COUNT, 2, 2, 0, 3, false>(p, use_lds, stream); // one tile per wave
     }
 }
 
@@ -506,7 +584,9 @@ hipError_t launch_render(const Params& p, uint32_t flags, hipStream_t stream) {
             return count ? launch_pool<true, 4>(p, use_lds, stream) : launch_pool<false, 4>(p, use_lds, stream);
         return count ? launch_pool<true, 2>(p, use_lds, stream) : launch_pool<false, 2>(p, use_lds, stream);
     }
-    const uint32_t geom = (flags >> 24) & 7u;
+    uint32_t geom = (flags >> 24) & 7u;
+    // The persistent kernels claim 8x8 tiles by a 32-bit index.
+    if (geom != 0 && (uint64_t)((p.width + 7) / 8) * ((p.rows + 7) / 8) > 0xFFFF0000ull) geom = 0;
     return count ? launch_wave<true>(p, geom, use_lds, stream) : launch_wave<false>(p, geom, use_lds, stream);
 }
 

@@ -21,6 +21,8 @@
 //   node:   a = (bmin.x, bmin.y, bmin.z, int escape)   b = (bmax.x, bmax.y, bmax.z, int RTX_E_NODE)
 //   sphere: a = (c.x, c.y, c.z, radius)                b = (radius*radius, int sphere, 0, int material >= 0)
 // radius*radius is the float32 product hittables.go:100 computes, precomputed.
+// On the device the halves live in two arrays (all a, then all b: rtxd::SceneRef), so
+// a wave's gathers spread over every LDS bank group.
 #pragma once
 #include <stdint.h>
 

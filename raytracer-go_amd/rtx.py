@@ -96,7 +96,8 @@ class Stats(ctypes.Structure):
                 ("prim_tests", c_uint64), ("hits", c_uint64), ("texel_fetches", c_uint64),
                 ("rng_draws", c_uint64), ("kernel_ms", c_double), ("gather_ms", c_double),
                 ("wave_iters", c_uint64), ("lane_steps", c_uint64), ("shade_phases", c_uint64),
-                ("shade_lanes", c_uint64), ("trav_cycles", c_uint64), ("shade_cycles", c_uint64)]
+                ("shade_lanes", c_uint64), ("trav_cycles", c_uint64), ("shade_cycles", c_uint64),
+                ("idle_lanes", c_uint64)]
 
     def as_dict(self) -> dict:
         return {name: getattr(self, name) for name, _ in self._fields_}

@@ -171,10 +171,12 @@ KERNELS = {
     "v1-global-scene": rtx.RTX_FLAG_NO_LDS,
     "v2-global-scene": rtx.RTX_FLAG_KERNEL_POOL | rtx.RTX_FLAG_NO_LDS,
     "v1-thresh1": rtx.RTX_FLAG_SHADE_THRESH(1),
-    "v1-1step": rtx.RTX_FLAG_WAVE_GEOM(1),
+    "v1-persistent": rtx.RTX_FLAG_WAVE_GEOM(1),
+    "v1-1step": rtx.RTX_FLAG_WAVE_GEOM(2),
     "v1-4steps": rtx.RTX_FLAG_WAVE_GEOM(3),
+    "v1-8waves": rtx.RTX_FLAG_WAVE_GEOM(4),
     "v1-8waves-occ8": rtx.RTX_FLAG_WAVE_GEOM(5),
-    "v1-16waves": rtx.RTX_FLAG_WAVE_GEOM(6),
+    "v1-1wave-blocks": rtx.RTX_FLAG_WAVE_GEOM(6),
     "v2-thresh64": rtx.RTX_FLAG_KERNEL_POOL | rtx.RTX_FLAG_SHADE_THRESH(64),
 }
 
