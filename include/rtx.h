@@ -74,7 +74,7 @@ typedef struct rtx_sphere {
 } rtx_sphere;
 
 /* internal/hittables.go:138-165 (NewQuad) — derived fields as the constructor
- * computes them.  Reserved for the Quad/Box row.                  80 B */
+ * computes them (w = n / dot(n, n), normal = Unit(n), d = dot(normal, q)).      80 B */
 typedef struct rtx_quad {
     float q[3];
     uint32_t material;

@@ -400,6 +400,24 @@ static int sphere_hit(const ctx_t* cx, const rtx_sphere* s, const ray_t* r, floa
     return 1;
 }
 
+/* (Quad).Hit, hittables.go:167-190, with InPlane :192-194.  The derived fields (normal,
+ * D, w) are NewQuad's (hittables.go:149-165), computed on the host. */
+static int quad_hit(const rtx_quad* q, const ray_t* r, float tmin, float tmax, hit_t* out) {
+    vec3 n = v3(q->normal[0], q->normal[1], q->normal[2]);
+    float denom = v_dot(r->dir, n);                                        /* :168 */
+    if (fabs((double)denom) < 1e-8) return 0;                              /* :170 */
+    float t = (q->d - v_dot(n, r->origin)) / denom;                        /* :174 */
+    if (!interval_in(tmin, tmax, t)) return 0;                             /* :176 */
+    vec3 point = ray_at(r, t);                                             /* :180 */
+    vec3 php = v_sub(point, v3(q->q[0], q->q[1], q->q[2]));                /* :181 */
+    vec3 w = v3(q->w[0], q->w[1], q->w[2]);
+    float alpha = v_dot(w, v_cross(php, v3(q->v[0], q->v[1], q->v[2])));   /* :182 */
+    float beta = v_dot(w, v_cross(v3(q->u[0], q->u[1], q->u[2]), php));    /* :183 */
+    if (alpha < 0.0f || 1.0f < alpha || beta < 0.0f || 1.0f < beta) return 0; /* :185, :193 */
+    *out = new_hit_info(t, alpha, beta, r->dir, point, n, q->material);    /* :189 */
+    return 1;
+}
+
 /* InBoundary, bvh.go:84-102. */
 static inline int in_boundary(float dir, float origin, float amin, float amax, float* rmin, float* rmax) {
     float inv_d = 1.0f / dir;
@@ -445,9 +463,9 @@ static int hit_ref(const ctx_t* cx, int32_t ref, const ray_t* r, float tmin, flo
     if (ref >= 0) return bvh_hit(cx, &cx->s->nodes[ref], r, tmin, tmax, out);
     uint32_t p = (uint32_t)(~ref);
     uint32_t type = p >> 28, idx = p & 0x0FFFFFFFu;
-    if (type != RTX_PRIM_SPHERE) return 0; /* quads rejected by oracle_render */
     cx->c->prim_tests_ref++;
     if (!dup) cx->c->prim_tests++;
+    if (type == RTX_PRIM_QUAD) return quad_hit(&cx->s->quads[idx], r, tmin, tmax, out);
     return sphere_hit(cx, &cx->s->spheres[idx], r, tmin, tmax, out);
 }
 
@@ -688,7 +706,7 @@ static int scene_supported(const rtx_scene_desc* s) {
         if (s->materials[i].type > RTX_MAT_DIFFUSE_LIGHT) return 0;
     for (uint32_t i = 0; i < s->n_textures; ++i)
         if (s->textures[i].type > RTX_TEX_IMAGE) return 0;
-    if (s->n_quads) return 0;
+    if (s->n_quads && !s->quads) return 0;
     return 1;
 }
 

@@ -57,6 +57,7 @@ struct DeviceCopy {
 
 struct rtx_scene {
     std::vector<rtx_entry> entries;
+    std::vector<float> quadtab;  // 16 floats per quad (rtx_layout.h)
     std::vector<rtx_material> materials;
     std::vector<rtx_texture> textures;
     std::vector<uint32_t> texels;
@@ -78,7 +79,10 @@ int check_ref(const rtx_scene_desc* d, int32_t ref) {
         if (idx >= d->n_spheres) return fail(RTX_ERR_INVALID_ARG, "sphere ref %u out of range (%u spheres)", idx, d->n_spheres);
         return RTX_OK;
     }
-    if (type == RTX_PRIM_QUAD) return fail(RTX_ERR_UNSUPPORTED, "Quad primitives are not on the GPU path yet (hittables.go:138-216)");
+    if (type == RTX_PRIM_QUAD) {
+        if (idx >= d->n_quads) return fail(RTX_ERR_INVALID_ARG, "quad ref %u out of range (%u quads)", idx, d->n_quads);
+        return RTX_OK;
+    }
     return fail(RTX_ERR_INVALID_ARG, "unknown primitive type %u", type);
 }
 
@@ -138,6 +142,14 @@ int emit(const rtx_scene_desc* d, int32_t root, std::vector<rtx_entry>& out) {
             stack.push_back({0, me});
             if (n.right != n.left) stack.push_back({n.right, -1});
             stack.push_back({n.left, -1});
+        } else if ((((uint32_t)(~f.ref)) >> 28) == RTX_PRIM_QUAD) {  // (normal, D | quad, tag)
+            const uint32_t idx = ((uint32_t)(~f.ref)) & 0x0FFFFFFFu;
+            const rtx_quad& q = d->quads[idx];
+            e.a[0] = q.normal[0]; e.a[1] = q.normal[1]; e.a[2] = q.normal[2]; e.a[3] = q.d;
+            const int32_t qi = (int32_t)idx, tag = RTX_E_QUAD;
+            std::memcpy(&e.b[0], &qi, 4);
+            std::memcpy(&e.b[3], &tag, 4);
+            out.push_back(e);
         } else {
             const uint32_t idx = ((uint32_t)(~f.ref)) & 0x0FFFFFFFu;
             const rtx_sphere& s = d->spheres[idx];
@@ -161,15 +173,16 @@ int ensure_device(rtx_scene* s, int device, DeviceCopy** out) {
     DeviceCopy c;
     c.device = device;
     HIP_TRY(hipSetDevice(device));
-    HIP_TRY(hipMalloc(&c.entries, s->entries.size() * sizeof(rtx_entry)));
+    HIP_TRY(hipMalloc(&c.entries, s->entries.size() * sizeof(rtx_entry) + s->quadtab.size() * sizeof(float)));
     {  // device layout: all 'a' halves, then all 'b' halves (rtxd::SceneRef)
         const size_t n = s->entries.size();
-        std::vector<float> soa(n * 8);
+        std::vector<float> soa(n * 8 + s->quadtab.size());
         for (size_t i = 0; i < n; ++i) {
             std::memcpy(&soa[4 * i], s->entries[i].a, 16);
             std::memcpy(&soa[4 * (n + i)], s->entries[i].b, 16);
         }
-        HIP_TRY(hipMemcpy(c.entries, soa.data(), n * sizeof(rtx_entry), hipMemcpyHostToDevice));
+        if (!s->quadtab.empty()) std::memcpy(&soa[8 * n], s->quadtab.data(), s->quadtab.size() * sizeof(float));
+        HIP_TRY(hipMemcpy(c.entries, soa.data(), soa.size() * sizeof(float), hipMemcpyHostToDevice));
     }
     HIP_TRY(hipMalloc(&c.materials, std::max<size_t>(1, s->materials.size()) * sizeof(rtx_material)));
     if (!s->materials.empty())
@@ -250,6 +263,7 @@ rtxd::Params make_params(const rtx_scene* s, const DeviceCopy* c, const rtx_came
     std::memset(&p, 0, sizeof(p));
     p.entries = reinterpret_cast<const float4*>(c->entries);
     p.n_entries = (uint32_t)s->entries.size();
+    p.n_quads = (uint32_t)(s->quadtab.size() / 16);
     p.n_materials = (uint32_t)s->materials.size();
     p.materials = c->materials;
     p.textures = c->textures;
@@ -342,7 +356,11 @@ int rtx_scene_create(const rtx_scene_desc* d, rtx_scene** out) {
     if (d->n_materials && !d->materials) return fail(RTX_ERR_INVALID_ARG, "materials is NULL");
     if (d->n_textures && !d->textures) return fail(RTX_ERR_INVALID_ARG, "textures is NULL");
     if (d->n_texels && !d->texels) return fail(RTX_ERR_INVALID_ARG, "texels is NULL");
-    if (d->n_quads) return fail(RTX_ERR_UNSUPPORTED, "Quad primitives are not on the GPU path yet (hittables.go:138-216)");
+    if (d->n_quads && !d->quads) return fail(RTX_ERR_INVALID_ARG, "quads is NULL");
+    if (d->n_quads > (1u << 26)) return fail(RTX_ERR_INVALID_ARG, "too many quads");
+    for (uint32_t i = 0; i < d->n_quads; ++i)
+        if (d->quads[i].material >= d->n_materials)
+            return fail(RTX_ERR_INVALID_ARG, "quad %u material %u out of range", i, d->quads[i].material);
     for (uint32_t i = 0; i < d->n_spheres; ++i)
         if (d->spheres[i].material >= d->n_materials)
             return fail(RTX_ERR_INVALID_ARG, "sphere %u material %u out of range", i, d->spheres[i].material);
@@ -368,6 +386,16 @@ int rtx_scene_create(const rtx_scene_desc* d, rtx_scene** out) {
             delete s;
             return rc;
         }
+    }
+    s->quadtab.resize((size_t)d->n_quads * 16);
+    for (uint32_t i = 0; i < d->n_quads; ++i) {  // (Q, material), (u, 0), (v, 0), (w, 0)
+        const rtx_quad& q = d->quads[i];
+        float* o = &s->quadtab[(size_t)i * 16];
+        std::memcpy(o, q.q, 12);
+        std::memcpy(o + 3, &q.material, 4);
+        std::memcpy(o + 4, q.u, 12);
+        std::memcpy(o + 8, q.v, 12);
+        std::memcpy(o + 12, q.w, 12);
     }
     s->materials.assign(d->materials, d->materials + d->n_materials);
     s->textures.assign(d->textures, d->textures + d->n_textures);
@@ -399,7 +427,8 @@ void rtx_scene_destroy(rtx_scene* s) {
 
 uint64_t rtx_scene_device_bytes(const rtx_scene* s) {
     if (!s) return 0;
-    return s->entries.size() * sizeof(rtx_entry) + s->materials.size() * sizeof(rtx_material) +
+    return s->entries.size() * sizeof(rtx_entry) + s->quadtab.size() * sizeof(float) +
+           s->materials.size() * sizeof(rtx_material) +
            s->textures.size() * sizeof(rtx_texture) + s->texels.size() * sizeof(uint32_t);
 }
 

@@ -27,6 +27,9 @@ __device__ __forceinline__ V3 mul(V3 a, V3 b) { return v3(a.x * b.x, a.y * b.y, 
 __device__ __forceinline__ V3 scale(V3 a, float s) { return v3(a.x * s, a.y * s, a.z * s); }        // vec3.go:97
 __device__ __forceinline__ float lensq(V3 v) { return v.x * v.x + v.y * v.y + v.z * v.z; }          // vec3.go:115
 __device__ __forceinline__ float dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }      // vec3.go:137
+__device__ __forceinline__ V3 cross(V3 l, V3 r) {                                                 // vec3.go:129-135
+    return v3(l.y * r.z - l.z * r.y, l.z * r.x - l.x * r.z, l.x * r.y - l.y * r.x);
+}
 __device__ __forceinline__ V3 unit(V3 v) {                                                         // vec3.go:103-113
     float l = __builtin_sqrtf(lensq(v));
     return scale(v, 1.0f / l);
@@ -198,14 +201,19 @@ __device__ __forceinline__ uint32_t lane_pull(uint32_t src_lane, uint32_t v) {
 struct SceneRef {
     const float4* __restrict__ a;
     const float4* __restrict__ b;
+    const float4* __restrict__ q;  // quad table, 4 float4 per quad (rtx_layout.h)
 };
+__device__ __forceinline__ SceneRef scene_ref(const float4* base, uint32_t n_entries) {
+    return SceneRef{base, base + n_entries, base + 2 * n_entries};
+}
 
 // ---------------------------------------------------------------------------------
 // Kernel parameters
 // ---------------------------------------------------------------------------------
 struct Params {
-    const float4* entries;   // n_entries 'a' halves, then n_entries 'b' halves (SceneRef)
+    const float4* entries;   // n_entries 'a' halves, n_entries 'b' halves, 4 * n_quads (SceneRef)
     uint32_t n_entries;
+    uint32_t n_quads;
     uint32_t n_materials;
     const rtx_material* materials;
     const rtx_texture* textures;
@@ -291,6 +299,14 @@ __device__ __forceinline__ V3 texture_value(const Params& p, uint32_t ti, float 
               (float)(((px >> 16) & 0xFFu) * 257u) * cs);
 }
 
+// Material index of the primitive at entry `hit`.
+template <bool QUADS>
+__device__ __forceinline__ uint32_t hit_material(const SceneRef E, uint32_t hit) {
+    const float4 b = E.b[hit];
+    if (QUADS && __float_as_int(b.w) == RTX_E_QUAD) return (uint32_t)__float_as_int(E.q[4u * __float_as_int(b.x)].w);
+    return (uint32_t)__float_as_int(b.w);
+}
+
 // Wave-cooperative rejection sampling for NewVec3UnitRandOnUnitSphere32 (vec3.go:182-190).
 // Must be called by the whole wave (converged).  A lane with hit >= 0 draws block (e, 0);
 // its words 0-2 are attempt 0 of the unit-sphere loop.  The loop's result is the FIRST
@@ -300,6 +316,7 @@ __device__ __forceinline__ V3 texture_value(const Params& p, uint32_t ti, float 
 // lanes), the n lanes still rejecting get 64/n consecutive lanes each, which evaluate
 // attempts base .. base+64/n-1 of that owner in one round; the owner takes the first
 // accepted one.  Same attempt, same bits, about 3 Philox rounds per phase.
+template <bool QUADS>
 __device__ __forceinline__ Scatter coop_scatter(const Params& p, const SceneRef E, const PathRng& rng,
                                                 uint32_t e, int32_t hit) {
     Scatter out{v3(0.0f, 0.0f, 0.0f), 0u, 0u};
@@ -307,7 +324,7 @@ __device__ __forceinline__ Scatter coop_scatter(const Params& p, const SceneRef 
     float x = 0.0f, y = 0.0f, z = 0.0f;
     if (hit >= 0) {
         const U4 b0 = rng.block(e, 0);
-        const uint32_t mi = (uint32_t)__float_as_int(E.b[hit].w);
+        const uint32_t mi = hit_material<QUADS>(E, (uint32_t)hit);
         const uint32_t ty = p.materials[mi].type;
         need = ty == RTX_MAT_LAMBERTIAN || ty == RTX_MAT_METAL;
         out.u0 = b0.x;
@@ -383,7 +400,33 @@ __device__ __forceinline__ void trav_begin(Trav& t, const Ray& r) {
     t.i = 0;
 }
 
+// (Quad).Hit, hittables.go:167-194, of quad entry t.i = (ea, eb) against (tmin, closest).
 template <bool COUNT>
+__device__ __forceinline__ void quad_test(Trav& t, const Ray& r, const SceneRef E, const float4 ea, const float4 eb,
+                                          Counters& cnt) {
+    const float tmin = 0.001f;  // ray.go:37
+    if (COUNT) ++cnt.prim_tests;
+    const float denom = r.d.x * ea.x + r.d.y * ea.y + r.d.z * ea.z;                 // :168
+    if (!(__builtin_fabs((double)denom) < 1e-8)) {                                   // :170
+        const float tt = (ea.w - (ea.x * r.o.x + ea.y * r.o.y + ea.z * r.o.z)) / denom;  // :174
+        if (tmin < tt && tt < t.closest) {                                           // :176
+            const uint32_t qi = 4u * (uint32_t)__float_as_int(eb.x);
+            const float4 q0 = E.q[qi], q1 = E.q[qi + 1], q2 = E.q[qi + 2], q3 = E.q[qi + 3];
+            const V3 php = sub(add(scale(r.d, tt), r.o), v3(q0.x, q0.y, q0.z));     // :180-181
+            const V3 w = v3(q3.x, q3.y, q3.z);
+            const float alpha = dot(w, cross(php, v3(q2.x, q2.y, q2.z)));           // :182
+            const float beta = dot(w, cross(v3(q1.x, q1.y, q1.z), php));            // :183
+            if (!(alpha < 0.0f || 1.0f < alpha || beta < 0.0f || 1.0f < beta)) {   // :185, :193
+                t.closest = tt;
+                t.hit = (int32_t)t.i;
+            }
+        }
+    }
+    ++t.i;
+}
+
+// QUADS: the scene holds quads (a third entry kind); false compiles the sphere-only step.
+template <bool COUNT, bool QUADS = false>
 __device__ __forceinline__ void trav_step(Trav& t, const Ray& r, const SceneRef E, Counters& cnt) {
     const float tmin = 0.001f;  // ray.go:37
     const float4 ea = E.a[t.i];
@@ -408,6 +451,8 @@ __device__ __forceinline__ void trav_step(Trav& t, const Ray& r, const SceneRef 
         const float lo = __builtin_fmaxf(__builtin_fmaxf(__builtin_fmaxf(tmin, t0x), t0y), t0z);
         const float hi = __builtin_fminf(__builtin_fminf(__builtin_fminf(t.closest, t1x), t1y), t1z);
         t.i = (lo < hi) ? t.i + 1 : (uint32_t)__float_as_int(ea.w);
+    } else if (QUADS && __float_as_int(eb.w) == RTX_E_QUAD) {
+        quad_test<COUNT>(t, r, E, ea, eb, cnt);
     } else {
         if (COUNT) ++cnt.prim_tests;
         const float ox = r.o.x - ea.x, oy = r.o.y - ea.y, oz = r.o.z - ea.z;  // :97
@@ -434,7 +479,7 @@ __device__ __forceinline__ void trav_step(Trav& t, const Ray& r, const SceneRef 
 // Shade the result of segment `seg` (ray.go:36-53, materials.go:33-113).  Returns true
 // when the path ends, with its colour in `color`; otherwise r / thr hold the next
 // segment.  Lockstep RNG: every hitting lane evaluates block (seg+1, 0) first.
-template <bool COUNT>
+template <bool COUNT, bool QUADS = false>
 __device__ __forceinline__ bool shade(const Params& p, const SceneRef E, const Trav& t, uint32_t seg,
                                       Ray& r, V3& thr, V3& acc, const PathRng& rng, Counters& cnt, V3& color,
                                       const Scatter* pre = nullptr) {
@@ -449,18 +494,38 @@ __device__ __forceinline__ bool shade(const Params& p, const SceneRef E, const T
     else b0 = rng.block(e, 0);
     const float4 sa = E.a[t.hit];
     const float4 sb = E.b[t.hit];
-    const V3 c = v3(sa.x, sa.y, sa.z);
-    const uint32_t mi = (uint32_t)__float_as_int(sb.w);
     const V3 pt = add(scale(r.d, t.closest), r.o);              // ray.go:25-30
-    V3 n = unit(scale(sub(pt, c), sa.w));                       // hittables.go:119-120
+    const bool quad = QUADS && __float_as_int(sb.w) == RTX_E_QUAD;
+    uint32_t mi;
+    V3 n;
+    float4 q0, q1, q2, q3;
+    if (quad) {                                                 // hittables.go:167-190
+        const uint32_t qi = 4u * (uint32_t)__float_as_int(sb.x);
+        q0 = E.q[qi];
+        q1 = E.q[qi + 1];
+        q2 = E.q[qi + 2];
+        q3 = E.q[qi + 3];
+        mi = (uint32_t)__float_as_int(q0.w);
+        n = v3(sa.x, sa.y, sa.z);                               // q.normal
+    } else {
+        mi = (uint32_t)__float_as_int(sb.w);
+        n = unit(scale(sub(pt, v3(sa.x, sa.y, sa.z)), sa.w));   // hittables.go:119-120
+    }
     const bool front = dot(r.d, n) < 0.0f;                      // hittables.go:23
     const rtx_material m = p.materials[mi];
     float u = 0.0f, v = 0.0f;
     if (p.has_uv && (m.type == RTX_MAT_LAMBERTIAN || m.type == RTX_MAT_DIFFUSE_LIGHT) &&
         p.textures[m.texture].type == RTX_TEX_IMAGE) {           // only an image texture reads UV
-        const UV uv = sphere_uv(n.x, n.y, n.z);
-        u = uv.u;
-        v = uv.v;
+        if (quad) {  // (alpha, beta) of the hit, recomputed as quad_test did (hittables.go:181-183)
+            const V3 php = sub(pt, v3(q0.x, q0.y, q0.z));
+            const V3 w = v3(q3.x, q3.y, q3.z);
+            u = dot(w, cross(php, v3(q2.x, q2.y, q2.z)));
+            v = dot(w, cross(v3(q1.x, q1.y, q1.z), php));
+        } else {
+            const UV uv = sphere_uv(n.x, n.y, n.z);
+            u = uv.u;
+            v = uv.v;
+        }
     }
     if (!front) n = scale(n, -1.0f);                            // hittables.go:24-26
 

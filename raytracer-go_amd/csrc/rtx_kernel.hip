@@ -46,7 +46,7 @@ constexpr int TILE_W = 16;
 constexpr int TILE_H = 16;
 constexpr int BLOCK = TILE_W * TILE_H;
 
-template <bool COUNT>
+template <bool COUNT, bool QUADS>
 __global__ __launch_bounds__(BLOCK) void render_pixels(Params p) {
     const uint32_t lx = blockIdx.x * TILE_W + (threadIdx.x % TILE_W);
     const uint32_t lr = blockIdx.y * TILE_H + (threadIdx.x / TILE_W);
@@ -57,7 +57,7 @@ __global__ __launch_bounds__(BLOCK) void render_pixels(Params p) {
     const V3 base = pixel_base(c, x, y);
     PathRng rng{(uint32_t)p.seed, (uint32_t)(p.seed >> 32), y * c.image_width + x, 0};
     Counters cnt{0, 0, 0, 0, 0, 0};
-    const SceneRef E{p.entries, p.entries + p.n_entries};
+    const SceneRef E = scene_ref(p.entries, p.n_entries);
     V3 sum = v3(0.0f, 0.0f, 0.0f);
     for (uint32_t k = 0; k < c.samples_per_pixel; ++k) {
         rng.sample = k;
@@ -67,8 +67,8 @@ __global__ __launch_bounds__(BLOCK) void render_pixels(Params p) {
             if (COUNT) ++cnt.segments;
             Trav t;
             trav_begin(t, r);
-            while (t.i < p.n_entries) trav_step<COUNT>(t, r, E, cnt);
-            if (shade<COUNT>(p, E, t, seg, r, thr, acc, rng, cnt, col)) break;
+            while (t.i < p.n_entries) trav_step<COUNT, QUADS>(t, r, E, cnt);
+            if (shade<COUNT, QUADS>(p, E, t, seg, r, thr, acc, rng, cnt, col)) break;
         }
         sum = add(sum, col);  // camera.go:259 (col = 0 when the depth ran out)
     }
@@ -91,7 +91,7 @@ __global__ __launch_bounds__(BLOCK) void render_pixels(Params p) {
 // STEPS > 1 takes up to STEPS entries per lane between two wave votes.  (A branch-free
 // step that evaluates the box and the sphere test on every lane measured 8 % slower:
 // most waves hold only box entries at a step, and the branch skips the sphere test.)
-template <bool COUNT, int STEPS = 1>
+template <bool COUNT, int STEPS = 1, bool QUADS = false>
 __device__ __forceinline__ void traverse_phase(uint32_t& mode, Trav& t, const Ray& r, const SceneRef E,
                                                uint32_t n_entries, uint32_t thresh, Counters& cnt,
                                                uint64_t& wave_iters, uint64_t& lane_steps, uint64_t& shade_phases,
@@ -100,7 +100,7 @@ __device__ __forceinline__ void traverse_phase(uint32_t& mode, Trav& t, const Ra
 #pragma unroll
         for (int s = 0; s < STEPS; ++s) {
             if (mode == 0) {
-                trav_step<COUNT>(t, r, E, cnt);
+                trav_step<COUNT, QUADS>(t, r, E, cnt);
                 if (t.i >= n_entries) mode = 1;
             }
         }
@@ -140,18 +140,18 @@ enum : uint32_t { M_TRAV = 0, M_SHADE = 1, M_START = 2, M_DONE = 3, M_CLAIM = 4 
 // BLOCK = 64 * WX * WY threads: a WX x WY grid of waves, each an 8x8 pixel tile; one LDS
 // copy of the scene per block.  MINW = minimum waves per SIMD requested from the
 // register allocator (0 = compiler's choice).  STEPS: entries per lane between votes.
-template <bool COUNT, bool USE_LDS, int WX, int WY, int MINW, int STEPS, bool PERSIST>
+template <bool COUNT, bool USE_LDS, int WX, int WY, int MINW, int STEPS, bool PERSIST, bool QUADS>
 __global__ __launch_bounds__(64 * WX * WY, MINW) void render_wave(Params p) {
     constexpr uint32_t WAVE_BLOCK = 64 * WX * WY;
     extern __shared__ float4 lds_entries[];
     SceneRef E;
     if constexpr (USE_LDS) {
-        const uint32_t n4 = 2 * p.n_entries;
+        const uint32_t n4 = 2 * p.n_entries + 4 * p.n_quads;  // entries, then the quad table
         for (uint32_t t = threadIdx.x; t < n4; t += WAVE_BLOCK) lds_entries[t] = p.entries[t];
         __syncthreads();
-        E = SceneRef{lds_entries, lds_entries + p.n_entries};
+        E = scene_ref(lds_entries, p.n_entries);
     } else {
-        E = SceneRef{p.entries, p.entries + p.n_entries};
+        E = scene_ref(p.entries, p.n_entries);
     }
     const uint32_t n_entries = p.n_entries;
     const uint32_t thresh = p.shade_thresh;
@@ -181,7 +181,7 @@ __global__ __launch_bounds__(64 * WX * WY, MINW) void render_wave(Params p) {
 
     for (;;) {
         if (COUNT) clk = __builtin_amdgcn_s_memtime();
-        traverse_phase<COUNT, STEPS>(mode, t, r, E, n_entries, thresh, cnt, wave_iters, lane_steps, shade_phases,
+        traverse_phase<COUNT, STEPS, QUADS>(mode, t, r, E, n_entries, thresh, cnt, wave_iters, lane_steps, shade_phases,
                                      shade_lanes, idle_lanes);
         if (COUNT) {
             const uint64_t now = __builtin_amdgcn_s_memtime();
@@ -192,12 +192,12 @@ __global__ __launch_bounds__(64 * WX * WY, MINW) void render_wave(Params p) {
 
         // ---- shading phase ----------------------------------------------------------
         // The scatter samples of this phase, drawn by the whole wave together.
-        const Scatter sc = coop_scatter(p, E, rng, seg + 1, mode == M_SHADE ? t.hit : -1);
+        const Scatter sc = coop_scatter<QUADS>(p, E, rng, seg + 1, mode == M_SHADE ? t.hit : -1);
         bool ready = false;                // a ray to trace (continued path or new sample)
         bool fresh = mode == M_START;      // the lane needs its pixel's next sample
         if (mode == M_SHADE) {
             V3 color;
-            bool done = shade<COUNT>(p, E, t, seg, r, thr, acc, rng, cnt, color, &sc);
+            bool done = shade<COUNT, QUADS>(p, E, t, seg, r, thr, acc, rng, cnt, color, &sc);
             ++seg;
             if (!done && seg == c.max_depth) {  // depth exhausted: GetColor(0) = 0 (ray.go:33)
                 done = true;
@@ -340,9 +340,9 @@ __global__ __launch_bounds__(POOL_BLOCK) void render_pool(Params p) {
         float4* scene = lds_dyn + (POOL_WAVES * sizeof(Pool)) / 16;
         const uint32_t n4 = 2 * p.n_entries;
         for (uint32_t t = threadIdx.x; t < n4; t += POOL_BLOCK) scene[t] = p.entries[t];
-        E = SceneRef{scene, scene + p.n_entries};
+        E = scene_ref(scene, p.n_entries);
     } else {
-        E = SceneRef{p.entries, p.entries + p.n_entries};
+        E = scene_ref(p.entries, p.n_entries);
     }
     const uint32_t n_entries = p.n_entries;
     const uint32_t thresh = p.shade_thresh;
@@ -498,9 +498,12 @@ __global__ __launch_bounds__(POOL_BLOCK) void render_pool(Params p) {
 // ------------------------------------------------------------------------------------
 constexpr uint32_t LDS_MAX_BYTES = 64 * 1024;
 
+// LDS bytes of the scene copy: entries and the quad table.
+inline size_t scene_lds_bytes(const Params& p) { return (size_t)p.n_entries * 32 + (size_t)p.n_quads * 64; }
+
 template <bool COUNT, int NCH>
 hipError_t launch_pool(const Params& p, bool use_lds, hipStream_t stream) {
-    const size_t shmem = POOL_WAVES * sizeof(WavePool<NCH>) + (use_lds ? (size_t)p.n_entries * 32 : 0);
+    const size_t shmem = POOL_WAVES * sizeof(WavePool<NCH>) + (use_lds ? scene_lds_bytes(p) : 0);
     int dev = 0, cus = 0, per_cu = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
@@ -524,11 +527,11 @@ hipError_t launch_pool(const Params& p, bool use_lds, hipStream_t stream) {
     return hipGetLastError();
 }
 
-template <bool COUNT, int WX, int WY, int MINW, int STEPS = 1, bool PERSIST = false>
+template <bool COUNT, int WX, int WY, int MINW, int STEPS = 1, bool PERSIST = false, bool QUADS = false>
 hipError_t launch_wave_geom(const Params& p, bool use_lds, hipStream_t stream) {
-    const size_t shmem = use_lds ? (size_t)p.n_entries * 32 : 0;
-    const auto kern = use_lds ? render_wave<COUNT, true, WX, WY, MINW, STEPS, PERSIST>
-                              : render_wave<COUNT, false, WX, WY, MINW, STEPS, PERSIST>;
+    const size_t shmem = use_lds ? scene_lds_bytes(p) : 0;
+    const auto kern = use_lds ? render_wave<COUNT, true, WX, WY, MINW, STEPS, PERSIST, QUADS>
+                              : render_wave<COUNT, false, WX, WY, MINW, STEPS, PERSIST, QUADS>;
     constexpr int block = 64 * WX * WY;
     if constexpr (PERSIST) {
         int dev = 0, cus = 0, per_cu = 0;
@@ -569,15 +572,20 @@ hipError_t launch_wave(const Params& p, uint32_t geom, bool use_lds, hipStream_t
 hipError_t launch_render(const Params& p, uint32_t flags, hipStream_t stream) {
     if (p.width == 0 || p.rows == 0) return hipSuccess;
     const bool count = (flags & RTX_FLAG_COUNTERS) != 0;
+    const bool quads = p.n_quads > 0;
     if (flags & RTX_FLAG_KERNEL_V0) {
         const dim3 grid((p.width + TILE_W - 1) / TILE_W, (p.rows + TILE_H - 1) / TILE_H);
-        if (count)
-            hipLaunchKernelGGL(render_pixels<true>, grid, dim3(BLOCK), 0, stream, p);
-        else
-            hipLaunchKernelGGL(render_pixels<false>, grid, dim3(BLOCK), 0, stream, p);
+        const auto kern = count ? (quads ? render_pixels<true, true> : render_pixels<true, false>)
+                                : (quads ? render_pixels<false, true> : render_pixels<false, false>);
+        hipLaunchKernelGGL(kern, grid, dim3(BLOCK), 0, stream, p);
         return hipGetLastError();
     }
-    const bool use_lds = !(flags & RTX_FLAG_NO_LDS) && (uint64_t)p.n_entries * 32 <= LDS_MAX_BYTES;
+    const bool use_lds = !(flags & RTX_FLAG_NO_LDS) && scene_lds_bytes(p) <= LDS_MAX_BYTES;
+    // Scenes with quads (hittables.go:138-216) run the default v1 schedule built with the
+    // three-kind step; the scheduling variants below are sphere-only.
+    if (quads)
+        return count ? launch_wave_geom<true, 2, 2, 0, 3, false, true>(p, use_lds, stream)
+                     : launch_wave_geom<false, 2, 2, 0, 3, false, true>(p, use_lds, stream);
     // v2 keeps tile origins in 16 bits: regions wider or taller than 65535 use v1.
     if ((flags & RTX_FLAG_KERNEL_POOL) && p.width <= 0xFFFFu && p.rows <= 0xFFFFu) {
         if (flags & RTX_FLAG_POOL4)

@@ -20,6 +20,11 @@
 // Entry (two float4 = 32 B, 16-B aligned; loads are 2 x global/ds 128-bit):
 //   node:   a = (bmin.x, bmin.y, bmin.z, int escape)   b = (bmax.x, bmax.y, bmax.z, int RTX_E_NODE)
 //   sphere: a = (c.x, c.y, c.z, radius)                b = (radius*radius, int sphere, 0, int material >= 0)
+//   quad:   a = (normal.x, normal.y, normal.z, D)      b = (int quad, 0, 0, int RTX_E_QUAD)
+// A quad's plane test needs only its entry; the in-plane test and shading read its
+// record from the quad table that follows the entries (4 float4 per quad):
+//   (Q.x, Q.y, Q.z, int material), (u, 0), (v, 0), (w, 0)   — NewQuad's fields,
+// hittables.go:149-165, computed on the host.
 // radius*radius is the float32 product hittables.go:100 computes, precomputed.
 // On the device the halves live in two arrays (all a, then all b: rtxd::SceneRef), so
 // a wave's gathers spread over every LDS bank group.
@@ -27,6 +32,7 @@
 #include <stdint.h>
 
 #define RTX_E_NODE (-1)
+#define RTX_E_QUAD (-2)
 
 struct rtx_entry {
     float a[4];

@@ -124,8 +124,18 @@ struct Flattener {
                 r = RTX_REF_PRIM(RTX_PRIM_SPHERE, fs.spheres.size());
                 fs.spheres.push_back(sp);
                 refs[h] = r;
-            } else if (dynamic_cast<const Quad*>(h)) {
-                return fail(RTX_ERR_UNSUPPORTED, "Quad primitives are not on the GPU path yet (hittables.go:138-216)");
+            } else if (auto q = dynamic_cast<const Quad*>(h)) {  // hittables.go:138-165
+                rtx_quad qd{};
+                qd.q[0] = q->Q.X; qd.q[1] = q->Q.Y; qd.q[2] = q->Q.Z;
+                qd.u[0] = q->u.X; qd.u[1] = q->u.Y; qd.u[2] = q->u.Z;
+                qd.v[0] = q->v.X; qd.v[1] = q->v.Y; qd.v[2] = q->v.Z;
+                qd.w[0] = q->w.X; qd.w[1] = q->w.Y; qd.w[2] = q->w.Z;
+                qd.normal[0] = q->normal.X; qd.normal[1] = q->normal.Y; qd.normal[2] = q->normal.Z;
+                qd.d = q->D;
+                if (!material(q->material, qd.material)) return false;
+                r = RTX_REF_PRIM(RTX_PRIM_QUAD, fs.quads.size());
+                fs.quads.push_back(qd);
+                refs[h] = r;
             } else if (dynamic_cast<const World*>(h)) {
                 return fail(RTX_ERR_UNSUPPORTED, "a World nested inside a BVH is not on the GPU path");
             } else {

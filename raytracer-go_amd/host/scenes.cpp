@@ -162,11 +162,71 @@ SceneSpec Earth(uint64_t seed, int tex_w, int tex_h) {  // main.go:80-104
     return s;
 }
 
+SceneSpec QuadDemo(uint64_t seed) {  // main.go:132-160
+    SceneSpec s;
+    s.name = "quad_demo";
+    s.aspect = 16.0f / 9.0f;
+    s.width = 400;
+    s.opts = {WithSamplesPerPixel(100),
+              WithMaxRayDepth(50),
+              WithLookFrom(NewVec3(0, 0, 9)),
+              WithLookAt(NewVec3(0, 0, 0)),
+              WithFOVDegrees(80),
+              WithDefocusAngleDegrees(0),
+              WithBackgroundColor(NewVec3(0.7f, 0.8f, 1))};
+    Seed(seed);  // BVH axis choice (bvh.go:147)
+    auto world = NewWorld();
+    auto leftRed = NewLambertian(NewSolidColor(1, 0.2f, 0.2f));
+    auto backGreen = NewLambertian(NewSolidColor(0.2f, 1, 0.2f));
+    auto rightBlue = NewLambertian(NewSolidColor(0.2f, 0.2f, 1));
+    auto upperOrange = NewLambertian(NewSolidColor(1, 0.5f, 0));
+    auto lowerTeal = NewLambertian(NewSolidColor(0.2f, 0.8f, 0.8f));
+    world->Add(NewQuad(NewVec3(-3, -2, 5), NewVec3(0, 0, -4), NewVec3(0, 4, 0), leftRed));
+    world->Add(NewQuad(NewVec3(-2, -2, 0), NewVec3(4, 0, 0), NewVec3(0, 4, 0), backGreen));
+    world->Add(NewQuad(NewVec3(3, -2, 1), NewVec3(0, 0, 4), NewVec3(0, 4, 0), rightBlue));
+    world->Add(NewQuad(NewVec3(-2, 3, 1), NewVec3(4, 0, 0), NewVec3(0, 0, 4), upperOrange));
+    world->Add(NewQuad(NewVec3(-2, -3, 5), NewVec3(4, 0, 0), NewVec3(0, 0, -4), lowerTeal));
+    s.world = NewBVHFromWorld(*world);
+    return s;
+}
+
+SceneSpec CornellBox(uint64_t seed) {  // main.go:194-225 (main.go:55: the selected scene)
+    SceneSpec s;
+    s.name = "cornell_box";
+    s.aspect = 1.0f;
+    s.width = 600;
+    s.opts = {WithSamplesPerPixel(200),
+              WithMaxRayDepth(50),
+              WithLookFrom(NewVec3(278, 278, -800)),
+              WithLookAt(NewVec3(278, 278, 0)),
+              WithFOVDegrees(40),
+              WithDefocusAngleDegrees(0),
+              WithBackgroundColor(NewVec3(0, 0, 0))};
+    Seed(seed);
+    auto world = NewWorld();
+    auto red = NewLambertian(NewSolidColor(0.65f, 0.05f, 0.05f));
+    auto white = NewLambertian(NewSolidColor(0.73f, 0.73f, 0.73f));
+    auto green = NewLambertian(NewSolidColor(0.12f, 0.45f, 0.15f));
+    auto light = NewDiffuseLight(NewSolidColor(15, 15, 15));
+    world->Add(NewQuad(NewVec3(555, 0, 0), NewVec3(0, 555, 0), NewVec3(0, 0, 555), green));
+    world->Add(NewQuad(NewVec3(0, 0, 0), NewVec3(0, 555, 0), NewVec3(0, 0, 555), red));
+    world->Add(NewQuad(NewVec3(343, 554, 332), NewVec3(-130, 0, 0), NewVec3(0, 0, -105), light));
+    world->Add(NewQuad(NewVec3(0, 0, 0), NewVec3(555, 0, 0), NewVec3(0, 0, 555), white));
+    world->Add(NewQuad(NewVec3(555, 555, 555), NewVec3(-555, 0, 0), NewVec3(0, 0, -555), white));
+    world->Add(NewQuad(NewVec3(0, 0, 555), NewVec3(555, 0, 0), NewVec3(0, 555, 0), white));
+    world->Add(Box(NewVec3(130, 0, 65), NewVec3(295, 165, 230), white));
+    world->Add(Box(NewVec3(265, 0, 295), NewVec3(430, 330, 460), white));
+    s.world = NewBVHFromWorld(*world);
+    return s;
+}
+
 bool BuildScene(const std::string& name, uint64_t seed, SceneSpec& out) {
     if (name == "random_spheres") out = RandSpheres(seed);
     else if (name == "stress_100k") out = StressSpheres(seed, 100000);
     else if (name == "earth_dielectric") out = EarthDielectric(seed, 2048, 1024);
     else if (name == "earth") out = Earth(seed, 2048, 1024);
+    else if (name == "quad_demo") out = QuadDemo(seed);
+    else if (name == "cornell_box") out = CornellBox(seed);
     else return false;
     return true;
 }

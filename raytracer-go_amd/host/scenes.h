@@ -31,7 +31,14 @@ SceneSpec Earth(uint64_t seed, int tex_w, int tex_h);
 // A seeded RGBA8 "earth-like" raster (oceans, continents, ice caps).
 ImagePtr SyntheticEarth(uint64_t seed, int w, int h);
 
-// By name: "random_spheres", "stress_100k", "earth_dielectric", "earth".
+// quadDemo, main.go:132-160: five Lambertian quads.
+SceneSpec QuadDemo(uint64_t seed);
+// cornellBox, main.go:194-225 (the scene main.go:55 selects): 6 walls/light + 2 Boxes
+// = 18 quads, DiffuseLight(15) ceiling lamp, black background, 600x600 at 200 spp.
+SceneSpec CornellBox(uint64_t seed);
+
+// By name: "random_spheres", "stress_100k", "earth_dielectric", "earth", "quad_demo",
+// "cornell_box".
 bool BuildScene(const std::string& name, uint64_t seed, SceneSpec& out);
 
 }  // namespace internal

@@ -116,9 +116,24 @@ def test_noise_texture_is_unsupported(built):
     assert rc == rtx.RTX_ERR_UNSUPPORTED and "Perlin" in msg
 
 
-def test_quads_are_unsupported(built):
+def test_quad_validation(built):
+    """Quads are on the GPU path (hittables.go:138-216); bad tables are rejected."""
     rc, msg = create(make_desc([sphere()], [lambertian()], [texture()], quads=1))
-    assert rc == rtx.RTX_ERR_UNSUPPORTED and "Quad" in msg
+    assert rc == rtx.RTX_ERR_INVALID_ARG and "quads is NULL" in msg
+    q = rtx.Quad()
+    q.material = 5
+    Q = (rtx.Quad * 1)(q)
+    d = make_desc([sphere()], [lambertian()], [texture()], quads=1)
+    d.quads = Q
+    rc, msg = create(d)
+    assert rc == rtx.RTX_ERR_INVALID_ARG and "quad 0 material" in msg
+    q.material = 0
+    Q = (rtx.Quad * 1)(q)
+    d = make_desc([sphere()], [lambertian()], [texture()], quads=1,
+                  roots=[rtx.ref_prim(rtx.RTX_PRIM_QUAD, 1)])
+    d.quads = Q
+    rc, msg = create(d)
+    assert rc == rtx.RTX_ERR_INVALID_ARG and "quad ref 1 out of range" in msg
 
 
 def test_material_out_of_range(built):
