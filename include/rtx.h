@@ -207,6 +207,11 @@ typedef struct rtx_stats {
 #define RTX_FLAG_KERNEL_POOL 8u /* A/B: the pixel-pool persistent kernel (v2) instead of
                                    the default one-pixel-per-lane wave kernel (v1) */
 #define RTX_FLAG_POOL4 16u      /* A/B: v2 with 4 instead of 2 pixel chunks per wave */
+#define RTX_FLAG_KERNEL_ITEMS 32u /* v3 (the default schedule when no other is chosen):
+                                     (pixel, sample) items, colours stored in HBM and summed
+                                     in sample order afterwards (RTX_SCRATCH_MB bounds the
+                                     per-device scratch, default 16 GiB; identical output) */
+#define RTX_FLAG_KERNEL_V1 64u    /* A/B: v1, one 8x8 tile per wave, one lane per pixel */
 /* Tuning: lanes of a wave that must wait before it shades (1..64; 0 = default, or the
  * RTX_SHADE_THRESH environment variable). */
 #define RTX_FLAG_SHADE_THRESH(n) (((uint32_t)(n)&0x7Fu) << 8)

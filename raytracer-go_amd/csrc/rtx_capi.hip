@@ -53,6 +53,17 @@ struct DeviceCopy {
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
 };
 
+// v3 sample-colour scratch, one per device, shared by all scenes (grown on demand and
+// kept for the process).  `last` marks its latest use, so a render on another stream
+// waits for the previous one before reusing it.
+struct Scratch {
+    float* ptr = nullptr;
+    size_t bytes = 0;
+    hipEvent_t last = nullptr;
+};
+std::mutex g_scratch_mu;
+std::map<int, Scratch> g_scratch;
+
 }  // namespace
 
 struct rtx_scene {
@@ -235,6 +246,13 @@ uint32_t region_rows(const rtx_region* r) {
     return (r->height - r->rank + r->world - 1) / r->world;
 }
 
+// Integer knob from the environment (read per call), clamped to [lo, hi].
+uint32_t env_knob(const char* name, long dflt, long lo, long hi) {
+    const char* e = std::getenv(name);
+    const long x = e ? std::strtol(e, nullptr, 10) : dflt;
+    return (uint32_t)(x < lo ? lo : (x > hi ? hi : x));
+}
+
 // Tuning knob of the v1 kernel (lanes waiting before a wave shades); RTX_SHADE_THRESH.
 uint32_t shade_thresh() {
     static const uint32_t v = [] {
@@ -292,9 +310,37 @@ int enqueue_on(rtx_scene* s, DeviceCopy* c, const rtx_camera* cam, uint64_t seed
     rtxd::Params p = make_params(s, c, cam, seed, r, d_out);
     const uint32_t th = (flags >> 8) & 0x7Fu;  // RTX_FLAG_SHADE_THRESH(n) override
     if (th) p.shade_thresh = th > 64 ? 64 : th;
+    Scratch* scr = nullptr;
+    std::unique_lock<std::mutex> scr_lock(g_scratch_mu, std::defer_lock);
+    if (rtxd::uses_items(p, flags)) {
+        // v3 scratch: up to RTX_SCRATCH_MB (default 16 GiB of the 288 GB HBM) of sample
+        // colours, 12 B each; the samples are rendered in chunks that fit.
+        const uint64_t per_sample = (uint64_t)p.width * p.rows * 12;
+        const uint64_t budget = (uint64_t)env_knob("RTX_SCRATCH_MB", 16384, 1, 1 << 20) << 20;
+        uint64_t chunk = per_sample ? budget / per_sample : 0;
+        if (chunk > cam->samples_per_pixel) chunk = cam->samples_per_pixel;
+        if (chunk < 1) return fail(RTX_ERR_OOM, "RTX_SCRATCH_MB too small for one sample of the region");
+        const size_t need = (size_t)(chunk * per_sample);
+        scr_lock.lock();
+        scr = &g_scratch[c->device];
+        if (!scr->last) HIP_TRY(hipEventCreateWithFlags(&scr->last, hipEventDisableTiming));
+        if (scr->bytes < need) {
+            HIP_TRY(hipEventSynchronize(scr->last));
+            if (scr->ptr) HIP_TRY(hipFree(scr->ptr));
+            scr->ptr = nullptr;
+            scr->bytes = 0;
+            HIP_TRY(hipMalloc(&scr->ptr, need));
+            scr->bytes = need;
+        }
+        HIP_TRY(hipStreamWaitEvent(stream, scr->last, 0));
+        p.scratch = scr->ptr;
+        p.kn = (uint32_t)chunk;
+        p.sub = env_knob("RTX_ITEM_SUB", 16, 1, 4096);
+    }
     if (flags & RTX_FLAG_COUNTERS) HIP_TRY(hipMemsetAsync(c->counters, 0, 16 * sizeof(unsigned long long), stream));
     if (timed) HIP_TRY(hipEventRecord(c->ev0, stream));
     HIP_TRY(rtxd::launch_render(p, flags, stream));
+    if (scr) HIP_TRY(hipEventRecord(scr->last, stream));
     if (timed) HIP_TRY(hipEventRecord(c->ev1, stream));
     return RTX_OK;
 }

@@ -228,6 +228,10 @@ struct Params {
     uint32_t* error_flag;          // v2: set to 1 by a wave that hit the watchdog
     uint64_t watchdog_ticks;       // v2: per-wave limit in s_memrealtime ticks (100 MHz)
     uint32_t has_uv;               // scene has an image texture (UV needed at hits)
+    // v3 (render_items): samples [k0, k0 + kn) of every pixel, one colour per sample
+    // into scratch[(k - k0) * width * rows + pixel] (3 floats), `sub` samples per unit.
+    float* scratch;
+    uint32_t k0, kn, sub;
 };
 
 struct Ray {

@@ -7,12 +7,15 @@
 // keyed by global pixel index and k), so a pixel's value does not depend on the tile,
 // the region, the scheduling or the number of GPUs.
 //
-// Three schedules of the same per-sample code (rtx_device.h), identical output:
-//  v1 render_wave   (default) persistent loop, one pixel per lane, path regeneration.
+// Four schedules of the same per-sample code (rtx_device.h), identical output:
+//  v3 render_items  (default) persistent waves over (pixel, sample) items; colours go
+//                   to an HBM scratch and reduce_samples sums them in sample order.
+//  v1 render_wave   one 8x8 tile per wave, one pixel per lane, path regeneration
+//                   (RTX_FLAG_KERNEL_V1; RTX_FLAG_WAVE_GEOM variants).
 //  v2 render_pool   persistent waves over a pool of pixels fed by a global tile queue;
 //                   lanes take any idle pixel of the pool (RTX_FLAG_KERNEL_POOL).
 //  v0 render_pixels thread per pixel, samples in a plain loop (the first version).
-// v1 and v2 step every traversing lane through one BVH entry per iteration and shade
+// v1-v3 step every traversing lane through BVH entries (three per wave vote) and shade
 // in batches: once `shade_thresh` lanes of the wave wait (or none traverses), all
 // waiting lanes shade together, so shading and its Philox blocks run in lockstep.
 #include <hip/hip_runtime.h>
@@ -289,6 +292,198 @@ __global__ __launch_bounds__(64 * WX * WY, MINW) void render_wave(Params p) {
             atomicAdd(&p.counters[14], (unsigned long long)idle_lanes);
         }
     }
+}
+
+// ------------------------------------------------------------------------------------
+// v3: persistent waves over (pixel, sample) items; the sum is formed afterwards.
+//
+// GetPixelColor's float32 sum (camera.go:256-261) must add a pixel's samples in order
+// k = 0..spp-1, which ties v1 to one lane per pixel: a wave lasts as long as its slowest
+// pixel, and an image with fewer 8x8 tiles than the device has wave slots (the Cornell
+// box: 5625 tiles, 4096 slots) leaves the GPU part-idle.  v3 spends HBM instead: every
+// sample's colour is stored (12 B; 12.4 GB for 1920x1080x500 of the 288 GB), and
+// reduce_samples adds each pixel's colours in k order afterwards — the same float32
+// operations in the same order, so the same bits.  The work is then a pool of
+// independent items: a wave claims units of (8x8 tile, `sub` consecutive samples) from a
+// global counter and hands the unit's items to its lanes in sample-major order as they
+// finish, so a wave stays on one tile (coherent rays) and no lane waits for another.
+// Samples beyond the scratch budget run in chunks [k0, k0 + kn); the running sum of a
+// pixel is carried in the output between chunks.
+// ------------------------------------------------------------------------------------
+template <bool COUNT, bool USE_LDS, bool QUADS>
+__global__ __launch_bounds__(256) void render_items(Params p) {
+    constexpr uint32_t WAVE_BLOCK = 256, STEPS = 3;
+    extern __shared__ float4 lds_entries[];
+    SceneRef E;
+    if constexpr (USE_LDS) {
+        const uint32_t n4 = 2 * p.n_entries + 4 * p.n_quads;
+        for (uint32_t t = threadIdx.x; t < n4; t += WAVE_BLOCK) lds_entries[t] = p.entries[t];
+        __syncthreads();
+        E = scene_ref(lds_entries, p.n_entries);
+    } else {
+        E = scene_ref(p.entries, p.n_entries);
+    }
+    const uint32_t n_entries = p.n_entries;
+    const uint32_t thresh = p.shade_thresh;
+    const uint32_t lane = threadIdx.x & 63u;
+    const rtx_camera& c = p.cam;
+    const uint32_t tiles_x = (p.width + 7u) / 8u;
+    const uint32_t n_tiles = tiles_x * ((p.rows + 7u) / 8u);
+    const uint32_t nsub = (p.kn + p.sub - 1u) / p.sub;
+    const uint64_t n_units = (uint64_t)n_tiles * nsub;
+    const size_t npix = (size_t)p.width * p.rows;
+
+    // the wave's unit (uniform): tile, first sample, items, next item
+    uint32_t u_tile = 0, u_k0 = 0, u_items = 0, cursor = 0;
+    bool exhausted = false;
+
+    uint32_t mode = M_CLAIM, seg = 0, items_done = 0;
+    size_t pix = 0;  // region-linear pixel of the lane's item
+    V3 base = v3(0.0f, 0.0f, 0.0f);
+    V3 thr = v3(1.0f, 1.0f, 1.0f), acc = v3(0.0f, 0.0f, 0.0f);
+    Ray r{v3(0, 0, 0), v3(0, 0, 0)};
+    PathRng rng{(uint32_t)p.seed, (uint32_t)(p.seed >> 32), 0u, 0u};
+    Trav t{};
+    Counters cnt{0, 0, 0, 0, 0, 0};
+    uint64_t wave_iters = 0, lane_steps = 0, shade_phases = 0, shade_lanes = 0;
+    uint64_t trav_cycles = 0, shade_cycles = 0, clk = 0, idle_lanes = 0;  // COUNT only
+
+    auto store = [&](V3 col) {  // the item's colour, GetColor's result for sample k
+        float* o = p.scratch + ((size_t)(rng.sample - p.k0) * npix + pix) * 3;
+        o[0] = col.x;
+        o[1] = col.y;
+        o[2] = col.z;
+        ++items_done;
+    };
+
+    for (;;) {
+        if (COUNT) clk = __builtin_amdgcn_s_memtime();
+        traverse_phase<COUNT, STEPS, QUADS>(mode, t, r, E, n_entries, thresh, cnt, wave_iters, lane_steps,
+                                            shade_phases, shade_lanes, idle_lanes);
+        if (COUNT) {
+            const uint64_t now = __builtin_amdgcn_s_memtime();
+            trav_cycles += now - clk;
+            clk = now;
+        }
+        if (__ballot(mode != M_DONE) == 0) break;
+
+        // ---- shading phase ----------------------------------------------------------
+        const Scatter sc = coop_scatter<QUADS>(p, E, rng, seg + 1, mode == M_SHADE ? t.hit : -1);
+        bool ready = false;
+        if (mode == M_SHADE) {
+            V3 color;
+            bool done = shade<COUNT, QUADS>(p, E, t, seg, r, thr, acc, rng, cnt, color, &sc);
+            ++seg;
+            if (!done && seg == c.max_depth) {  // depth exhausted: GetColor(0) = 0 (ray.go:33)
+                done = true;
+                color = acc;
+            }
+            if (done) {
+                store(color);
+                mode = M_CLAIM;
+            } else {
+                ready = true;
+            }
+        }
+        // Lanes without an item take the next ones of the wave's unit; new camera rays
+        // at one program point.  Loops only for max depth 0 and ragged tiles.
+        for (;;) {
+            const uint64_t wm = __ballot(mode == M_CLAIM);
+            if (wm == 0) break;
+            if (cursor >= u_items && !exhausted) {  // claim the next unit (wave-uniform)
+                uint32_t un = 0;
+                if (lane == 0) un = atomicAdd(p.tile_counter, 1u);
+                const uint64_t uu = (uint32_t)__shfl((int)un, 0);
+                exhausted = uu >= n_units;
+                if (!exhausted) {
+                    u_tile = (uint32_t)(uu / nsub);
+                    u_k0 = p.k0 + (uint32_t)(uu % nsub) * p.sub;
+                    const uint32_t cnt_k = min(p.sub, p.k0 + p.kn - u_k0);
+                    u_items = 64u * cnt_k;
+                    cursor = 0;
+                }
+            }
+            if (exhausted) {
+                if (mode == M_CLAIM) mode = M_DONE;
+                break;
+            }
+            const uint32_t rank = (uint32_t)__popcll(wm & ((1ull << lane) - 1ull));
+            bool got = false;
+            if (mode == M_CLAIM && rank < u_items - cursor) {
+                const uint32_t j = cursor + rank, l = j & 63u;  // sample-major within the unit
+                const uint32_t lx = (u_tile % tiles_x) * 8u + (l & 7u);
+                const uint32_t lr = (u_tile / tiles_x) * 8u + (l >> 3);
+                if (lx < p.width && lr < p.rows) {  // else: outside a ragged tile, claim again
+                    const uint32_t x = p.x0 + lx, y = p.y0 + p.rank + lr * p.world;
+                    base = pixel_base(c, x, y);
+                    rng.pixel = y * c.image_width + x;
+                    rng.sample = u_k0 + (j >> 6);
+                    pix = (size_t)lr * p.width + lx;
+                    got = true;
+                }
+            }
+            const uint32_t taken = (uint32_t)__popcll(wm);
+            cursor = cursor + taken > u_items ? u_items : cursor + taken;
+            if (got) {
+                r = camera_ray(c, base, rng, cnt.draws);  // GetRay, camera.go:257
+                thr = v3(1.0f, 1.0f, 1.0f);
+                acc = v3(0.0f, 0.0f, 0.0f);
+                seg = 0;
+                if (c.max_depth > 0) {
+                    mode = M_START;
+                    ready = true;
+                } else {
+                    store(acc);  // max depth 0: GetColor returns black
+                }
+            }
+        }
+        if (ready) {  // begin a segment: world.Hit (ray.go:36)
+            if (COUNT) ++cnt.segments;
+            trav_begin(t, r);
+            mode = n_entries > 0 ? M_TRAV : M_SHADE;
+        }
+        if (COUNT) shade_cycles += __builtin_amdgcn_s_memtime() - clk;
+    }
+    if (COUNT) {
+        flush_counters(p, items_done, cnt);
+        if (lane == 0) {
+            flush_sched(p, wave_iters, lane_steps, shade_phases, shade_lanes);
+            atomicAdd(&p.counters[12], (unsigned long long)trav_cycles);
+            atomicAdd(&p.counters[13], (unsigned long long)shade_cycles);
+            atomicAdd(&p.counters[14], (unsigned long long)idle_lanes);
+        }
+    }
+}
+
+// GetPixelColor's sum over the stored colours of samples [k0, k0 + kn), in k order
+// (camera.go:256-259), continued from the running sum in `out` when k0 > 0; the last
+// chunk applies Scale(1/spp) (camera.go:261).  One thread per pixel, coalesced reads.
+__global__ __launch_bounds__(256) void reduce_samples(Params p, uint32_t last) {
+    const size_t npix = (size_t)p.width * p.rows;
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= npix) return;
+    float* o = p.out + i * 3;
+    float sx = 0.0f, sy = 0.0f, sz = 0.0f;
+    if (p.k0 > 0) {
+        sx = o[0];
+        sy = o[1];
+        sz = o[2];
+    }
+    const float* src = p.scratch + i * 3;
+    for (uint32_t k = 0; k < p.kn; ++k, src += npix * 3) {
+        sx = sx + src[0];
+        sy = sy + src[1];
+        sz = sz + src[2];
+    }
+    if (last) {
+        const float inv = 1.0f / (float)p.cam.samples_per_pixel;
+        sx = sx * inv;
+        sy = sy * inv;
+        sz = sz * inv;
+    }
+    o[0] = sx;
+    o[1] = sy;
+    o[2] = sz;
 }
 
 // ------------------------------------------------------------------------------------
@@ -569,6 +764,44 @@ hipError_t launch_wave(const Params& p, uint32_t geom, bool use_lds, hipStream_t
     }
 }
 
+// v3: chunks of p.kn samples (the scratch holds one chunk), each rendered by a
+// resident-capacity grid of render_items and summed into p.out by reduce_samples.
+template <bool COUNT, bool QUADS>
+hipError_t launch_items(Params p, bool use_lds, hipStream_t stream) {
+    const size_t shmem = use_lds ? scene_lds_bytes(p) : 0;
+    const auto kern = use_lds ? render_items<COUNT, true, QUADS> : render_items<COUNT, false, QUADS>;
+    int dev = 0, cus = 0, per_cu = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256, shmem);
+    if (e != hipSuccess) return e;
+    if (per_cu < 1) per_cu = 1;
+    const uint32_t spp = p.cam.samples_per_pixel, chunk = p.kn;
+    const uint64_t tiles = (uint64_t)((p.width + 7) / 8) * ((p.rows + 7) / 8);
+    const uint64_t npix = (uint64_t)p.width * p.rows;
+    for (uint32_t k0 = 0; k0 < spp; k0 += chunk) {
+        p.k0 = k0;
+        p.kn = spp - k0 < chunk ? spp - k0 : chunk;
+        const uint64_t units = tiles * ((p.kn + p.sub - 1) / p.sub);
+        uint64_t blocks = (uint64_t)per_cu * cus;
+        if (blocks > (units + 3) / 4) blocks = (units + 3) / 4;  // no wave starts without a unit
+        e = hipMemsetAsync(p.tile_counter, 0, 2 * sizeof(uint32_t), stream);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(kern, dim3((uint32_t)blocks), dim3(256), shmem, stream, p);
+        hipLaunchKernelGGL(reduce_samples, dim3((uint32_t)((npix + 255) / 256)), dim3(256), 0, stream, p,
+                           (uint32_t)(k0 + p.kn >= spp));
+        e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
+bool uses_items(const Params& p, uint32_t flags) {
+    if (flags & (RTX_FLAG_KERNEL_V0 | RTX_FLAG_KERNEL_V1 | RTX_FLAG_KERNEL_POOL)) return false;
+    if (((flags >> 24) & 7u) != 0) return false;  // RTX_FLAG_WAVE_GEOM tunes v1
+    return p.width > 0 && p.rows > 0 && p.cam.samples_per_pixel > 0 && p.cam.max_depth > 0;
+}
+
 hipError_t launch_render(const Params& p, uint32_t flags, hipStream_t stream) {
     if (p.width == 0 || p.rows == 0) return hipSuccess;
     const bool count = (flags & RTX_FLAG_COUNTERS) != 0;
@@ -581,6 +814,10 @@ hipError_t launch_render(const Params& p, uint32_t flags, hipStream_t stream) {
         return hipGetLastError();
     }
     const bool use_lds = !(flags & RTX_FLAG_NO_LDS) && scene_lds_bytes(p) <= LDS_MAX_BYTES;
+    if (uses_items(p, flags) && p.scratch) {
+        if (quads) return count ? launch_items<true, true>(p, use_lds, stream) : launch_items<false, true>(p, use_lds, stream);
+        return count ? launch_items<true, false>(p, use_lds, stream) : launch_items<false, false>(p, use_lds, stream);
+    }
     // Scenes with quads (hittables.go:138-216) run the default v1 schedule built with the
     // three-kind step; the scheduling variants below are sphere-only.
     if (quads)

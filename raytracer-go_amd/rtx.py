@@ -30,6 +30,8 @@ RTX_FLAG_KERNEL_V0 = 2
 RTX_FLAG_NO_LDS = 4
 RTX_FLAG_KERNEL_POOL = 8
 RTX_FLAG_POOL4 = 16
+RTX_FLAG_KERNEL_ITEMS = 32
+RTX_FLAG_KERNEL_V1 = 64
 
 
 def RTX_FLAG_SHADE_THRESH(n: int) -> int:

@@ -15,11 +15,13 @@ import torch  # noqa: E402
 import rtx  # noqa: E402
 
 POOL = 8  # RTX_FLAG_KERNEL_POOL
-VARIANTS = {"v1": 0, "v2": POOL, "v0": rtx.RTX_FLAG_KERNEL_V0, "nolds": rtx.RTX_FLAG_NO_LDS, "p4": POOL | 16}
+V1 = rtx.RTX_FLAG_KERNEL_V1
+VARIANTS = {"v3": 0, "v1": V1, "v2": POOL, "v0": rtx.RTX_FLAG_KERNEL_V0, "nolds": rtx.RTX_FLAG_NO_LDS,
+            "v1nolds": V1 | rtx.RTX_FLAG_NO_LDS, "p4": POOL | 16}
 for _g in range(8):
-    VARIANTS[f"g{_g}"] = rtx.RTX_FLAG_WAVE_GEOM(_g)
+    VARIANTS[f"g{_g}"] = V1 | rtx.RTX_FLAG_WAVE_GEOM(_g)
 for _t in (1, 4, 8, 12, 16, 20, 24, 32, 40, 48, 56, 64):
-    VARIANTS[f"t{_t}"] = _t << 8  # RTX_FLAG_SHADE_THRESH (v1)
+    VARIANTS[f"t{_t}"] = _t << 8  # RTX_FLAG_SHADE_THRESH (default schedule)
     VARIANTS[f"v2t{_t}"] = (_t << 8) | POOL
 
 ap = argparse.ArgumentParser()

@@ -21,7 +21,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("pmc_dir")
 ap.add_argument("out")
 ap.add_argument("--workload", required=True)
-ap.add_argument("--kernel", default="render_wave<false")
+ap.add_argument("--kernel", default="render_items<false")
 args = ap.parse_args()
 
 vals = {"FETCH_SIZE": [], "WRITE_SIZE": []}

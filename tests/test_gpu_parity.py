@@ -163,14 +163,17 @@ def test_full_c2_properties(torch_cuda, spheres, dev_spheres):
     assert 2.0 < st.segments / st.samples < 4.0
 
 
+V1 = rtx.RTX_FLAG_KERNEL_V1
 KERNELS = {
-    "v1-wave": 0,
+    "v3-default": 0,
+    "v1-wave": V1,
     "v2-pool": rtx.RTX_FLAG_KERNEL_POOL,
     "v2-pool4": rtx.RTX_FLAG_KERNEL_POOL | rtx.RTX_FLAG_POOL4,
     "v0-pixels": rtx.RTX_FLAG_KERNEL_V0,
-    "v1-global-scene": rtx.RTX_FLAG_NO_LDS,
+    "v1-global-scene": V1 | rtx.RTX_FLAG_NO_LDS,
     "v2-global-scene": rtx.RTX_FLAG_KERNEL_POOL | rtx.RTX_FLAG_NO_LDS,
-    "v1-thresh1": rtx.RTX_FLAG_SHADE_THRESH(1),
+    "v1-thresh1": V1 | rtx.RTX_FLAG_SHADE_THRESH(1),
+    "v3-thresh1": rtx.RTX_FLAG_SHADE_THRESH(1),
     "v1-persistent": rtx.RTX_FLAG_WAVE_GEOM(1),
     "v1-1step": rtx.RTX_FLAG_WAVE_GEOM(2),
     "v1-4steps": rtx.RTX_FLAG_WAVE_GEOM(3),
@@ -178,6 +181,8 @@ KERNELS = {
     "v1-8waves-occ8": rtx.RTX_FLAG_WAVE_GEOM(5),
     "v1-1wave-blocks": rtx.RTX_FLAG_WAVE_GEOM(6),
     "v2-thresh64": rtx.RTX_FLAG_KERNEL_POOL | rtx.RTX_FLAG_SHADE_THRESH(64),
+    "v3-items-flag": rtx.RTX_FLAG_KERNEL_ITEMS,
+    "v3-global-scene": rtx.RTX_FLAG_NO_LDS,
 }
 
 
@@ -191,7 +196,7 @@ def test_every_kernel_variant_is_bit_exact(torch_cuda, spheres, dev_spheres, nam
     check_parity(gpu, spheres.desc, cam, 17, reg, st)
 
 
-@pytest.mark.parametrize("name", ["v1-wave", "v2-pool"])
+@pytest.mark.parametrize("name", ["v3-default", "v1-wave", "v2-pool"])
 def test_variant_shards(torch_cuda, spheres, dev_spheres, name):
     cam = spheres.camera(width=96, spp=3)
     full, _ = gpu_region(torch_cuda, dev_spheres, cam, 2, rtx.Region(0, 0, 96, cam.image_height, 0, 1),
@@ -258,3 +263,27 @@ def test_watchdog_reports_error(torch_cuda, spheres):
     res = subprocess.run([sys.executable, "-c", code], cwd=root, env=env, capture_output=True, text=True,
                          timeout=120)
     assert f"ERR {rtx.RTX_ERR_HIP}" in res.stdout, res.stdout + res.stderr
+
+
+def test_v3_chunked_scratch(torch_cuda, spheres, dev_spheres, monkeypatch):
+    """v3 with a 1 MB scratch: the 500 samples of a C2 window run in 14 chunks whose
+    running sums are carried in the output; same bits as the oracle."""
+    monkeypatch.setenv("RTX_SCRATCH_MB", "1")
+    monkeypatch.setenv("RTX_ITEM_SUB", "7")
+    cam = spheres.camera(width=1920, spp=500, depth=50)
+    reg = rtx.Region(1000, 700, 64, 36, 0, 1)
+    gpu, st = gpu_region(torch_cuda, dev_spheres, cam, 17, reg)
+    check_parity(gpu, spheres.desc, cam, 17, reg, st)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_v3_shards(torch_cuda, spheres, dev_spheres, world):
+    cam = spheres.camera(width=200, spp=4, depth=50)
+    H = cam.image_height
+    full, _ = gpu_region(torch_cuda, dev_spheres, cam, 5, rtx.Region(0, 0, 200, H, 0, 1), counters=False)
+    got = np.full_like(full, np.nan)
+    for rank in range(world):
+        part, _ = gpu_region(torch_cuda, dev_spheres, cam, 5, rtx.Region(0, 0, 200, H, rank, world),
+                             counters=False, flags=V1)
+        got[rank::world] = part
+    assert np.array_equal(full, got)
