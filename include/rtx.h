@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define RTX_ABI_VERSION 1
+#define RTX_ABI_VERSION 2
 
 /* ---- status codes ------------------------------------------------------------ */
 enum {
@@ -266,6 +266,26 @@ int rtx_render_region_device(rtx_scene* scene, const rtx_camera* cam, uint64_t s
 
 /* Number of output rows of a region shard: ceil((height - rank) / world). */
 uint32_t rtx_region_rows(const rtx_region* region);
+
+/* ---- PPM output on the GPU ---------------------------------
+ * Render's output tail, camera.go:183-188 and 212-215 with vec3.go:141-166: the P3
+ * header "P3\n<W> <H>\n255\n", then per pixel int(Clamp(0,1,float32(sqrt(c)))*255.999)
+ * for R, G, B as "%d %d %d\n" (a NaN channel prints Go's int(NaN) = MinInt64).     */
+
+/* Upper bound of the PPM text of a width x height image (header + 63 B per pixel). */
+uint64_t rtx_ppm_max_bytes(uint32_t width, uint32_t height);
+
+/* Encode a float32 RGB image in device memory (d_rgb, width*height*3, row-major) into
+ * device memory d_text (capacity bytes) on the current device and the given stream;
+ * synchronises that stream and stores the text length in *out_len.  Replaces the
+ * reference's per-pixel fmt.Sprintf + channel pipeline (camera.go:198-231).          */
+int rtx_encode_ppm_device(const float* d_rgb, uint32_t width, uint32_t height, char* d_text, uint64_t capacity,
+                          uint64_t* out_len, void* hip_stream);
+
+/* Render + encode on the current device and copy the PPM text to the caller's host
+ * buffer: the bytes (*Camera).Render(world, writer) writes (camera.go:180).  Blocking. */
+int rtx_render_ppm(rtx_scene* scene, const rtx_camera* cam, uint64_t seed, char* out_text, uint64_t capacity,
+                   uint64_t* out_len, rtx_stats* stats);
 
 #ifdef __cplusplus
 }

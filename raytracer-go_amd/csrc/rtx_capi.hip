@@ -7,6 +7,7 @@
 // thread-local message; nothing throws across the ABI.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -20,6 +21,7 @@
 #include "rtx_device.h"
 #include "rtx_kernel.h"
 #include "rtx_layout.h"
+#include "rtx_ppm.h"
 
 namespace {
 
@@ -561,6 +563,78 @@ int rtx_render(rtx_scene* s, const rtx_camera* cam, uint64_t seed, int n_gpus, f
             stats->kernel_ms = std::max(stats->kernel_ms, sts[d].kernel_ms);
         }
     }
+    return rc;
+}
+
+uint64_t rtx_ppm_max_bytes(uint32_t width, uint32_t height) { return rtxd::ppm_max_bytes(width, height); }
+
+int rtx_encode_ppm_device(const float* d_rgb, uint32_t width, uint32_t height, char* d_text, uint64_t capacity,
+                          uint64_t* out_len, void* hip_stream) {
+    g_last_error.clear();
+    if (!d_text || !out_len || (!d_rgb && (uint64_t)width * height)) return fail(RTX_ERR_INVALID_ARG, "NULL argument");
+    const uint64_t n = (uint64_t)width * height;
+    if (n > 0x7FFFFFFFull) return fail(RTX_ERR_INVALID_ARG, "image too large for the PPM encoder");
+    const uint64_t need = rtxd::ppm_max_bytes(width, height);
+    if (capacity < need) return fail(RTX_ERR_INVALID_ARG, "capacity %llu < rtx_ppm_max_bytes %llu",
+                                     (unsigned long long)capacity, (unsigned long long)need);
+    hipStream_t st = (hipStream_t)hip_stream;
+    char header[64];
+    const uint64_t hl = rtxd::ppm_header(width, height, header);
+    HIP_TRY(hipMemcpyAsync(d_text, header, hl, hipMemcpyHostToDevice, st));
+    uint64_t total = hl;
+    if (n) {
+        size_t sb = 0;
+        HIP_TRY(rtxd::ppm_scratch_bytes(n, &sb));
+        void* scratch = nullptr;
+        HIP_TRY(hipMalloc(&scratch, sb));
+        hipError_t e = rtxd::ppm_encode(d_rgb, width, height, d_text, scratch, sb, hl, st);
+        uint64_t last_off = 0;
+        uint32_t last_len = 0;
+        if (e == hipSuccess) e = hipMemcpyAsync(&last_off, rtxd::ppm_last_offset(scratch, n), 8, hipMemcpyDeviceToHost, st);
+        if (e == hipSuccess) e = hipMemcpyAsync(&last_len, rtxd::ppm_last_length(scratch, n), 4, hipMemcpyDeviceToHost, st);
+        if (e == hipSuccess) e = hipStreamSynchronize(st);
+        (void)hipFree(scratch);
+        HIP_TRY(e);
+        total += last_off + last_len;
+    } else {
+        HIP_TRY(hipStreamSynchronize(st));
+    }
+    *out_len = total;
+    return RTX_OK;
+}
+
+int rtx_render_ppm(rtx_scene* s, const rtx_camera* cam, uint64_t seed, char* out_text, uint64_t capacity,
+                   uint64_t* out_len, rtx_stats* stats) {
+    g_last_error.clear();
+    if (!s || !out_text || !out_len) return fail(RTX_ERR_INVALID_ARG, "NULL argument");
+    if (int rc = check_camera(cam)) return rc;
+    const uint32_t W = cam->image_width, H = cam->image_height;
+    const uint64_t need = rtxd::ppm_max_bytes(W, H);
+    float* rgb = nullptr;
+    char* text = nullptr;
+    hipStream_t st = nullptr;
+    auto cleanup = [&]() {
+        if (st) (void)hipStreamDestroy(st);
+        (void)hipFree(rgb);
+        (void)hipFree(text);
+    };
+    HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    if (hipMalloc(&rgb, std::max<size_t>(1, (size_t)W * H * 3 * sizeof(float))) != hipSuccess ||
+        hipMalloc(&text, need) != hipSuccess) {
+        cleanup();
+        return fail(RTX_ERR_OOM, "device buffers for a %ux%u PPM", W, H);
+    }
+    rtx_region reg{0, 0, W, H, 0, 1};
+    rtx_stats local;
+    int rc = rtx_render_region_device(s, cam, seed, &reg, rgb, st, 0, stats ? stats : &local);
+    uint64_t len = 0;
+    if (rc == RTX_OK) rc = rtx_encode_ppm_device(rgb, W, H, text, need, &len, st);
+    if (rc == RTX_OK && len > capacity) rc = fail(RTX_ERR_INVALID_ARG, "capacity %llu < PPM length %llu",
+                                                  (unsigned long long)capacity, (unsigned long long)len);
+    if (rc == RTX_OK && hipMemcpy(out_text, text, len, hipMemcpyDeviceToHost) != hipSuccess)
+        rc = fail(RTX_ERR_HIP, "copying the PPM text to the host");
+    cleanup();
+    if (rc == RTX_OK) *out_len = len;
     return rc;
 }
 

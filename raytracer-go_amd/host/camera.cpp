@@ -6,6 +6,7 @@
 #include <cmath>
 #include <cstring>
 #include <fstream>
+#include <sstream>
 
 #include "internal.h"
 
@@ -126,11 +127,29 @@ std::string EncodePPM(const float* rgb, int w, int h) {  // camera.go:212-215, 2
 Error Camera::Render(const HittablePtr& world, std::ostream& writer) {  // camera.go:180-231
     init();
     const int W = (int)imageWidth, H = (int)imageHeight;
-    writer << "P3\n" << W << " " << H << "\n255\n";  // :183-188
+    std::ostringstream head;
+    head << "P3\n" << W << " " << H << "\n255\n";  // :183-188, written before rendering
+    writer << head.str();
     if (!writer) return Error{RTX_ERR_INVALID_ARG, "write failed"};
+    if (gpus <= 1) {  // one device: render and encode on the GPU (rtx_render_ppm)
+        FlatScene fs;
+        if (Error e = Flatten(world, fs)) return e;
+        if (samplesPerPixel <= 0) return Error{RTX_ERR_INVALID_ARG, "samplesPerPixel must be > 0"};
+        rtx_scene* scene = nullptr;
+        if (int rc = rtx_scene_create(&fs.desc, &scene)) return rtx_error(rc);
+        std::string text(rtx_ppm_max_bytes((uint32_t)W, (uint32_t)H), '\0');
+        uint64_t len = 0;
+        const int rc = rtx_render_ppm(scene, &derived_, seed, text.data(), text.size(), &len, nullptr);
+        rtx_scene_destroy(scene);
+        if (rc) return rtx_error(rc);
+        const size_t hl = head.str().size();  // the text repeats the header: skip it
+        writer.write(text.data() + hl, (std::streamsize)(len - hl));  // :237-251
+        if (!writer) return Error{RTX_ERR_INVALID_ARG, "write failed"};
+        return Error{};
+    }
     std::vector<float> rgb;
     if (Error e = RenderLinear(world, rgb)) return e;
-    writer << EncodePPM(rgb.data(), W, H);  // :237-251
+    writer << EncodePPM(rgb.data(), W, H);  // :237-251 (multi-GPU: gathered on the host)
     if (!writer) return Error{RTX_ERR_INVALID_ARG, "write failed"};
     return Error{};
 }

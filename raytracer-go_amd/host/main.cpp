@@ -1,6 +1,7 @@
 // main.cpp — the reference's main.go (main.go:22-78) on the GPU path.
 //
-//   rtx_main [scene] [width] [spp] [gpus]      scene: random_spheres (default), earth,
+//   rtx_main [scene] [width] [spp] [gpus]      scene: cornell_box (default, as main.go:55
+//                                              selects), random_spheres, quad_demo, earth,
 //                                              earth_dielectric, stress_100k
 // Writes out/img.ppm (file.go Overwrite) and prints the wall time like main.go:77.
 #include <chrono>
@@ -15,7 +16,7 @@ using namespace internal;
 
 int main(int argc, char** argv) {
     const auto now = std::chrono::steady_clock::now();
-    const std::string name = argc > 1 ? argv[1] : "random_spheres";
+    const std::string name = argc > 1 ? argv[1] : "cornell_box";  // main.go:55
     const int width = argc > 2 ? std::atoi(argv[2]) : 0;
     const int spp = argc > 3 ? std::atoi(argv[3]) : 0;
     const int gpus = argc > 4 ? std::atoi(argv[4]) : 1;

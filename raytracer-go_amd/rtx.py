@@ -108,6 +108,7 @@ class Stats(ctypes.Structure):
 RTX_SYMBOLS = [
     "rtx_version", "rtx_build_info", "rtx_last_error", "rtx_device_count", "rtx_scene_create",
     "rtx_scene_destroy", "rtx_scene_device_bytes", "rtx_render", "rtx_render_region_device", "rtx_region_rows",
+    "rtx_ppm_max_bytes", "rtx_encode_ppm_device", "rtx_render_ppm",
 ]
 RTXHOST_SYMBOLS = [
     "rtxhost_build_scene", "rtxhost_scene_free", "rtxhost_scene_desc", "rtxhost_scene_camera",
@@ -148,6 +149,13 @@ def load() -> ctypes.CDLL:
     L.rtx_render_region_device.restype = c_int
     L.rtx_region_rows.argtypes = [POINTER(Region)]
     L.rtx_region_rows.restype = c_uint32
+    L.rtx_ppm_max_bytes.argtypes = [c_uint32, c_uint32]
+    L.rtx_ppm_max_bytes.restype = c_uint64
+    L.rtx_encode_ppm_device.argtypes = [c_void_p, c_uint32, c_uint32, c_void_p, c_uint64, POINTER(c_uint64), c_void_p]
+    L.rtx_encode_ppm_device.restype = c_int
+    L.rtx_render_ppm.argtypes = [c_void_p, POINTER(Camera), c_uint64, c_void_p, c_uint64, POINTER(c_uint64),
+                                 POINTER(Stats)]
+    L.rtx_render_ppm.restype = c_int
     _lib = L
     return L
 
@@ -262,6 +270,15 @@ class DeviceScene:
         check(rc, "rtx_render")
         return out, st
 
+    def render_ppm(self, cam: Camera, seed: int) -> bytes:
+        """rtx_render_ppm: the P3 bytes Render writes, rendered and encoded on the GPU."""
+        L = load()
+        cap = int(L.rtx_ppm_max_bytes(cam.image_width, cam.image_height))
+        buf = ctypes.create_string_buffer(cap)
+        n = c_uint64()
+        check(L.rtx_render_ppm(self._h, ctypes.byref(cam), seed, buf, cap, ctypes.byref(n), None), "rtx_render_ppm")
+        return buf.raw[: n.value]
+
     def close(self) -> None:
         if self._h:
             load().rtx_scene_destroy(self._h)
@@ -287,3 +304,11 @@ def ppm_encode(rgb) -> bytes:
     buf = ctypes.create_string_buffer(int(n))
     H.rtxhost_ppm_encode(a.ctypes.data_as(c_void_p), w, h, buf, n)
     return buf.raw[: int(n)]
+
+
+def encode_ppm_device(rgb_ptr: int, width: int, height: int, text_ptr: int, capacity: int, stream: int = 0) -> int:
+    """rtx_encode_ppm_device on device buffers; returns the text length."""
+    n = c_uint64()
+    check(load().rtx_encode_ppm_device(rgb_ptr, width, height, text_ptr, capacity, ctypes.byref(n), stream),
+          "rtx_encode_ppm_device")
+    return n.value
