@@ -110,8 +110,11 @@ enum {
     RTX_TEX_CHECKERED = 1, /* scale, even[3], odd[3]                 materials.go:121-145 */
     RTX_TEX_IMAGE = 2,     /* width x height RGBA8 texels at texel_offset (row-major,
                               y down, as image.RGBA.At)             materials.go:165-193 */
-    RTX_TEX_NOISE = 3      /* Perlin; not on the GPU path (RTX_ERR_UNSUPPORTED)         */
+    RTX_TEX_NOISE = 3      /* Perlin: scale, and RTX_NOISE_TEXELS words at texel_offset:
+                              256 gradient vectors (x, y, z float32 bits), then permX,
+                              permY, permZ (256 indices each)        materials.go:195-295 */
 };
+#define RTX_NOISE_TEXELS 1536u
 typedef struct rtx_texture { /* 48 B */
     uint32_t type;
     float scale;

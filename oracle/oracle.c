@@ -484,6 +484,153 @@ static int world_hit(const ctx_t* cx, const ray_t* r, float tmin, float tmax, hi
     return hit_any;
 }
 
+/* Go's math.Sin (Go 1.21 src/math/sin.go, trig_reduce.go; pure Go on amd64, no FMA
+ * contraction with the default GOAMD64=v1): Cephes polynomials after Cody-Waite
+ * reduction by pi/4 in three parts, Payne-Hanek (trigReduce) from 2^29 up.  Used by
+ * NoiseTexture.GetTexture (materials.go:285-287).  The 4/pi words below are the binary
+ * expansion of 4/pi (Go's mPi4), computed with integer arithmetic. */
+static const uint64_t GO_MPI4[20] = {
+    0x0000000000000001ull, 0x45f306dc9c882a53ull, 0xf84eafa3ea69bb81ull, 0xb6c52b3278872083ull,
+    0xfca2c757bd778ac3ull, 0x6e48dc74849ba5c0ull, 0x0c925dd413a32439ull, 0xfc3bd63962534e7dull,
+    0xd1046bea5d768909ull, 0xd338e04d68befc82ull, 0x7323ac7306a673e9ull, 0x3908bf177bf25076ull,
+    0x3ff12fffbc0b301full, 0xde5e2316b414da3eull, 0xda6cfd9e4f96136eull, 0x9e8c7ecd3cbfd45aull,
+    0xea4f758fd7cbe2f6ull, 0x7a0e73ef14a525d4ull, 0xd7f6bf623f1aba10ull, 0xac06608df8f6d757ull};
+
+static void go_trig_reduce(double x, uint64_t* j_out, double* z_out) {
+    const double PI4 = 3.14159265358979323846 / 4;
+    if (x < PI4) {
+        *j_out = 0;
+        *z_out = x;
+        return;
+    }
+    uint64_t ix;
+    memcpy(&ix, &x, 8);
+    const int shift = 52, bias = 1023;
+    const uint64_t mask = 0x7FF;
+    const int exp = (int)((ix >> shift) & mask) - bias - shift;
+    ix &= ~(mask << shift);
+    ix |= 1ull << shift;
+    const unsigned digit = (unsigned)(exp + 61) / 64, bitshift = (unsigned)(exp + 61) % 64;
+    #define SHR(v, s) ((s) >= 64 ? 0ull : (v) >> (s))
+    const uint64_t z0 = (GO_MPI4[digit] << bitshift) | SHR(GO_MPI4[digit + 1], 64 - bitshift);
+    const uint64_t z1 = (GO_MPI4[digit + 1] << bitshift) | SHR(GO_MPI4[digit + 2], 64 - bitshift);
+    const uint64_t z2 = (GO_MPI4[digit + 2] << bitshift) | SHR(GO_MPI4[digit + 3], 64 - bitshift);
+    const unsigned __int128 p2 = (unsigned __int128)z2 * ix, p1 = (unsigned __int128)z1 * ix;
+    const uint64_t z2hi = (uint64_t)(p2 >> 64), z1hi = (uint64_t)(p1 >> 64), z1lo = (uint64_t)p1;
+    const uint64_t z0lo = z0 * ix;
+    const uint64_t lo = z1lo + z2hi;
+    const uint64_t c = lo < z1lo;
+    uint64_t hi = z0lo + z1hi + c;
+    uint64_t j = hi >> 61;
+    hi = hi << 3 | lo >> 61;
+    const unsigned lz = (unsigned)__builtin_clzll(hi);
+    const uint64_t e = (uint64_t)(bias - (lz + 1));
+    hi = (hi << (lz + 1)) | SHR(lo, 64 - (lz + 1));
+    hi >>= 64 - shift;
+    hi |= e << shift;
+    #undef SHR
+    double z;
+    memcpy(&z, &hi, 8);
+    if (j & 1) {
+        j++;
+        j &= 7;
+        z--;
+    }
+    *j_out = j;
+    *z_out = z * PI4;
+}
+
+double oracle_go_sin(double x) {
+    static const double S[6] = {1.58962301576546568060e-10, -2.50507477628578072866e-8, 2.75573136213857245213e-6,
+                                -1.98412698295895385996e-4, 8.33333333332211858878e-3, -1.66666666666666307295e-1};
+    static const double C[6] = {-1.13585365213876817300e-11, 2.08757008419747316778e-9, -2.75573141792967388112e-7,
+                                2.48015872888517045348e-5, -1.38888888888730564116e-3, 4.16666666666665929218e-2};
+    const double PI4A = 7.85398125648498535156e-1, PI4B = 3.77489470793079817668e-8,
+                 PI4C = 2.69515142907905952645e-15;
+    if (x == 0 || x != x) return x;
+    if (isinf(x)) return NAN;
+    int sign = 0;
+    if (x < 0) {
+        x = -x;
+        sign = 1;
+    }
+    uint64_t j;
+    double y, z;
+    if (x >= (double)(1 << 29)) {
+        go_trig_reduce(x, &j, &z);
+    } else {
+        j = (uint64_t)(x * (4 / 3.14159265358979323846));
+        y = (double)j;
+        if (j & 1) {
+            j++;
+            y++;
+        }
+        j &= 7;
+        z = ((x - y * PI4A) - y * PI4B) - y * PI4C;
+    }
+    if (j > 3) {
+        sign = !sign;
+        j -= 4;
+    }
+    const double zz = z * z;
+    if (j == 1 || j == 2)
+        y = 1.0 - 0.5 * zz + zz * zz * ((((((C[0] * zz) + C[1]) * zz + C[2]) * zz + C[3]) * zz + C[4]) * zz + C[5]);
+    else
+        y = z + z * zz * ((((((S[0] * zz) + S[1]) * zz + S[2]) * zz + S[3]) * zz + S[4]) * zz + S[5]);
+    return sign ? -y : y;
+}
+
+/* Perlin noise, materials.go:218-249, with math.go:58-92 (Lerp, BiLinearLerp,
+ * TriLinearLerp) as written.  tab = RTX_NOISE_TEXELS words (rtx.h). */
+static inline float go_lerp(float t, float x, float y) { return x * (1 - t) + y * t; }
+static inline float go_smoothstep(float t) { return t * t * (3 - 2 * t); }
+static inline int64_t go_int_f32_trunc(float v) {
+    if (v != v || v >= 9.2233720368547758e18f || v < -9.2233720368547758e18f) return INT64_MIN;
+    return (int64_t)v;
+}
+static float perlin_corner(const uint32_t* tab, int ix, int iy, int iz, float x, float y, float z) {
+    const uint32_t h = tab[768 + ix] ^ tab[1024 + iy] ^ tab[1280 + iz];
+    float g[3];
+    memcpy(g, &tab[3 * h], 12);
+    return g[0] * x + g[1] * y + g[2] * z; /* Dot(randVec3[h], (x, y, z)) */
+}
+static float perlin_noise(const uint32_t* tab, vec3 p) {
+    const float xi = (float)floor((double)p.x), yi = (float)floor((double)p.y), zi = (float)floor((double)p.z);
+    const float tx = p.x - xi, ty = p.y - yi, tz = p.z - zi;
+    const int rx0 = (int)(go_int_f32_trunc(xi) & 255), rx1 = (rx0 + 1) & 255;
+    const int ry0 = (int)(go_int_f32_trunc(yi) & 255), ry1 = (ry0 + 1) & 255;
+    const int rz0 = (int)(go_int_f32_trunc(zi) & 255), rz1 = (rz0 + 1) & 255;
+    const float c000 = perlin_corner(tab, rx0, ry0, rz0, tx, ty, tz);
+    const float c001 = perlin_corner(tab, rx0, ry0, rz1, tx, ty, tz - 1);
+    const float c010 = perlin_corner(tab, rx0, ry1, rz0, tx, ty - 1, tz);
+    const float c011 = perlin_corner(tab, rx0, ry1, rz1, tx, ty - 1, tz - 1);
+    const float c100 = perlin_corner(tab, rx1, ry0, rz0, tx - 1, ty, tz);
+    const float c101 = perlin_corner(tab, rx1, ry0, rz1, tx - 1, ty, tz - 1);
+    const float c110 = perlin_corner(tab, rx1, ry1, rz0, tx - 1, ty - 1, tz);
+    const float c111 = perlin_corner(tab, rx1, ry1, rz1, tx - 1, ty - 1, tz - 1);
+    const float sx = go_smoothstep(tx), sy = go_smoothstep(ty), sz = go_smoothstep(tz);
+    const float e = go_lerp(sy, go_lerp(sx, c000, c100), go_lerp(sx, c010, c110));
+    const float f = go_lerp(sy, go_lerp(sx, c001, c101), go_lerp(sx, c011, c111));
+    return go_lerp(sz, e, f);
+}
+static float perlin_turb(const uint32_t* tab, vec3 p, int depth) { /* materials.go:238-249 */
+    float sum = 0, weight = 1.0f;
+    for (int i = 0; i < depth; ++i) {
+        sum += weight * perlin_noise(tab, p);
+        weight *= 0.5f;
+        p = v_scale(p, 2);
+    }
+    return (float)fabs((double)sum);
+}
+/* NoiseTexture.GetTexture, materials.go:280-288. */
+static float noise_texture(const uint32_t* tab, float scale, vec3 p) {
+    p = v_scale(p, scale);
+    return 0.5f * (1 + (float)oracle_go_sin((double)(p.z + 10 * perlin_turb(tab, p, 7))));
+}
+float oracle_noise_texture(const uint32_t* tab, float scale, const float p[3]) {
+    return noise_texture(tab, scale, v3(p[0], p[1], p[2]));
+}
+
 /* ============================================================================
  * Textures and materials — internal/materials.go:9-193, 297-313.
  * ========================================================================== */
@@ -519,6 +666,10 @@ static vec3 texture_value(const ctx_t* cx, uint32_t ti, float u, float v, vec3 p
         const float col_scale = 1.0f / 65535.0f;
         uint32_t r8 = px & 0xFFu, g8 = (px >> 8) & 0xFFu, b8 = (px >> 16) & 0xFFu;
         return v3((float)(r8 * 257u) * col_scale, (float)(g8 * 257u) * col_scale, (float)(b8 * 257u) * col_scale);
+    }
+    case RTX_TEX_NOISE: {                                                   /* :267-288 */
+        const float g = noise_texture(&cx->s->texels[t->texel_offset], t->scale, p);
+        return v3(g, g, g);
     }
     default:
         return v3(0.0f, 0.0f, 0.0f);
@@ -705,7 +856,7 @@ static int scene_supported(const rtx_scene_desc* s) {
     for (uint32_t i = 0; i < s->n_materials; ++i)
         if (s->materials[i].type > RTX_MAT_DIFFUSE_LIGHT) return 0;
     for (uint32_t i = 0; i < s->n_textures; ++i)
-        if (s->textures[i].type > RTX_TEX_IMAGE) return 0;
+        if (s->textures[i].type > RTX_TEX_NOISE) return 0;
     if (s->n_quads && !s->quads) return 0;
     return 1;
 }

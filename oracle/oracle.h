@@ -100,6 +100,9 @@ void oracle_scene_free(oracle_scene* s);
 /* Go's math.Atan2 / math.Acos algorithms (the UV of hittables.go:122-123). */
 double oracle_go_atan2(double y, double x);
 double oracle_go_acos(double x);
+double oracle_go_sin(double x); /* Go 1.21 math.Sin (sin.go + trig_reduce.go) */
+/* NoiseTexture.GetTexture (materials.go:280-288) over an RTX_NOISE_TEXELS table. */
+float oracle_noise_texture(const uint32_t* tab, float scale, const float p[3]);
 
 /* Independent recompute of rtx_region_rows. */
 uint32_t oracle_region_rows(const rtx_region* r);

@@ -76,6 +76,7 @@ struct rtx_scene {
     std::vector<uint32_t> texels;
     std::map<int, DeviceCopy> copies;
     bool has_image = false;  // some texture is an ImageTexture: hits need UV
+    bool has_noise = false;  // some texture is a Perlin NoiseTexture
     std::mutex mu;
 };
 
@@ -303,6 +304,7 @@ rtxd::Params make_params(const rtx_scene* s, const DeviceCopy* c, const rtx_came
     p.watchdog_ticks = watchdog_ticks();
     p.shade_thresh = shade_thresh();
     p.has_uv = s->has_image ? 1u : 0u;
+    p.has_noise = s->has_noise ? 1u : 0u;
     return p;
 }
 
@@ -420,8 +422,13 @@ int rtx_scene_create(const rtx_scene_desc* d, rtx_scene** out) {
     }
     for (uint32_t i = 0; i < d->n_textures; ++i) {
         const rtx_texture& t = d->textures[i];
-        if (t.type == RTX_TEX_NOISE)
-            return fail(RTX_ERR_UNSUPPORTED, "NoiseTexture (Perlin, materials.go:195-295) is not on the GPU path");
+        if (t.type == RTX_TEX_NOISE) {
+            if ((uint64_t)t.texel_offset + RTX_NOISE_TEXELS > d->n_texels)
+                return fail(RTX_ERR_INVALID_ARG, "texture %u: Perlin tables out of range", i);
+            for (uint32_t k = 768; k < RTX_NOISE_TEXELS; ++k)
+                if (d->texels[t.texel_offset + k] > 255)
+                    return fail(RTX_ERR_INVALID_ARG, "texture %u: Perlin permutation entry out of range", i);
+        }
         if (t.type > RTX_TEX_NOISE) return fail(RTX_ERR_INVALID_ARG, "texture %u: unknown type %u", i, t.type);
         if (t.type == RTX_TEX_IMAGE && (int32_t)t.height > 0 &&
             (uint64_t)t.texel_offset + (uint64_t)t.width * t.height > d->n_texels)
@@ -447,7 +454,10 @@ int rtx_scene_create(const rtx_scene_desc* d, rtx_scene** out) {
     }
     s->materials.assign(d->materials, d->materials + d->n_materials);
     s->textures.assign(d->textures, d->textures + d->n_textures);
-    for (const rtx_texture& t : s->textures) s->has_image |= t.type == RTX_TEX_IMAGE;
+    for (const rtx_texture& t : s->textures) {
+        s->has_image |= t.type == RTX_TEX_IMAGE;
+        s->has_noise |= t.type == RTX_TEX_NOISE;
+    }
     if (d->n_texels) s->texels.assign(d->texels, d->texels + d->n_texels);
     int cur = 0;
     if (hipGetDevice(&cur) != hipSuccess) {

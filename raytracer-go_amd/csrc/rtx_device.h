@@ -126,6 +126,132 @@ __device__ __noinline__ UV sphere_uv(float nx, float ny, float nz) {
 }
 
 // ---------------------------------------------------------------------------------
+// Go's math.Sin (Go 1.21 sin.go + trig_reduce.go, pure Go on amd64) op for op, for
+// NoiseTexture.GetTexture (materials.go:285-287); oracle/oracle.c has the same.
+// ---------------------------------------------------------------------------------
+__constant__ uint64_t kGoMPi4[20] = {
+    0x0000000000000001ull, 0x45f306dc9c882a53ull, 0xf84eafa3ea69bb81ull, 0xb6c52b3278872083ull,
+    0xfca2c757bd778ac3ull, 0x6e48dc74849ba5c0ull, 0x0c925dd413a32439ull, 0xfc3bd63962534e7dull,
+    0xd1046bea5d768909ull, 0xd338e04d68befc82ull, 0x7323ac7306a673e9ull, 0x3908bf177bf25076ull,
+    0x3ff12fffbc0b301full, 0xde5e2316b414da3eull, 0xda6cfd9e4f96136eull, 0x9e8c7ecd3cbfd45aull,
+    0xea4f758fd7cbe2f6ull, 0x7a0e73ef14a525d4ull, 0xd7f6bf623f1aba10ull, 0xac06608df8f6d757ull};
+
+__device__ __noinline__ double go_sin(double x) {
+    const double S0 = 1.58962301576546568060e-10, S1 = -2.50507477628578072866e-8, S2 = 2.75573136213857245213e-6,
+                 S3 = -1.98412698295895385996e-4, S4 = 8.33333333332211858878e-3, S5 = -1.66666666666666307295e-1;
+    const double C0 = -1.13585365213876817300e-11, C1 = 2.08757008419747316778e-9, C2 = -2.75573141792967388112e-7,
+                 C3 = 2.48015872888517045348e-5, C4 = -1.38888888888730564116e-3, C5 = 4.16666666666665929218e-2;
+    const double PI4A = 7.85398125648498535156e-1, PI4B = 3.77489470793079817668e-8,
+                 PI4C = 2.69515142907905952645e-15;
+    if (x == 0 || x != x) return x;
+    if (__builtin_isinf(x)) return __builtin_nan("");
+    bool sign = false;
+    if (x < 0) {
+        x = -x;
+        sign = true;
+    }
+    uint64_t j;
+    double y, z;
+    if (x >= (double)(1 << 29)) {  // trigReduce (Payne-Hanek)
+        const double PI4 = 3.14159265358979323846 / 4;
+        uint64_t ix = (uint64_t)__double_as_longlong(x);
+        const int exp = (int)((ix >> 52) & 0x7FF) - 1023 - 52;
+        ix &= ~(0x7FFull << 52);
+        ix |= 1ull << 52;
+        const unsigned digit = (unsigned)(exp + 61) / 64, bs = (unsigned)(exp + 61) % 64;
+        auto shr = [](uint64_t v, unsigned s) { return s >= 64 ? 0ull : v >> s; };
+        const uint64_t z0 = (kGoMPi4[digit] << bs) | shr(kGoMPi4[digit + 1], 64 - bs);
+        const uint64_t z1 = (kGoMPi4[digit + 1] << bs) | shr(kGoMPi4[digit + 2], 64 - bs);
+        const uint64_t z2 = (kGoMPi4[digit + 2] << bs) | shr(kGoMPi4[digit + 3], 64 - bs);
+        const uint64_t z2hi = __umul64hi(z2, ix), z1hi = __umul64hi(z1, ix), z1lo = z1 * ix;
+        const uint64_t z0lo = z0 * ix;
+        const uint64_t lo = z1lo + z2hi;
+        uint64_t hi = z0lo + z1hi + (lo < z1lo ? 1ull : 0ull);
+        j = hi >> 61;
+        hi = hi << 3 | lo >> 61;
+        const unsigned lz = (unsigned)__builtin_clzll(hi);
+        const uint64_t e = (uint64_t)(1023 - (int)(lz + 1));
+        hi = (hi << (lz + 1)) | shr(lo, 64 - (lz + 1));
+        hi >>= 64 - 52;
+        hi |= e << 52;
+        z = __longlong_as_double((long long)hi);
+        if (j & 1) {
+            j++;
+            j &= 7;
+            z--;
+        }
+        z = z * PI4;
+    } else {
+        j = (uint64_t)(x * (4 / 3.14159265358979323846));
+        y = (double)j;
+        if (j & 1) {
+            j++;
+            y++;
+        }
+        j &= 7;
+        z = ((x - y * PI4A) - y * PI4B) - y * PI4C;
+    }
+    if (j > 3) {
+        sign = !sign;
+        j -= 4;
+    }
+    const double zz = z * z;
+    if (j == 1 || j == 2)
+        y = 1.0 - 0.5 * zz + zz * zz * ((((((C0 * zz) + C1) * zz + C2) * zz + C3) * zz + C4) * zz + C5);
+    else
+        y = z + z * zz * ((((((S0 * zz) + S1) * zz + S2) * zz + S3) * zz + S4) * zz + S5);
+    return sign ? -y : y;
+}
+
+// Perlin noise and turbulence (materials.go:218-249, math.go:58-92) over the
+// RTX_NOISE_TEXELS table of a NoiseTexture; NoiseTexture.GetTexture (:280-288).
+__device__ __forceinline__ float go_lerp(float t, float x, float y) { return x * (1 - t) + y * t; }
+__device__ __forceinline__ float go_smoothstep(float t) { return t * t * (3 - 2 * t); }
+__device__ __forceinline__ int go_cell(float v) {  // int(float32) & 255; out of range -> MinInt64 & 255 = 0
+    if (!(v >= -9.2233720368547758e18f && v < 9.2233720368547758e18f)) return 0;
+    return (int)((long long)v & 255);
+}
+__device__ __forceinline__ float perlin_corner(const uint32_t* __restrict__ tab, int ix, int iy, int iz, float x,
+                                               float y, float z) {
+    const uint32_t h = tab[768 + ix] ^ tab[1024 + iy] ^ tab[1280 + iz];
+    return __uint_as_float(tab[3 * h]) * x + __uint_as_float(tab[3 * h + 1]) * y + __uint_as_float(tab[3 * h + 2]) * z;
+}
+__device__ __noinline__ float noise_texture(const uint32_t* __restrict__ tab, float scale, float px, float py,
+                                             float pz) {
+    px = px * scale;
+    py = py * scale;
+    pz = pz * scale;
+    const float z0 = pz;
+    float sum = 0, weight = 1.0f;
+    for (int o = 0; o < 7; ++o) {  // Turb(point, 7)
+        const float xi = (float)__builtin_floor((double)px), yi = (float)__builtin_floor((double)py),
+                    zi = (float)__builtin_floor((double)pz);
+        const float tx = px - xi, ty = py - yi, tz = pz - zi;
+        const int rx0 = go_cell(xi), rx1 = (rx0 + 1) & 255;
+        const int ry0 = go_cell(yi), ry1 = (ry0 + 1) & 255;
+        const int rz0 = go_cell(zi), rz1 = (rz0 + 1) & 255;
+        const float c000 = perlin_corner(tab, rx0, ry0, rz0, tx, ty, tz);
+        const float c001 = perlin_corner(tab, rx0, ry0, rz1, tx, ty, tz - 1);
+        const float c010 = perlin_corner(tab, rx0, ry1, rz0, tx, ty - 1, tz);
+        const float c011 = perlin_corner(tab, rx0, ry1, rz1, tx, ty - 1, tz - 1);
+        const float c100 = perlin_corner(tab, rx1, ry0, rz0, tx - 1, ty, tz);
+        const float c101 = perlin_corner(tab, rx1, ry0, rz1, tx - 1, ty, tz - 1);
+        const float c110 = perlin_corner(tab, rx1, ry1, rz0, tx - 1, ty - 1, tz);
+        const float c111 = perlin_corner(tab, rx1, ry1, rz1, tx - 1, ty - 1, tz - 1);
+        const float sx = go_smoothstep(tx), sy = go_smoothstep(ty), sz = go_smoothstep(tz);
+        const float e = go_lerp(sy, go_lerp(sx, c000, c100), go_lerp(sx, c010, c110));
+        const float f = go_lerp(sy, go_lerp(sx, c001, c101), go_lerp(sx, c011, c111));
+        sum += weight * go_lerp(sz, e, f);
+        weight *= 0.5f;
+        px = px * 2;
+        py = py * 2;
+        pz = pz * 2;
+    }
+    const float turb = __builtin_fabsf(sum);
+    return 0.5f * (1 + (float)go_sin((double)(z0 + 10 * turb)));
+}
+
+// ---------------------------------------------------------------------------------
 // RNG contract (GPU-first): Philox4x32-10 keyed by the seed, one block
 // of four 32-bit words per (global pixel, sample, event, attempt); u = float32(w >> 8)
 // * 2^-24 in [0, 1) (the range of rand.Float32).  The reference's draw ORDER is kept:
@@ -228,6 +354,7 @@ struct Params {
     uint32_t* error_flag;          // v2: set to 1 by a wave that hit the watchdog
     uint64_t watchdog_ticks;       // v2: per-wave limit in s_memrealtime ticks (100 MHz)
     uint32_t has_uv;               // scene has an image texture (UV needed at hits)
+    uint32_t has_noise;            // scene has a Perlin NoiseTexture (v3 NOISE kernels)
     // v3 (render_items): samples [k0, k0 + kn) of every pixel, one colour per sample
     // into scratch[(k - k0) * width * rows + pixel] (3 floats), `sub` samples per unit.
     float* scratch;
@@ -274,8 +401,10 @@ __device__ __forceinline__ V3 pixel_base(const rtx_camera& c, uint32_t x, uint32
                scale(v3(c.pixel_dv[0], c.pixel_dv[1], c.pixel_dv[2]), (float)y));
 }
 
-// Texture.GetTexture, materials.go:127-193.
-template <bool COUNT>
+// Texture.GetTexture, materials.go:127-193, 267-288.  NOISE: the scene has a Perlin
+// texture (its evaluation is an out-of-line call that costs the caller registers, so
+// only kernels built for such scenes contain it).
+template <bool COUNT, bool NOISE = false>
 __device__ __forceinline__ V3 texture_value(const Params& p, uint32_t ti, float u, float v, V3 pt, Counters& cnt) {
     const rtx_texture& t = p.textures[ti];
     if (t.type == RTX_TEX_SOLID) return v3(t.even[0], t.even[1], t.even[2]);
@@ -285,6 +414,10 @@ __device__ __forceinline__ V3 texture_value(const Params& p, uint32_t ti, float 
         const int64_t y = (int64_t)__builtin_floorf(inv * pt.y);
         const int64_t z = (int64_t)__builtin_floorf(inv * pt.z);
         return ((x + y + z) & 1) == 0 ? v3(t.even[0], t.even[1], t.even[2]) : v3(t.odd[0], t.odd[1], t.odd[2]);
+    }
+    if (NOISE && t.type == RTX_TEX_NOISE) {
+        const float g = noise_texture(p.texels + t.texel_offset, t.scale, pt.x, pt.y, pt.z);
+        return v3(g, g, g);
     }
     // RTX_TEX_IMAGE
     if ((int32_t)t.height <= 0) return v3(0.0f, 1.0f, 1.0f);
@@ -483,7 +616,7 @@ __device__ __forceinline__ void trav_step(Trav& t, const Ray& r, const SceneRef 
 // Shade the result of segment `seg` (ray.go:36-53, materials.go:33-113).  Returns true
 // when the path ends, with its colour in `color`; otherwise r / thr hold the next
 // segment.  Lockstep RNG: every hitting lane evaluates block (seg+1, 0) first.
-template <bool COUNT, bool QUADS = false>
+template <bool COUNT, bool QUADS = false, bool NOISE = false>
 __device__ __forceinline__ bool shade(const Params& p, const SceneRef E, const Trav& t, uint32_t seg,
                                       Ray& r, V3& thr, V3& acc, const PathRng& rng, Counters& cnt, V3& color,
                                       const Scatter* pre = nullptr) {
@@ -546,7 +679,7 @@ __device__ __forceinline__ bool shade(const Params& p, const SceneRef E, const T
         if (m.type == RTX_MAT_LAMBERTIAN) {                     // materials.go:33-42
             V3 dir = add(n, s);
             if (near_zero(dir)) dir = n;
-            const V3 att = texture_value<COUNT>(p, m.texture, u, v, pt, cnt);
+            const V3 att = texture_value<COUNT, NOISE>(p, m.texture, u, v, pt, cnt);
             thr = mul(thr, att);
             r = Ray{pt, dir};
             return false;
@@ -579,7 +712,7 @@ __device__ __forceinline__ bool shade(const Params& p, const SceneRef E, const T
         return false;
     }
     // DiffuseLight: emit, never scatters (materials.go:303-313)
-    const V3 em = texture_value<COUNT>(p, m.texture, u, v, pt, cnt);
+    const V3 em = texture_value<COUNT, NOISE>(p, m.texture, u, v, pt, cnt);
     color = add(acc, mul(thr, em));
     return true;
 }

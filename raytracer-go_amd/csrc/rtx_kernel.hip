@@ -310,7 +310,7 @@ __global__ __launch_bounds__(64 * WX * WY, MINW) void render_wave(Params p) {
 // Samples beyond the scratch budget run in chunks [k0, k0 + kn); the running sum of a
 // pixel is carried in the output between chunks.
 // ------------------------------------------------------------------------------------
-template <bool COUNT, bool USE_LDS, bool QUADS>
+template <bool COUNT, bool USE_LDS, bool QUADS, bool NOISE>
 __global__ __launch_bounds__(256) void render_items(Params p) {
     constexpr uint32_t WAVE_BLOCK = 256, STEPS = 3;
     extern __shared__ float4 lds_entries[];
@@ -372,7 +372,7 @@ __global__ __launch_bounds__(256) void render_items(Params p) {
         bool ready = false;
         if (mode == M_SHADE) {
             V3 color;
-            bool done = shade<COUNT, QUADS>(p, E, t, seg, r, thr, acc, rng, cnt, color, &sc);
+            bool done = shade<COUNT, QUADS, NOISE>(p, E, t, seg, r, thr, acc, rng, cnt, color, &sc);
             ++seg;
             if (!done && seg == c.max_depth) {  // depth exhausted: GetColor(0) = 0 (ray.go:33)
                 done = true;
@@ -766,10 +766,10 @@ hipError_t launch_wave(const Params& p, uint32_t geom, bool use_lds, hipStream_t
 
 // v3: chunks of p.kn samples (the scratch holds one chunk), each rendered by a
 // resident-capacity grid of render_items and summed into p.out by reduce_samples.
-template <bool COUNT, bool QUADS>
+template <bool COUNT, bool QUADS, bool NOISE>
 hipError_t launch_items(Params p, bool use_lds, hipStream_t stream) {
     const size_t shmem = use_lds ? scene_lds_bytes(p) : 0;
-    const auto kern = use_lds ? render_items<COUNT, true, QUADS> : render_items<COUNT, false, QUADS>;
+    const auto kern = use_lds ? render_items<COUNT, true, QUADS, NOISE> : render_items<COUNT, false, QUADS, NOISE>;
     int dev = 0, cus = 0, per_cu = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
@@ -797,26 +797,36 @@ hipError_t launch_items(Params p, bool use_lds, hipStream_t stream) {
 }
 
 bool uses_items(const Params& p, uint32_t flags) {
+    const bool work = p.width > 0 && p.rows > 0 && p.cam.samples_per_pixel > 0 && p.cam.max_depth > 0;
+    if (p.has_noise) return work;  // Perlin scenes run v3 only (the NOISE instantiations)
     if (flags & (RTX_FLAG_KERNEL_V0 | RTX_FLAG_KERNEL_V1 | RTX_FLAG_KERNEL_POOL)) return false;
     if (((flags >> 24) & 7u) != 0) return false;  // RTX_FLAG_WAVE_GEOM tunes v1
-    return p.width > 0 && p.rows > 0 && p.cam.samples_per_pixel > 0 && p.cam.max_depth > 0;
+    return work;
+}
+
+template <bool COUNT>
+hipError_t launch_items_for(const Params& p, bool use_lds, hipStream_t stream) {
+    if (p.has_noise) return p.n_quads ? launch_items<COUNT, true, true>(p, use_lds, stream)
+                                      : launch_items<COUNT, false, true>(p, use_lds, stream);
+    return p.n_quads ? launch_items<COUNT, true, false>(p, use_lds, stream)
+                     : launch_items<COUNT, false, false>(p, use_lds, stream);
 }
 
 hipError_t launch_render(const Params& p, uint32_t flags, hipStream_t stream) {
     if (p.width == 0 || p.rows == 0) return hipSuccess;
     const bool count = (flags & RTX_FLAG_COUNTERS) != 0;
     const bool quads = p.n_quads > 0;
+    const bool use_lds = !(flags & RTX_FLAG_NO_LDS) && scene_lds_bytes(p) <= LDS_MAX_BYTES;
+    if (uses_items(p, flags)) {
+        if (!p.scratch) return hipErrorInvalidValue;  // the caller sizes the v3 scratch
+        return count ? launch_items_for<true>(p, use_lds, stream) : launch_items_for<false>(p, use_lds, stream);
+    }
     if (flags & RTX_FLAG_KERNEL_V0) {
         const dim3 grid((p.width + TILE_W - 1) / TILE_W, (p.rows + TILE_H - 1) / TILE_H);
         const auto kern = count ? (quads ? render_pixels<true, true> : render_pixels<true, false>)
                                 : (quads ? render_pixels<false, true> : render_pixels<false, false>);
         hipLaunchKernelGGL(kern, grid, dim3(BLOCK), 0, stream, p);
         return hipGetLastError();
-    }
-    const bool use_lds = !(flags & RTX_FLAG_NO_LDS) && scene_lds_bytes(p) <= LDS_MAX_BYTES;
-    if (uses_items(p, flags) && p.scratch) {
-        if (quads) return count ? launch_items<true, true>(p, use_lds, stream) : launch_items<false, true>(p, use_lds, stream);
-        return count ? launch_items<true, false>(p, use_lds, stream) : launch_items<false, false>(p, use_lds, stream);
     }
     // Scenes with quads (hittables.go:138-216) run the default v1 schedule built with the
     // three-kind step; the scheduling variants below are sphere-only.

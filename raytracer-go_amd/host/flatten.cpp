@@ -8,6 +8,8 @@
 // scan order, hittables.go:55-72).
 #include <unordered_map>
 
+#include <cstring>
+
 #include "internal.h"
 
 namespace internal {
@@ -51,8 +53,22 @@ struct Flattener {
                 if (img->rgba.size() != (size_t)img->W * img->H) return fail(RTX_ERR_INVALID_ARG, "image size mismatch");
                 fs.texels.insert(fs.texels.end(), img->rgba.begin(), img->rgba.end());
             }
-        } else if (dynamic_cast<const NoiseTexture*>(t.get())) {
-            return fail(RTX_ERR_UNSUPPORTED, "NoiseTexture (Perlin, materials.go:195-295) is not on the GPU path");
+        } else if (auto nt = dynamic_cast<const NoiseTexture*>(t.get())) {  // RTX_NOISE_TEXELS layout
+            const Perlin& per = nt->perlin;
+            if (per.randVec3.size() != 256 || per.permX.size() != 256 || per.permY.size() != 256 ||
+                per.permZ.size() != 256)
+                return fail(RTX_ERR_INVALID_ARG, "Perlin tables must hold 256 entries");
+            r.type = RTX_TEX_NOISE;
+            r.scale = nt->scale;
+            r.texel_offset = (uint32_t)fs.texels.size();
+            for (const Vec3& g : per.randVec3)
+                for (float c : {g.X, g.Y, g.Z}) {
+                    uint32_t bits;
+                    std::memcpy(&bits, &c, 4);
+                    fs.texels.push_back(bits);
+                }
+            for (const auto* perm : {&per.permX, &per.permY, &per.permZ})
+                for (int v : *perm) fs.texels.push_back((uint32_t)v);
         } else {
             return fail(RTX_ERR_UNSUPPORTED, "unknown Texture type");
         }

@@ -1,5 +1,6 @@
 // hittables.cpp — constructors of internal/hittables.go.  The intersection code
 // (Sphere.Hit :96-132, World.Hit :55-72) runs on the device.
+#include <algorithm>
 #include "internal.h"
 
 namespace internal {
@@ -58,8 +59,29 @@ std::vector<HittablePtr> Box(Vec3 a, Vec3 b, MaterialPtr mat) {  // hittables.go
 std::shared_ptr<SolidColor> NewSolidColor(float x, float y, float z) { return std::make_shared<SolidColor>(NewVec3(x, y, z)); }
 std::shared_ptr<Checkered> NewCheckered(float scale, Vec3 even, Vec3 odd) { return std::make_shared<Checkered>(scale, even, odd); }
 std::shared_ptr<ImageTexture> NewImageTexture(ImagePtr img) { return std::make_shared<ImageTexture>(std::move(img)); }
-std::shared_ptr<NoiseTexture> NewNoiseTexture(std::shared_ptr<Rand> randCtx, float scale) {
-    return std::make_shared<NoiseTexture>(std::move(randCtx), scale);
+static std::vector<int> Permute(std::vector<int> p) {  // materials.go:259-265, global rand
+    for (int i = (int)p.size() - 1; i > 0; --i) {
+        const int target = GlobalRand().Intn(i);
+        std::swap(p[i], p[target]);
+    }
+    return p;
+}
+
+Perlin NewPerlin(Rand& randCtx) {  // materials.go:202-216
+    const int pointCount = 256;
+    Perlin per;
+    per.randVec3.resize(pointCount);
+    for (int i = 0; i < pointCount; ++i) per.randVec3[i] = NewVec3RandRange32(randCtx, -1, 1);
+    std::vector<int> nums(pointCount);  // GetNums, :251-257
+    for (int i = 0; i < pointCount; ++i) nums[i] = i;
+    per.permX = Permute(nums);
+    per.permY = Permute(nums);
+    per.permZ = Permute(nums);
+    return per;
+}
+
+std::shared_ptr<NoiseTexture> NewNoiseTexture(std::shared_ptr<Rand> randCtx, float scale) {  // :290-295
+    return std::make_shared<NoiseTexture>(NewPerlin(*randCtx), scale);
 }
 std::shared_ptr<Lambertian> NewLambertian(TexturePtr albedo) { return std::make_shared<Lambertian>(std::move(albedo)); }
 std::shared_ptr<Metal> NewMetal(Vec3 albedo, float fuzz) { return std::make_shared<Metal>(albedo, fuzz); }

@@ -138,10 +138,17 @@ public:
     explicit ImageTexture(ImagePtr im) : img(std::move(im)) {}
     ImagePtr img;
 };
-class NoiseTexture : public Texture {  // Perlin; not on the GPU path (RTX_ERR_UNSUPPORTED)
+// Perlin, materials.go:195-295.  NewPerlin draws the 256 gradient vectors from randCtx
+// and the three permutations from the global rand (Permute, :259-265).
+struct Perlin {
+    std::vector<Vec3> randVec3;
+    std::vector<int> permX, permY, permZ;
+};
+Perlin NewPerlin(Rand& randCtx);
+class NoiseTexture : public Texture {  // materials.go:267-295
 public:
-    NoiseTexture(std::shared_ptr<Rand> r, float s) : rng(std::move(r)), scale(s) {}
-    std::shared_ptr<Rand> rng;
+    NoiseTexture(Perlin p, float s) : perlin(std::move(p)), scale(s) {}
+    Perlin perlin;
     float scale;
 };
 std::shared_ptr<SolidColor> NewSolidColor(float x, float y, float z);

@@ -2,6 +2,7 @@
 //
 //   rtx_main [scene] [width] [spp] [gpus]      scene: cornell_box (default, as main.go:55
 //                                              selects), random_spheres, quad_demo, earth,
+//                                              perlin_demo, simple_light_demo,
 //                                              earth_dielectric, stress_100k
 // Writes out/img.ppm (file.go Overwrite) and prints the wall time like main.go:77.
 #include <chrono>

@@ -220,6 +220,56 @@ SceneSpec CornellBox(uint64_t seed) {  // main.go:194-225 (main.go:55: the selec
     return s;
 }
 
+SceneSpec PerlinDemo(uint64_t seed) {  // main.go:106-130
+    SceneSpec s;
+    s.name = "perlin_demo";
+    s.aspect = 16.0f / 9.0f;
+    s.width = 400;
+    s.opts = {WithSamplesPerPixel(100),
+              WithMaxRayDepth(50),
+              WithLookFrom(NewVec3(13, 2, 3)),
+              WithLookAt(NewVec3(0, 0, 0)),
+              WithFOVDegrees(20),
+              WithDefocusAngleDegrees(0),
+              WithBackgroundColor(NewVec3(0.7f, 0.8f, 1))};
+    Seed(seed);                       // global rand: Permute (materials.go:259-265), BVH axis
+    auto randCtx = NewRand(seed);     // main.go:122-123, time-seeded in the reference
+    auto world = NewWorld();
+    auto perlinTex = NewNoiseTexture(randCtx, 4);
+    auto mat = NewLambertian(perlinTex);
+    world->Add(NewSphere(NewVec3(0, -1000, 0), 1000, mat));
+    world->Add(NewSphere(NewVec3(0, 2, 0), 2, mat));
+    s.world = NewBVHFromWorld(*world);
+    return s;
+}
+
+SceneSpec SimpleLightDemo(uint64_t seed) {  // main.go:162-192
+    SceneSpec s;
+    s.name = "simple_light_demo";
+    s.aspect = 16.0f / 9.0f;
+    s.width = 400;
+    s.opts = {WithSamplesPerPixel(500),
+              WithMaxRayDepth(50),
+              WithLookFrom(NewVec3(26, 3, 6)),
+              WithLookAt(NewVec3(0, 2, 0)),
+              WithFOVDegrees(20),
+              WithDefocusAngleDegrees(0),
+              WithBackgroundColor(NewVec3(0, 0, 0))};
+    Seed(seed);
+    auto randCtx = NewRand(seed);
+    auto world = NewWorld();
+    auto perlinTex = NewNoiseTexture(randCtx, 4);
+    auto mat = NewLambertian(perlinTex);
+    world->Add(NewSphere(NewVec3(0, -1000, 0), 1000, mat));
+    world->Add(NewSphere(NewVec3(0, 2, 0), 2, mat));
+    auto red = NewLambertian(NewSolidColor(1, 0, 0));
+    world->Add(NewSphere(NewVec3(-4, 2, 4), 2, red));
+    auto diffLight = NewDiffuseLight(NewSolidColor(4, 4, 4));
+    world->Add(NewSphere(NewVec3(0, 7, 0), 2, diffLight));
+    s.world = NewBVHFromWorld(*world);
+    return s;
+}
+
 bool BuildScene(const std::string& name, uint64_t seed, SceneSpec& out) {
     if (name == "random_spheres") out = RandSpheres(seed);
     else if (name == "stress_100k") out = StressSpheres(seed, 100000);
@@ -227,6 +277,8 @@ bool BuildScene(const std::string& name, uint64_t seed, SceneSpec& out) {
     else if (name == "earth") out = Earth(seed, 2048, 1024);
     else if (name == "quad_demo") out = QuadDemo(seed);
     else if (name == "cornell_box") out = CornellBox(seed);
+    else if (name == "perlin_demo") out = PerlinDemo(seed);
+    else if (name == "simple_light_demo") out = SimpleLightDemo(seed);
     else return false;
     return true;
 }

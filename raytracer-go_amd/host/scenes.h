@@ -37,8 +37,13 @@ SceneSpec QuadDemo(uint64_t seed);
 // = 18 quads, DiffuseLight(15) ceiling lamp, black background, 600x600 at 200 spp.
 SceneSpec CornellBox(uint64_t seed);
 
+// perlinDemo, main.go:106-130, and simpleLightDemo, main.go:162-192: Perlin
+// NoiseTexture(scale 4) spheres (+ a red sphere and a DiffuseLight(4) sphere).
+SceneSpec PerlinDemo(uint64_t seed);
+SceneSpec SimpleLightDemo(uint64_t seed);
+
 // By name: "random_spheres", "stress_100k", "earth_dielectric", "earth", "quad_demo",
-// "cornell_box".
+// "cornell_box", "perlin_demo", "simple_light_demo".
 bool BuildScene(const std::string& name, uint64_t seed, SceneSpec& out);
 
 }  // namespace internal

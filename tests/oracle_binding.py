@@ -76,6 +76,10 @@ def load():
     L.oracle_scene_free.restype = None
     L.oracle_region_rows.argtypes = [POINTER(rtx.Region)]
     L.oracle_region_rows.restype = c_uint32
+    L.oracle_go_sin.argtypes = [ctypes.c_double]
+    L.oracle_go_sin.restype = ctypes.c_double
+    L.oracle_noise_texture.argtypes = [POINTER(c_uint32), c_float, POINTER(c_float)]
+    L.oracle_noise_texture.restype = c_float
     _lib = L
     return L
 

@@ -111,9 +111,10 @@ def test_null_arguments(built):
     L.rtx_scene_destroy(None)  # no-op
 
 
-def test_noise_texture_is_unsupported(built):
+def test_noise_texture_validation(built):
+    """Perlin textures are on the GPU path; their RTX_NOISE_TEXELS tables must exist."""
     rc, msg = create(make_desc([sphere()], [lambertian()], [texture(rtx.RTX_TEX_NOISE)]))
-    assert rc == rtx.RTX_ERR_UNSUPPORTED and "Perlin" in msg
+    assert rc == rtx.RTX_ERR_INVALID_ARG and "Perlin tables out of range" in msg
 
 
 def test_quad_validation(built):
