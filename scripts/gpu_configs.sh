@@ -14,6 +14,8 @@ run c4_stress_100k --scene stress_100k --width 1920 --spp 100 && \
 run c5_earth_dielectric --scene earth_dielectric --width 3840 --spp 1000 --no-cpu && \
 run cornell_box --scene cornell_box --width 600 --spp 200 && \
 run quad_demo --scene quad_demo --width 400 --spp 100 && \
+run perlin_demo --scene perlin_demo --width 400 --spp 100 && \
+run simple_light_demo --scene simple_light_demo --width 400 --spp 500 && \
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_cornell" -o run --output-format csv -- \
     python bench.py --scene cornell_box --width 600 --spp 200 --steps 2 --warmup 1 --no-cpu > "$OUT/cornell_prof.log" 2>&1
 rc=$?
