@@ -270,6 +270,23 @@ int rtx_render_region_device(rtx_scene* scene, const rtx_camera* cam, uint64_t s
 /* Number of output rows of a region shard: ceil((height - rank) / world). */
 uint32_t rtx_region_rows(const rtx_region* region);
 
+/* ---- BVH build on the GPU ----------------------------------
+ * rtx_scene_create for NewBVHFromWorld(world) (bvh.go:138-185) of a World holding only
+ * spheres, with the BVH built on the current device instead of by the caller: spheres
+ * in World.Add order; the k-th NewBVH call (pre-order) takes Intn(3) from word
+ * bvh_draw0 + k of the global host stream of bvh_seed (the RNG contract, DESIGN.md
+ * §3), which is the axis the host builder draws.  The scene equals the one
+ * rtx_scene_create makes from the host-built tree (same entries, tests).  build_ms
+ * (optional) receives the build's wall time.                                        */
+int rtx_scene_create_spheres(const rtx_sphere* spheres, uint32_t n_spheres, const rtx_material* materials,
+                             uint32_t n_materials, const rtx_texture* textures, uint32_t n_textures,
+                             const uint32_t* texels, uint64_t n_texels, uint64_t bvh_seed, uint64_t bvh_draw0,
+                             rtx_scene** out, double* build_ms);
+
+/* Copy the scene's threaded BVH entries (32 B each, rtx_layout.h order) to out when
+ * cap is large enough; returns their size in bytes.  For tests and tools.            */
+uint64_t rtx_scene_export(const rtx_scene* scene, void* out, uint64_t cap);
+
 /* ---- PPM output on the GPU ---------------------------------
  * Render's output tail, camera.go:183-188 and 212-215 with vec3.go:141-166: the P3
  * header "P3\n<W> <H>\n255\n", then per pixel int(Clamp(0,1,float32(sqrt(c)))*255.999)

@@ -40,6 +40,14 @@ int rtxhost_render_ppm(const char* scene_name, uint64_t scene_seed, int32_t imag
  * returns the byte count, writing at most cap bytes (call with cap = 0 to size). */
 uint64_t rtxhost_ppm_encode(const float* rgb, uint32_t width, uint32_t height, char* out, uint64_t cap);
 
+/* The World the scene's BVH was built from, in World.Add order: its spheres (material
+ * indices into rtxhost_scene_desc's table; at most cap written), the global-rand
+ * position at NewBVHFromWorld and the scene seed — the inputs of
+ * rtx_scene_create_spheres.  Returns the sphere count, or a negative rtx error code
+ * if the World holds other primitives. */
+int64_t rtxhost_scene_world_spheres(const rtxhost_scene* s, rtx_sphere* out, uint64_t cap, uint64_t* bvh_draw0,
+                                    uint64_t* seed);
+
 /* Last error of this thread from an rtxhost_* call. */
 const char* rtxhost_last_error(void);
 

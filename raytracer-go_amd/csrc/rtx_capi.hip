@@ -22,6 +22,7 @@
 #include "rtx_kernel.h"
 #include "rtx_layout.h"
 #include "rtx_ppm.h"
+#include "rtx_bvh.h"
 
 namespace {
 
@@ -376,32 +377,8 @@ int collect_on(DeviceCopy* c, bool count, uint64_t samples, rtx_stats* st) {
     return RTX_OK;
 }
 
-}  // namespace
-
-extern "C" {
-
-int rtx_version(void) { return RTX_ABI_VERSION; }
-
-const char* rtx_build_info(void) {
-    return "librtx gfx950 megakernel v1 (persistent wave loop, LDS scene, threaded pre-order BVH); built " __DATE__ " " __TIME__;
-}
-
-const char* rtx_last_error(void) { return g_last_error.c_str(); }
-
-int rtx_device_count(void) {
-    int n = 0;
-    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
-    return n;
-}
-
-uint32_t rtx_region_rows(const rtx_region* region) { return region ? region_rows(region) : 0; }
-
-int rtx_scene_create(const rtx_scene_desc* d, rtx_scene** out) {
-    g_last_error.clear();
-    if (!d || !out) return fail(RTX_ERR_INVALID_ARG, "NULL argument");
-    *out = nullptr;
-    if (d->n_roots == 0 || !d->roots) return fail(RTX_ERR_INVALID_ARG, "scene has no root");
-    if (d->n_nodes && !d->nodes) return fail(RTX_ERR_INVALID_ARG, "nodes is NULL");
+// Checks of the tables every scene shares (materials, textures, texels, primitives).
+int validate_tables(const rtx_scene_desc* d) {
     if (d->n_spheres && !d->spheres) return fail(RTX_ERR_INVALID_ARG, "spheres is NULL");
     if (d->n_materials && !d->materials) return fail(RTX_ERR_INVALID_ARG, "materials is NULL");
     if (d->n_textures && !d->textures) return fail(RTX_ERR_INVALID_ARG, "textures is NULL");
@@ -434,14 +411,12 @@ int rtx_scene_create(const rtx_scene_desc* d, rtx_scene** out) {
             (uint64_t)t.texel_offset + (uint64_t)t.width * t.height > d->n_texels)
             return fail(RTX_ERR_INVALID_ARG, "texture %u texels out of range", i);
     }
-    if (int rc = check_acyclic(d)) return rc;
-    rtx_scene* s = new rtx_scene();
-    for (uint32_t i = 0; i < d->n_roots; ++i) {
-        if (int rc = emit(d, d->roots[i], s->entries)) {
-            delete s;
-            return rc;
-        }
-    }
+    return RTX_OK;
+}
+
+// Quad table, materials, textures and texels of a scene whose entries are built; then
+// the copy on the current device.  Takes ownership of s (deleted on failure).
+int finish_scene(rtx_scene* s, const rtx_scene_desc* d, rtx_scene** out) {
     s->quadtab.resize((size_t)d->n_quads * 16);
     for (uint32_t i = 0; i < d->n_quads; ++i) {  // (Q, material), (u, 0), (v, 0), (w, 0)
         const rtx_quad& q = d->quads[i];
@@ -472,6 +447,83 @@ int rtx_scene_create(const rtx_scene_desc* d, rtx_scene** out) {
     }
     *out = s;
     return RTX_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int rtx_version(void) { return RTX_ABI_VERSION; }
+
+const char* rtx_build_info(void) {
+    return "librtx gfx950 megakernel v1 (persistent wave loop, LDS scene, threaded pre-order BVH); built " __DATE__ " " __TIME__;
+}
+
+const char* rtx_last_error(void) { return g_last_error.c_str(); }
+
+int rtx_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+uint32_t rtx_region_rows(const rtx_region* region) { return region ? region_rows(region) : 0; }
+
+int rtx_scene_create(const rtx_scene_desc* d, rtx_scene** out) {
+    g_last_error.clear();
+    if (!d || !out) return fail(RTX_ERR_INVALID_ARG, "NULL argument");
+    *out = nullptr;
+    if (d->n_roots == 0 || !d->roots) return fail(RTX_ERR_INVALID_ARG, "scene has no root");
+    if (d->n_nodes && !d->nodes) return fail(RTX_ERR_INVALID_ARG, "nodes is NULL");
+    if (int rc = validate_tables(d)) return rc;
+    if (int rc = check_acyclic(d)) return rc;
+    rtx_scene* s = new rtx_scene();
+    for (uint32_t i = 0; i < d->n_roots; ++i) {
+        if (int rc = emit(d, d->roots[i], s->entries)) {
+            delete s;
+            return rc;
+        }
+    }
+    return finish_scene(s, d, out);
+}
+
+int rtx_scene_create_spheres(const rtx_sphere* spheres, uint32_t n_spheres, const rtx_material* materials,
+                             uint32_t n_materials, const rtx_texture* textures, uint32_t n_textures,
+                             const uint32_t* texels, uint64_t n_texels, uint64_t bvh_seed, uint64_t bvh_draw0,
+                             rtx_scene** out, double* build_ms) {
+    g_last_error.clear();
+    if (!out || !spheres) return fail(RTX_ERR_INVALID_ARG, "NULL argument");
+    *out = nullptr;
+    if (n_spheres == 0) return fail(RTX_ERR_INVALID_ARG, "empty World (NewBVH indexes h[0], bvh.go:164)");
+    if (n_spheres > (1u << 25)) return fail(RTX_ERR_INVALID_ARG, "too many spheres for the GPU BVH build");
+    rtx_scene_desc d{};
+    d.spheres = spheres;
+    d.n_spheres = n_spheres;
+    d.materials = materials;
+    d.n_materials = n_materials;
+    d.textures = textures;
+    d.n_textures = n_textures;
+    d.texels = texels;
+    d.n_texels = n_texels;
+    if (int rc = validate_tables(&d)) return rc;
+    int cur = 0;
+    if (hipGetDevice(&cur) != hipSuccess) return fail(RTX_ERR_NO_DEVICE, "no HIP device");
+    rtx_scene* s = new rtx_scene();
+    double ms = 0;
+    hipError_t e = rtxd::build_sphere_bvh(spheres, n_spheres, bvh_seed, bvh_draw0, s->entries, &ms);
+    if (e != hipSuccess) {
+        delete s;
+        return fail(e == hipErrorOutOfMemory ? RTX_ERR_OOM : RTX_ERR_HIP, "GPU BVH build: %s", hipGetErrorString(e));
+    }
+    if (build_ms) *build_ms = ms;
+    return finish_scene(s, &d, out);
+}
+
+uint64_t rtx_scene_export(const rtx_scene* s, void* out, uint64_t cap) {
+    if (!s) return 0;
+    const uint64_t bytes = s->entries.size() * sizeof(rtx_entry);
+    if (out && cap >= bytes) std::memcpy(out, s->entries.data(), bytes);
+    return bytes;
 }
 
 void rtx_scene_destroy(rtx_scene* s) {

@@ -43,6 +43,29 @@ int rtxhost_build_scene(const char* name, uint64_t seed, rtxhost_scene** out) {
 
 void rtxhost_scene_free(rtxhost_scene* s) { delete s; }
 
+int64_t rtxhost_scene_world_spheres(const rtxhost_scene* s, rtx_sphere* out, uint64_t cap, uint64_t* bvh_draw0,
+                                    uint64_t* seed) {
+    g_err.clear();
+    if (!s || !s->spec.list) return set_err(Error{RTX_ERR_INVALID_ARG, "scene has no World list"});
+    const auto& hs = s->spec.list->hittables;
+    for (size_t i = 0; i < hs.size(); ++i) {
+        auto sp = dynamic_cast<const Sphere*>(hs[i].get());
+        if (!sp) return set_err(Error{RTX_ERR_UNSUPPORTED, "the World holds a non-sphere"});
+        auto it = s->flat.mat_index.find(sp->Mat.get());
+        if (it == s->flat.mat_index.end()) return set_err(Error{RTX_ERR_INVALID_ARG, "material not flattened"});
+        if (out && i < cap) {
+            rtx_sphere r{};
+            r.center[0] = sp->Center.X; r.center[1] = sp->Center.Y; r.center[2] = sp->Center.Z;
+            r.radius = sp->Radius;
+            r.material = it->second;
+            out[i] = r;
+        }
+    }
+    if (bvh_draw0) *bvh_draw0 = s->spec.bvh_draw0;
+    if (seed) *seed = s->spec.seed;
+    return (int64_t)hs.size();
+}
+
 const rtx_scene_desc* rtxhost_scene_desc(const rtxhost_scene* s) { return s ? &s->flat.desc : nullptr; }
 
 static CameraPtr make_camera(const SceneSpec& spec, int32_t w, int32_t spp, int32_t depth, uint64_t seed, int gpus) {

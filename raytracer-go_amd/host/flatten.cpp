@@ -183,6 +183,7 @@ Error Flatten(const HittablePtr& world, FlatScene& fs) {
         if (!f.ref(world, r)) return f.err;
         fs.roots.push_back(r);
     }
+    fs.mat_index = f.mats;
     rtx_scene_desc& d = fs.desc;
     d = rtx_scene_desc{};
     d.nodes = fs.nodes.data();

@@ -16,6 +16,7 @@
 #include <memory>
 #include <ostream>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/rtx.h"
@@ -298,6 +299,7 @@ struct FlatScene {
     std::vector<rtx_texture> textures;
     std::vector<uint32_t> texels;
     rtx_scene_desc desc{};  // views into the vectors above (valid while FlatScene lives)
+    std::unordered_map<const Material*, uint32_t> mat_index;  // Material -> materials[]
 };
 Error Flatten(const HittablePtr& world, FlatScene& out);
 

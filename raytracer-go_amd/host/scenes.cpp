@@ -69,6 +69,8 @@ SceneSpec RandSpheres(uint64_t seed) {
     world->Add(NewSphere(NewVec3(0, 1, 0), 1, NewDielectric(1.5f)));                         // :278-279
     world->Add(NewSphere(NewVec3(-4, 1, 0), 1, NewLambertian(NewSolidColor(0.4f, 0.2f, 0.1f))));  // :281-282
     world->Add(NewSphere(NewVec3(4, 1, 0), 1, NewMetal(NewVec3(0.7f, 0.6f, 0.5f), 0)));      // :284-285
+    s.list = world;
+    s.bvh_draw0 = GlobalRand().Drawn();
     s.world = NewBVHFromWorld(*world);                                                        // :287
     return s;
 }
@@ -89,6 +91,8 @@ SceneSpec StressSpheres(uint64_t seed, int n) {
         const float cz = -158.0f + 316.0f * g.Float32();
         world->Add(NewSphere(NewVec3(cx, 0.2f, cz), 0.2f, random_material(*randCtx, matPer, 0.8f, 0.95f)));
     }
+    s.list = world;
+    s.bvh_draw0 = GlobalRand().Drawn();
     s.world = NewBVHFromWorld(*world);
     return s;
 }
@@ -140,6 +144,8 @@ SceneSpec EarthDielectric(uint64_t seed, int tex_w, int tex_h) {
     world->Add(NewSphere(NewVec3(0, 1, 0), 1, earth));
     world->Add(NewSphere(NewVec3(-4, 1, 0), 1, NewDielectric(1.5f)));
     world->Add(NewSphere(NewVec3(4, 1, 0), 1, NewMetal(NewVec3(0.7f, 0.6f, 0.5f), 0)));
+    s.list = world;
+    s.bvh_draw0 = GlobalRand().Drawn();
     s.world = NewBVHFromWorld(*world);
     return s;
 }
@@ -158,6 +164,8 @@ SceneSpec Earth(uint64_t seed, int tex_w, int tex_h) {  // main.go:80-104
     auto world = NewWorld();
     auto mat = NewLambertian(NewImageTexture(SyntheticEarth(seed, tex_w, tex_h)));
     world->Add(NewSphere(NewVec3(0, 0, 0), 2, mat));
+    s.list = world;
+    s.bvh_draw0 = GlobalRand().Drawn();
     s.world = NewBVHFromWorld(*world);
     return s;
 }
@@ -186,6 +194,8 @@ SceneSpec QuadDemo(uint64_t seed) {  // main.go:132-160
     world->Add(NewQuad(NewVec3(3, -2, 1), NewVec3(0, 0, 4), NewVec3(0, 4, 0), rightBlue));
     world->Add(NewQuad(NewVec3(-2, 3, 1), NewVec3(4, 0, 0), NewVec3(0, 0, 4), upperOrange));
     world->Add(NewQuad(NewVec3(-2, -3, 5), NewVec3(4, 0, 0), NewVec3(0, 0, -4), lowerTeal));
+    s.list = world;
+    s.bvh_draw0 = GlobalRand().Drawn();
     s.world = NewBVHFromWorld(*world);
     return s;
 }
@@ -216,6 +226,8 @@ SceneSpec CornellBox(uint64_t seed) {  // main.go:194-225 (main.go:55: the selec
     world->Add(NewQuad(NewVec3(0, 0, 555), NewVec3(555, 0, 0), NewVec3(0, 555, 0), white));
     world->Add(Box(NewVec3(130, 0, 65), NewVec3(295, 165, 230), white));
     world->Add(Box(NewVec3(265, 0, 295), NewVec3(430, 330, 460), white));
+    s.list = world;
+    s.bvh_draw0 = GlobalRand().Drawn();
     s.world = NewBVHFromWorld(*world);
     return s;
 }
@@ -239,6 +251,8 @@ SceneSpec PerlinDemo(uint64_t seed) {  // main.go:106-130
     auto mat = NewLambertian(perlinTex);
     world->Add(NewSphere(NewVec3(0, -1000, 0), 1000, mat));
     world->Add(NewSphere(NewVec3(0, 2, 0), 2, mat));
+    s.list = world;
+    s.bvh_draw0 = GlobalRand().Drawn();
     s.world = NewBVHFromWorld(*world);
     return s;
 }
@@ -266,6 +280,8 @@ SceneSpec SimpleLightDemo(uint64_t seed) {  // main.go:162-192
     world->Add(NewSphere(NewVec3(-4, 2, 4), 2, red));
     auto diffLight = NewDiffuseLight(NewSolidColor(4, 4, 4));
     world->Add(NewSphere(NewVec3(0, 7, 0), 2, diffLight));
+    s.list = world;
+    s.bvh_draw0 = GlobalRand().Drawn();
     s.world = NewBVHFromWorld(*world);
     return s;
 }
@@ -280,6 +296,7 @@ bool BuildScene(const std::string& name, uint64_t seed, SceneSpec& out) {
     else if (name == "perlin_demo") out = PerlinDemo(seed);
     else if (name == "simple_light_demo") out = SimpleLightDemo(seed);
     else return false;
+    out.seed = seed;
     return true;
 }
 

@@ -14,6 +14,11 @@ struct SceneSpec {
     float aspect = 16.0f / 9.0f;
     int width = 400;
     std::vector<CameraOpt> opts;  // NewCamera options as main.go sets them
+    // The World passed to NewBVHFromWorld and the global-rand position at that call
+    // (the inputs of the GPU BVH build, rtx_scene_create_spheres), and the seed.
+    std::shared_ptr<World> list;
+    uint64_t bvh_draw0 = 0;
+    uint64_t seed = 0;
 };
 
 // randSpheres, main.go:227-289 — the north-star scene (configs 1-3).

@@ -108,11 +108,11 @@ class Stats(ctypes.Structure):
 RTX_SYMBOLS = [
     "rtx_version", "rtx_build_info", "rtx_last_error", "rtx_device_count", "rtx_scene_create",
     "rtx_scene_destroy", "rtx_scene_device_bytes", "rtx_render", "rtx_render_region_device", "rtx_region_rows",
-    "rtx_ppm_max_bytes", "rtx_encode_ppm_device", "rtx_render_ppm",
+    "rtx_ppm_max_bytes", "rtx_encode_ppm_device", "rtx_render_ppm", "rtx_scene_create_spheres", "rtx_scene_export",
 ]
 RTXHOST_SYMBOLS = [
     "rtxhost_build_scene", "rtxhost_scene_free", "rtxhost_scene_desc", "rtxhost_scene_camera",
-    "rtxhost_render_ppm", "rtxhost_ppm_encode", "rtxhost_last_error",
+    "rtxhost_render_ppm", "rtxhost_ppm_encode", "rtxhost_last_error", "rtxhost_scene_world_spheres",
 ]
 
 _lib = None
@@ -156,6 +156,12 @@ def load() -> ctypes.CDLL:
     L.rtx_render_ppm.argtypes = [c_void_p, POINTER(Camera), c_uint64, c_void_p, c_uint64, POINTER(c_uint64),
                                  POINTER(Stats)]
     L.rtx_render_ppm.restype = c_int
+    L.rtx_scene_create_spheres.argtypes = [POINTER(Sphere), c_uint32, POINTER(Material), c_uint32, POINTER(Texture),
+                                           c_uint32, POINTER(c_uint32), c_uint64, c_uint64, c_uint64,
+                                           POINTER(c_void_p), POINTER(c_double)]
+    L.rtx_scene_create_spheres.restype = c_int
+    L.rtx_scene_export.argtypes = [c_void_p, c_void_p, c_uint64]
+    L.rtx_scene_export.restype = c_uint64
     _lib = L
     return L
 
@@ -182,6 +188,8 @@ def load_host() -> ctypes.CDLL:
     H.rtxhost_ppm_encode.argtypes = [c_void_p, c_uint32, c_uint32, c_void_p, c_uint64]
     H.rtxhost_ppm_encode.restype = c_uint64
     H.rtxhost_last_error.restype = c_char_p
+    H.rtxhost_scene_world_spheres.argtypes = [c_void_p, POINTER(Sphere), c_uint64, POINTER(c_uint64), POINTER(c_uint64)]
+    H.rtxhost_scene_world_spheres.restype = ctypes.c_int64
     _host = H
     return H
 
@@ -222,6 +230,17 @@ class HostScene:
             raise RtxError(rc, load_host().rtxhost_last_error().decode())
         return cam
 
+    def world_spheres(self):
+        """(Sphere array in World.Add order, BVH draw position, seed): rtx_scene_create_spheres' inputs."""
+        H = load_host()
+        draw0, seed = c_uint64(), c_uint64()
+        n = H.rtxhost_scene_world_spheres(self._h, None, 0, None, None)
+        if n < 0:
+            raise RtxError(int(n), H.rtxhost_last_error().decode())
+        arr = (Sphere * max(int(n), 1))()
+        H.rtxhost_scene_world_spheres(self._h, arr, n, ctypes.byref(draw0), ctypes.byref(seed))
+        return arr, int(n), draw0.value, seed.value
+
     def close(self) -> None:
         if self._h:
             load_host().rtxhost_scene_free(self._h)
@@ -237,11 +256,37 @@ class HostScene:
 class DeviceScene:
     """rtx_scene_create: the tables uploaded once to the current HIP device."""
 
-    def __init__(self, desc_ptr):
+    def __init__(self, desc_ptr=None, handle=None):
         L = load()
+        self.build_ms = None
+        if handle is not None:
+            self._h = handle
+            return
         h = c_void_p()
         check(L.rtx_scene_create(desc_ptr, ctypes.byref(h)), "rtx_scene_create")
         self._h = h
+
+    @classmethod
+    def from_spheres(cls, host: "HostScene") -> "DeviceScene":
+        """rtx_scene_create_spheres: the BVH of host's World built on the GPU."""
+        L = load()
+        arr, n, draw0, seed = host.world_spheres()
+        d = host.desc.contents
+        h = c_void_p()
+        ms = c_double()
+        check(L.rtx_scene_create_spheres(arr, n, d.materials, d.n_materials, d.textures, d.n_textures, d.texels,
+                                         d.n_texels, seed, draw0, ctypes.byref(h), ctypes.byref(ms)),
+              "rtx_scene_create_spheres")
+        obj = cls(handle=h)
+        obj.build_ms = ms.value
+        return obj
+
+    def export(self) -> bytes:
+        L = load()
+        n = int(L.rtx_scene_export(self._h, None, 0))
+        buf = ctypes.create_string_buffer(n)
+        L.rtx_scene_export(self._h, buf, n)
+        return buf.raw
 
     @property
     def handle(self):
