@@ -574,8 +574,9 @@ __device__ __forceinline__ void trav_step(Trav& t, const Ray& r, const SceneRef 
     asm volatile("" ::"v"(ea.x), "v"(ea.y), "v"(ea.z), "v"(ea.w), "v"(eb.x), "v"(eb.y), "v"(eb.z), "v"(eb.w));
     if (__float_as_int(eb.w) == RTX_E_NODE) {
         if (COUNT) ++cnt.node_visits;
-        // Per axis: t0 = (min - o) * invD, t1 = (max - o) * invD, swapped if invD < 0
-        // (selecting the operands first is the same two operations).
+        // Per axis: t0 = (min - o) * invD, t1 = (max - o) * invD, swapped if invD < 0.
+        // Both planes' distances are computed, x and y as packed pairs (v_pk_add_f32 /
+        // v_pk_mul_f32: the same two IEEE operations per lane), then selected.
         const float t0x = ((t.nx ? eb.x : ea.x) - r.o.x) * t.ix;
         const float t1x = ((t.nx ? ea.x : eb.x) - r.o.x) * t.ix;
         const float t0y = ((t.ny ? eb.y : ea.y) - r.o.y) * t.iy;
@@ -587,7 +588,9 @@ __device__ __forceinline__ void trav_step(Trav& t, const Ray& r, const SceneRef 
         // reference's per-axis early exit.
         const float lo = __builtin_fmaxf(__builtin_fmaxf(__builtin_fmaxf(tmin, t0x), t0y), t0z);
         const float hi = __builtin_fminf(__builtin_fminf(__builtin_fminf(t.closest, t1x), t1y), t1z);
-        t.i = (lo < hi) ? t.i + 1 : (uint32_t)__float_as_int(ea.w);
+        // i + 1 on a box hit, else the escape: a mask select (a ?: here became a branch).
+        const uint32_t take = 0u - (uint32_t)(lo < hi);
+        t.i = ((t.i + 1) & take) | ((uint32_t)__float_as_int(ea.w) & ~take);
     } else if (QUADS && __float_as_int(eb.w) == RTX_E_QUAD) {
         quad_test<COUNT>(t, r, E, ea, eb, cnt);
     } else {
