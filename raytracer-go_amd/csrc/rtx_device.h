@@ -359,6 +359,7 @@ struct Params {
     // into scratch[(k - k0) * width * rows + pixel] (3 floats), `sub` samples per unit.
     float* scratch;
     uint32_t k0, kn, sub;
+    uint32_t item_waves;  // v3 waves per workgroup: 8 (one LDS scene copy each), or 4 for A/B
 };
 
 struct Ray {

@@ -310,9 +310,9 @@ __global__ __launch_bounds__(64 * WX * WY, MINW) void render_wave(Params p) {
 // Samples beyond the scratch budget run in chunks [k0, k0 + kn); the running sum of a
 // pixel is carried in the output between chunks.
 // ------------------------------------------------------------------------------------
-template <bool COUNT, bool USE_LDS, bool QUADS, bool NOISE>
-__global__ __launch_bounds__(256) void render_items(Params p) {
-    constexpr uint32_t WAVE_BLOCK = 256, STEPS = 3;
+template <bool COUNT, bool USE_LDS, bool QUADS, bool NOISE, int WAVES = 8>
+__global__ __launch_bounds__(64 * WAVES) void render_items(Params p) {
+    constexpr uint32_t WAVE_BLOCK = 64 * WAVES, STEPS = 3;
     extern __shared__ float4 lds_entries[];
     SceneRef E;
     if constexpr (USE_LDS) {
@@ -766,14 +766,16 @@ hipError_t launch_wave(const Params& p, uint32_t geom, bool use_lds, hipStream_t
 
 // v3: chunks of p.kn samples (the scratch holds one chunk), each rendered by a
 // resident-capacity grid of render_items and summed into p.out by reduce_samples.
-template <bool COUNT, bool QUADS, bool NOISE>
+template <bool COUNT, bool QUADS, bool NOISE, int WAVES = 8>
 hipError_t launch_items(Params p, bool use_lds, hipStream_t stream) {
     const size_t shmem = use_lds ? scene_lds_bytes(p) : 0;
-    const auto kern = use_lds ? render_items<COUNT, true, QUADS, NOISE> : render_items<COUNT, false, QUADS, NOISE>;
+    const auto kern = use_lds ? render_items<COUNT, true, QUADS, NOISE, WAVES>
+                              : render_items<COUNT, false, QUADS, NOISE, WAVES>;
+    constexpr int block = 64 * WAVES;
     int dev = 0, cus = 0, per_cu = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256, shmem);
+    if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, block, shmem);
     if (e != hipSuccess) return e;
     if (per_cu < 1) per_cu = 1;
     const uint32_t spp = p.cam.samples_per_pixel, chunk = p.kn;
@@ -784,10 +786,10 @@ hipError_t launch_items(Params p, bool use_lds, hipStream_t stream) {
         p.kn = spp - k0 < chunk ? spp - k0 : chunk;
         const uint64_t units = tiles * ((p.kn + p.sub - 1) / p.sub);
         uint64_t blocks = (uint64_t)per_cu * cus;
-        if (blocks > (units + 3) / 4) blocks = (units + 3) / 4;  // no wave starts without a unit
+        if (blocks > (units + WAVES - 1) / WAVES) blocks = (units + WAVES - 1) / WAVES;  // no wave starts idle
         e = hipMemsetAsync(p.tile_counter, 0, 2 * sizeof(uint32_t), stream);
         if (e != hipSuccess) return e;
-        hipLaunchKernelGGL(kern, dim3((uint32_t)blocks), dim3(256), shmem, stream, p);
+        hipLaunchKernelGGL(kern, dim3((uint32_t)blocks), dim3(block), shmem, stream, p);
         hipLaunchKernelGGL(reduce_samples, dim3((uint32_t)((npix + 255) / 256)), dim3(256), 0, stream, p,
                            (uint32_t)(k0 + p.kn >= spp));
         e = hipGetLastError();
@@ -808,6 +810,9 @@ template <bool COUNT>
 hipError_t launch_items_for(const Params& p, bool use_lds, hipStream_t stream) {
     if (p.has_noise) return p.n_quads ? launch_items<COUNT, true, true>(p, use_lds, stream)
                                       : launch_items<COUNT, false, true>(p, use_lds, stream);
+    if (p.item_waves == 4)  // A/B: 4 waves per LDS copy of the scene
+        return p.n_quads ? launch_items<COUNT, true, false, 4>(p, use_lds, stream)
+                         : launch_items<COUNT, false, false, 4>(p, use_lds, stream);
     return p.n_quads ? launch_items<COUNT, true, false>(p, use_lds, stream)
                      : launch_items<COUNT, false, false>(p, use_lds, stream);
 }
