@@ -310,8 +310,8 @@ __global__ __launch_bounds__(64 * WX * WY, MINW) void render_wave(Params p) {
 // Samples beyond the scratch budget run in chunks [k0, k0 + kn); the running sum of a
 // pixel is carried in the output between chunks.
 // ------------------------------------------------------------------------------------
-template <bool COUNT, bool USE_LDS, bool QUADS, bool NOISE, int WAVES = 8>
-__global__ __launch_bounds__(64 * WAVES) void render_items(Params p) {
+template <bool COUNT, bool USE_LDS, bool QUADS, bool NOISE, int WAVES = 8, int MINW = 0>
+__global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
     constexpr uint32_t WAVE_BLOCK = 64 * WAVES, STEPS = 3;
     extern __shared__ float4 lds_entries[];
     SceneRef E;
@@ -766,11 +766,11 @@ hipError_t launch_wave(const Params& p, uint32_t geom, bool use_lds, hipStream_t
 
 // v3: chunks of p.kn samples (the scratch holds one chunk), each rendered by a
 // resident-capacity grid of render_items and summed into p.out by reduce_samples.
-template <bool COUNT, bool QUADS, bool NOISE, int WAVES = 8>
+template <bool COUNT, bool QUADS, bool NOISE, int WAVES = 8, int MINW = 0>
 hipError_t launch_items(Params p, bool use_lds, hipStream_t stream) {
     const size_t shmem = use_lds ? scene_lds_bytes(p) : 0;
-    const auto kern = use_lds ? render_items<COUNT, true, QUADS, NOISE, WAVES>
-                              : render_items<COUNT, false, QUADS, NOISE, WAVES>;
+    const auto kern = use_lds ? render_items<COUNT, true, QUADS, NOISE, WAVES, MINW>
+                              : render_items<COUNT, false, QUADS, NOISE, WAVES, MINW>;
     constexpr int block = 64 * WAVES;
     int dev = 0, cus = 0, per_cu = 0;
     hipError_t e = hipGetDevice(&dev);
