@@ -257,11 +257,12 @@ uint32_t env_knob(const char* name, long dflt, long lo, long hi) {
     return (uint32_t)(x < lo ? lo : (x > hi ? hi : x));
 }
 
-// Tuning knob of the v1 kernel (lanes waiting before a wave shades); RTX_SHADE_THRESH.
+// Lanes of a wave that wait before it shades (v1-v3); RTX_SHADE_THRESH.  52 measured
+// best for v3 at the headline config (48 for v1).
 uint32_t shade_thresh() {
     static const uint32_t v = [] {
         const char* e = std::getenv("RTX_SHADE_THRESH");
-        const long x = e ? std::strtol(e, nullptr, 10) : 48;
+        const long x = e ? std::strtol(e, nullptr, 10) : 52;
         return (uint32_t)(x < 1 ? 1 : (x > 64 ? 64 : x));
     }();
     return v;
