@@ -201,8 +201,8 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
                 "alg_bytes_per_launch": launch_bytes,
-                "note": "algorithmic bytes (SURVEY §8d) of rank 0's launch / its HIP-event kernel time; the "
-                        "35 KB scene is cache-resident, so real HBM traffic is far lower",
+                "note": "algorithmic bytes (SURVEY §8d) of rank 0's launch / its HIP-event time; the 32 KB "
+                        "scene is LDS-resident, so real HBM traffic (PMC: the v3 sample scratch) is ~300x lower",
             },
         }
         if world == 1 and not args.no_cpu:
