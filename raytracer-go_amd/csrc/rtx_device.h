@@ -604,7 +604,9 @@ __device__ __forceinline__ void trav_step(Trav& t, const Ray& r, const SceneRef 
             const float sq = __builtin_sqrtf(disc);                            // :108
             float tt = (-hb - sq) / t.a;                                       // :110
             bool ok = tmin < tt && tt < t.closest;
-            if (!ok) {
+            // The second root (:112) only when the first is not beyond tmin (or NaN): a
+            // first root at or past closest makes the second, (-hb + sq) / a >= it, fail too.
+            if (!(tmin < tt)) {
                 tt = (-hb + sq) / t.a;                                         // :112
                 ok = tmin < tt && tt < t.closest;
             }

@@ -287,3 +287,17 @@ def test_v3_shards(torch_cuda, spheres, dev_spheres, world):
                              counters=False, flags=V1)
         got[rank::world] = part
     assert np.array_equal(full, got)
+
+
+@pytest.mark.parametrize("scene,width,spp", [("random_spheres", 1920, 16), ("cornell_box", 600, 24),
+                                             ("simple_light_demo", 400, 40)])
+def test_full_frame_bitwise(torch_cuda, built, scene, width, spp):
+    """Whole frames at the configs' sizes (reduced spp so the oracle takes seconds):
+    every pixel bit-identical to the oracle's iterative order, within 1e-4 of the
+    reference order, and identical work counters."""
+    s = rtx.HostScene(scene, 1)
+    cam = s.camera(width=width, spp=spp)
+    dev = rtx.DeviceScene(s.desc)
+    reg = rtx.Region(0, 0, cam.image_width, cam.image_height, 0, 1)
+    gpu, st = gpu_region(torch_cuda, dev, cam, 23, reg)
+    check_parity(gpu, s.desc, cam, 23, reg, st)
