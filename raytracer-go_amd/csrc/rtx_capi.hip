@@ -188,15 +188,19 @@ int ensure_device(rtx_scene* s, int device, DeviceCopy** out) {
     DeviceCopy c;
     c.device = device;
     HIP_TRY(hipSetDevice(device));
-    HIP_TRY(hipMalloc(&c.entries, s->entries.size() * sizeof(rtx_entry) + s->quadtab.size() * sizeof(float)));
-    {  // device layout: all 'a' halves, then all 'b' halves (rtxd::SceneRef)
-        const size_t n = s->entries.size();
-        std::vector<float> soa(n * 8 + s->quadtab.size());
+    HIP_TRY(hipMalloc(&c.entries, (s->entries.size() + 1) * sizeof(rtx_entry) + s->quadtab.size() * sizeof(float)));
+    {  // device layout: all 'a' halves, then all 'b' halves (rtxd::SceneRef), each ending
+       // with the sentinel entry (rtx_layout.h)
+        const size_t n = s->entries.size(), m = n + 1;
+        std::vector<float> soa(m * 8 + s->quadtab.size(), 0.0f);
         for (size_t i = 0; i < n; ++i) {
             std::memcpy(&soa[4 * i], s->entries[i].a, 16);
-            std::memcpy(&soa[4 * (n + i)], s->entries[i].b, 16);
+            std::memcpy(&soa[4 * (m + i)], s->entries[i].b, 16);
         }
-        if (!s->quadtab.empty()) std::memcpy(&soa[8 * n], s->quadtab.data(), s->quadtab.size() * sizeof(float));
+        const int32_t sent_a = (int32_t)n, sent_b = RTX_E_SENTINEL;
+        std::memcpy(&soa[4 * n + 3], &sent_a, 4);
+        std::memcpy(&soa[4 * (m + n) + 3], &sent_b, 4);
+        if (!s->quadtab.empty()) std::memcpy(&soa[8 * m], s->quadtab.data(), s->quadtab.size() * sizeof(float));
         HIP_TRY(hipMemcpy(c.entries, soa.data(), soa.size() * sizeof(float), hipMemcpyHostToDevice));
     }
     HIP_TRY(hipMalloc(&c.materials, std::max<size_t>(1, s->materials.size()) * sizeof(rtx_material)));

@@ -330,14 +330,19 @@ struct SceneRef {
     const float4* __restrict__ q;  // quad table, 4 float4 per quad (rtx_layout.h)
 };
 __device__ __forceinline__ SceneRef scene_ref(const float4* base, uint32_t n_entries) {
-    return SceneRef{base, base + n_entries, base + 2 * n_entries};
+    const uint32_t m = n_entries + 1;  // + the sentinel
+    return SceneRef{base, base + m, base + 2 * m};
+}
+// float4s of a scene's device table: both halves with their sentinels, then the quads.
+__host__ __device__ __forceinline__ uint32_t scene_float4s(uint32_t n_entries, uint32_t n_quads) {
+    return 2 * (n_entries + 1) + 4 * n_quads;
 }
 
 // ---------------------------------------------------------------------------------
 // Kernel parameters
 // ---------------------------------------------------------------------------------
 struct Params {
-    const float4* entries;   // n_entries 'a' halves, n_entries 'b' halves, 4 * n_quads (SceneRef)
+    const float4* entries;   // n_entries + 1 'a' halves, as many 'b', 4 * n_quads (SceneRef)
     uint32_t n_entries;
     uint32_t n_quads;
     uint32_t n_materials;
@@ -564,7 +569,9 @@ __device__ __forceinline__ void quad_test(Trav& t, const Ray& r, const SceneRef 
 }
 
 // QUADS: the scene holds quads (a third entry kind); false compiles the sphere-only step.
-template <bool COUNT, bool QUADS = false>
+// SENT: the step may land on the sentinel (rtx_layout.h), which it leaves unchanged
+// (spheres are then told apart by their material index, b.w >= 0).
+template <bool COUNT, bool QUADS = false, bool SENT = false>
 __device__ __forceinline__ void trav_step(Trav& t, const Ray& r, const SceneRef E, Counters& cnt) {
     const float tmin = 0.001f;  // ray.go:37
     const float4 ea = E.a[t.i];
@@ -594,7 +601,7 @@ __device__ __forceinline__ void trav_step(Trav& t, const Ray& r, const SceneRef 
         t.i = ((t.i + 1) & take) | ((uint32_t)__float_as_int(ea.w) & ~take);
     } else if (QUADS && __float_as_int(eb.w) == RTX_E_QUAD) {
         quad_test<COUNT>(t, r, E, ea, eb, cnt);
-    } else {
+    } else if (!SENT || __float_as_int(eb.w) >= 0) {
         if (COUNT) ++cnt.prim_tests;
         const float ox = r.o.x - ea.x, oy = r.o.y - ea.y, oz = r.o.z - ea.z;  // :97
         const float hb = r.d.x * ox + r.d.y * oy + r.d.z * oz;                 // :99

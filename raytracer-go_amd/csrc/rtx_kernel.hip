@@ -100,13 +100,12 @@ __device__ __forceinline__ void traverse_phase(uint32_t& mode, Trav& t, const Ra
                                                uint64_t& wave_iters, uint64_t& lane_steps, uint64_t& shade_phases,
                                                uint64_t& shade_lanes, uint64_t& idle_lanes) {
     for (;;) {
+        // Every lane steps: one that is not traversing (or finishes early) waits on the
+        // sentinel, t.i = n_entries, where a step changes nothing — cheaper than masking
+        // the wave per step.
 #pragma unroll
-        for (int s = 0; s < STEPS; ++s) {
-            if (mode == 0) {
-                trav_step<COUNT, QUADS>(t, r, E, cnt);
-                if (t.i >= n_entries) mode = 1;
-            }
-        }
+        for (int s = 0; s < STEPS; ++s) trav_step<COUNT, QUADS, true>(t, r, E, cnt);
+        if (mode == 0 && t.i >= n_entries) mode = 1;
         const uint64_t trav = __ballot(mode == 0);
         const uint64_t pend = __ballot(mode == 1 || mode == 2);
         if (COUNT) {
@@ -149,7 +148,7 @@ __global__ __launch_bounds__(64 * WX * WY, MINW) void render_wave(Params p) {
     extern __shared__ float4 lds_entries[];
     SceneRef E;
     if constexpr (USE_LDS) {
-        const uint32_t n4 = 2 * p.n_entries + 4 * p.n_quads;  // entries, then the quad table
+        const uint32_t n4 = scene_float4s(p.n_entries, p.n_quads);  // entries, then the quad table
         for (uint32_t t = threadIdx.x; t < n4; t += WAVE_BLOCK) lds_entries[t] = p.entries[t];
         __syncthreads();
         E = scene_ref(lds_entries, p.n_entries);
@@ -178,6 +177,7 @@ __global__ __launch_bounds__(64 * WX * WY, MINW) void render_wave(Params p) {
     PathRng rng{(uint32_t)p.seed, (uint32_t)(p.seed >> 32),
                 (p.y0 + p.rank + lr * p.world) * c.image_width + p.x0 + lx, 0};
     Trav t{};
+    t.i = p.n_entries;  // on the sentinel until its first ray
     Counters cnt{0, 0, 0, 0, 0, 0};
     uint64_t wave_iters = 0, lane_steps = 0, shade_phases = 0, shade_lanes = 0;
     uint64_t trav_cycles = 0, shade_cycles = 0, clk = 0, idle_lanes = 0;  // COUNT only
@@ -316,7 +316,7 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
     extern __shared__ float4 lds_entries[];
     SceneRef E;
     if constexpr (USE_LDS) {
-        const uint32_t n4 = 2 * p.n_entries + 4 * p.n_quads;
+        const uint32_t n4 = scene_float4s(p.n_entries, p.n_quads);
         for (uint32_t t = threadIdx.x; t < n4; t += WAVE_BLOCK) lds_entries[t] = p.entries[t];
         __syncthreads();
         E = scene_ref(lds_entries, p.n_entries);
@@ -344,6 +344,7 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
     Ray r{v3(0, 0, 0), v3(0, 0, 0)};
     PathRng rng{(uint32_t)p.seed, (uint32_t)(p.seed >> 32), 0u, 0u};
     Trav t{};
+    t.i = p.n_entries;  // on the sentinel until its first ray
     Counters cnt{0, 0, 0, 0, 0, 0};
     uint64_t wave_iters = 0, lane_steps = 0, shade_phases = 0, shade_lanes = 0;
     uint64_t trav_cycles = 0, shade_cycles = 0, clk = 0, idle_lanes = 0;  // COUNT only
@@ -533,7 +534,7 @@ __global__ __launch_bounds__(POOL_BLOCK) void render_pool(Params p) {
     SceneRef E;
     if constexpr (USE_LDS) {
         float4* scene = lds_dyn + (POOL_WAVES * sizeof(Pool)) / 16;
-        const uint32_t n4 = 2 * p.n_entries;
+        const uint32_t n4 = scene_float4s(p.n_entries, 0);
         for (uint32_t t = threadIdx.x; t < n4; t += POOL_BLOCK) scene[t] = p.entries[t];
         E = scene_ref(scene, p.n_entries);
     } else {
@@ -578,6 +579,7 @@ __global__ __launch_bounds__(POOL_BLOCK) void render_pool(Params p) {
     Ray r{v3(0, 0, 0), v3(0, 0, 0)};
     PathRng rng{(uint32_t)p.seed, (uint32_t)(p.seed >> 32), 0, 0};
     Trav t{};
+    t.i = p.n_entries;  // on the sentinel until its first ray
     Counters cnt{0, 0, 0, 0, 0, 0};
     uint64_t samples = 0;
     uint64_t wave_iters = 0, lane_steps = 0, shade_phases = 0, shade_lanes = 0;
@@ -694,7 +696,7 @@ __global__ __launch_bounds__(POOL_BLOCK) void render_pool(Params p) {
 constexpr uint32_t LDS_MAX_BYTES = 64 * 1024;
 
 // LDS bytes of the scene copy: entries and the quad table.
-inline size_t scene_lds_bytes(const Params& p) { return (size_t)p.n_entries * 32 + (size_t)p.n_quads * 64; }
+inline size_t scene_lds_bytes(const Params& p) { return (size_t)scene_float4s(p.n_entries, p.n_quads) * 16; }
 
 template <bool COUNT, int NCH>
 hipError_t launch_pool(const Params& p, bool use_lds, hipStream_t stream) {

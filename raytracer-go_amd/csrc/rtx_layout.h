@@ -27,12 +27,16 @@
 // hittables.go:149-165, computed on the host.
 // radius*radius is the float32 product hittables.go:100 computes, precomputed.
 // On the device the halves live in two arrays (all a, then all b: rtxd::SceneRef), so
-// a wave's gathers spread over every LDS bank group.
+// a wave's gathers spread over every LDS bank group.  Each array ends with one extra
+// entry, the sentinel at index n (b.w = RTX_E_SENTINEL): every walk ends there, and a
+// step on it changes nothing, so lanes that are not traversing can take the same steps
+// as those that are (rtxd::traverse_phase) instead of being masked off one step at a time.
 #pragma once
 #include <stdint.h>
 
 #define RTX_E_NODE (-1)
 #define RTX_E_QUAD (-2)
+#define RTX_E_SENTINEL (-3)
 
 struct rtx_entry {
     float a[4];
