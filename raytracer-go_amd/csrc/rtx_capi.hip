@@ -196,8 +196,15 @@ int ensure_device(rtx_scene* s, int device, DeviceCopy** out) {
         for (size_t i = 0; i < n; ++i) {
             std::memcpy(&soa[4 * i], s->entries[i].a, 16);
             std::memcpy(&soa[4 * (m + i)], s->entries[i].b, 16);
+            int32_t tag, esc;
+            std::memcpy(&tag, &s->entries[i].b[3], 4);
+            if (tag == RTX_E_NODE) {  // escapes as walk positions (rtxd::Trav::i: 16 * index)
+                std::memcpy(&esc, &s->entries[i].a[3], 4);
+                esc *= 16;
+                std::memcpy(&soa[4 * i + 3], &esc, 4);
+            }
         }
-        const int32_t sent_a = (int32_t)n, sent_b = RTX_E_SENTINEL;
+        const int32_t sent_a = (int32_t)(16 * n), sent_b = RTX_E_SENTINEL;
         std::memcpy(&soa[4 * n + 3], &sent_a, 4);
         std::memcpy(&soa[4 * (m + n) + 3], &sent_b, 4);
         if (!s->quadtab.empty()) std::memcpy(&soa[8 * m], s->quadtab.data(), s->quadtab.size() * sizeof(float));

@@ -333,6 +333,17 @@ __device__ __forceinline__ SceneRef scene_ref(const float4* base, uint32_t n_ent
     const uint32_t m = n_entries + 1;  // + the sentinel
     return SceneRef{base, base + m, base + 2 * m};
 }
+// v3's LDS layout: the 'a' halves from LDS byte 0, the 'b' halves from byte LDS_B, the
+// quad table after them.  A walk position is then the LDS address of its 'a' half and
+// both halves load from one register (ds_read_b128 offset:0 / offset:LDS_B): no address
+// arithmetic per step.
+constexpr uint32_t LDS_B = 32768;
+__host__ __device__ __forceinline__ uint32_t lds_fixed_bytes(uint32_t n_entries, uint32_t n_quads) {
+    return LDS_B + (n_entries + 1) * 16 + n_quads * 64;
+}
+__device__ __forceinline__ SceneRef scene_ref_fixed(const float4* lds, uint32_t n_entries) {
+    return SceneRef{lds, lds + LDS_B / 16, lds + LDS_B / 16 + n_entries + 1};
+}
 // float4s of a scene's device table: both halves with their sentinels, then the quads.
 __host__ __device__ __forceinline__ uint32_t scene_float4s(uint32_t n_entries, uint32_t n_quads) {
     return 2 * (n_entries + 1) + 4 * n_quads;
@@ -523,7 +534,7 @@ __device__ __forceinline__ Scatter coop_scatter(const Params& p, const SceneRef 
 // hittables.go:96-116).  The sequence of steps is the reference recursion's, with
 // running bound `closest` = the closest hit so far (bvh.go:227-232).
 struct Trav {
-    uint32_t i;
+    uint32_t i;  // walk position: the byte offset of the current entry's half, 16 * index
     int32_t hit;
     float closest, ix, iy, iz, a;
     bool nx, ny, nz;
@@ -543,6 +554,9 @@ __device__ __forceinline__ void trav_begin(Trav& t, const Ray& r) {
     t.i = 0;
 }
 
+// Entry index of a walk position (a byte offset, 16 per entry: Trav::i).
+__device__ __forceinline__ int32_t entry_of(uint32_t pos) { return (int32_t)(pos >> 4); }
+
 // (Quad).Hit, hittables.go:167-194, of quad entry t.i = (ea, eb) against (tmin, closest).
 template <bool COUNT>
 __device__ __forceinline__ void quad_test(Trav& t, const Ray& r, const SceneRef E, const float4 ea, const float4 eb,
@@ -561,25 +575,33 @@ __device__ __forceinline__ void quad_test(Trav& t, const Ray& r, const SceneRef 
             const float beta = dot(w, cross(v3(q1.x, q1.y, q1.z), php));            // :183
             if (!(alpha < 0.0f || 1.0f < alpha || beta < 0.0f || 1.0f < beta)) {   // :185, :193
                 t.closest = tt;
-                t.hit = (int32_t)t.i;
+                t.hit = entry_of(t.i);
             }
         }
     }
-    ++t.i;
+    t.i += 16;
 }
 
 // QUADS: the scene holds quads (a third entry kind); false compiles the sphere-only step.
 // SENT: the step may land on the sentinel (rtx_layout.h), which it leaves unchanged
 // (spheres are then told apart by their material index, b.w >= 0).
-template <bool COUNT, bool QUADS = false, bool SENT = false>
+// FIXED: E is v3's LDS layout at LDS address 0 (scene_ref_fixed).
+template <bool COUNT, bool QUADS = false, bool SENT = false, bool FIXED = false>
 __device__ __forceinline__ void trav_step(Trav& t, const Ray& r, const SceneRef E, Counters& cnt) {
     const float tmin = 0.001f;  // ray.go:37
-    const float4 ea = E.a[t.i];
-    const float4 eb = E.b[t.i];
-    // Both halves are consumed here, so the whole entry arrives in one round trip (two
-    // ds_read_b128); otherwise the compiler sinks the node-only dwords into the box branch
-    // behind a second, dependent LDS read.
-    asm volatile("" ::"v"(ea.x), "v"(ea.y), "v"(ea.z), "v"(ea.w), "v"(eb.x), "v"(eb.y), "v"(eb.z), "v"(eb.w));
+    float4 ea, eb;
+    if constexpr (FIXED) {
+        asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %2 offset:%3\n\ts_waitcnt lgkmcnt(0)"
+                     : "=&v"(ea), "=&v"(eb)
+                     : "v"(t.i), "i"(LDS_B));
+    } else {
+        ea = *reinterpret_cast<const float4*>(reinterpret_cast<const char*>(E.a) + t.i);
+        eb = *reinterpret_cast<const float4*>(reinterpret_cast<const char*>(E.b) + t.i);
+        // Both halves are consumed here, so the whole entry arrives in one round trip (two
+        // 128-bit loads); otherwise the compiler sinks the node-only dwords into the box
+        // branch behind a second, dependent read.
+        asm volatile("" ::"v"(ea.x), "v"(ea.y), "v"(ea.z), "v"(ea.w), "v"(eb.x), "v"(eb.y), "v"(eb.z), "v"(eb.w));
+    }
     if (__float_as_int(eb.w) == RTX_E_NODE) {
         if (COUNT) ++cnt.node_visits;
         // Per axis: t0 = (min - o) * invD, t1 = (max - o) * invD, swapped if invD < 0.
@@ -596,9 +618,10 @@ __device__ __forceinline__ void trav_step(Trav& t, const Ray& r, const SceneRef 
         // reference's per-axis early exit.
         const float lo = __builtin_fmaxf(__builtin_fmaxf(__builtin_fmaxf(tmin, t0x), t0y), t0z);
         const float hi = __builtin_fminf(__builtin_fminf(__builtin_fminf(t.closest, t1x), t1y), t1z);
-        // i + 1 on a box hit, else the escape: a mask select (a ?: here became a branch).
+        // the next entry on a box hit, else the escape (stored as a walk position): a mask
+        // select (a ?: here became a branch).
         const uint32_t take = 0u - (uint32_t)(lo < hi);
-        t.i = ((t.i + 1) & take) | ((uint32_t)__float_as_int(ea.w) & ~take);
+        t.i = ((t.i + 16) & take) | ((uint32_t)__float_as_int(ea.w) & ~take);
     } else if (QUADS && __float_as_int(eb.w) == RTX_E_QUAD) {
         quad_test<COUNT>(t, r, E, ea, eb, cnt);
     } else if (!SENT || __float_as_int(eb.w) >= 0) {
@@ -619,10 +642,10 @@ __device__ __forceinline__ void trav_step(Trav& t, const Ray& r, const SceneRef 
             }
             if (ok) {
                 t.closest = tt;
-                t.hit = (int32_t)t.i;
+                t.hit = entry_of(t.i);
             }
         }
-        ++t.i;
+        t.i += 16;
     }
 }
 

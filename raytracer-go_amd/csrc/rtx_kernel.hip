@@ -70,7 +70,7 @@ __global__ __launch_bounds__(BLOCK) void render_pixels(Params p) {
             if (COUNT) ++cnt.segments;
             Trav t;
             trav_begin(t, r);
-            while (t.i < p.n_entries) trav_step<COUNT, QUADS>(t, r, E, cnt);
+            while (t.i < 16 * p.n_entries) trav_step<COUNT, QUADS>(t, r, E, cnt);
             if (shade<COUNT, QUADS>(p, E, t, seg, r, thr, acc, rng, cnt, col)) break;
         }
         sum = add(sum, col);  // camera.go:259 (col = 0 when the depth ran out)
@@ -94,7 +94,7 @@ __global__ __launch_bounds__(BLOCK) void render_pixels(Params p) {
 // STEPS > 1 takes up to STEPS entries per lane between two wave votes.  (A branch-free
 // step that evaluates the box and the sphere test on every lane measured 8 % slower:
 // most waves hold only box entries at a step, and the branch skips the sphere test.)
-template <bool COUNT, int STEPS = 1, bool QUADS = false>
+template <bool COUNT, int STEPS = 1, bool QUADS = false, bool FIXED = false>
 __device__ __forceinline__ void traverse_phase(uint32_t& mode, Trav& t, const Ray& r, const SceneRef E,
                                                uint32_t n_entries, uint32_t thresh, Counters& cnt,
                                                uint64_t& wave_iters, uint64_t& lane_steps, uint64_t& shade_phases,
@@ -104,8 +104,8 @@ __device__ __forceinline__ void traverse_phase(uint32_t& mode, Trav& t, const Ra
         // sentinel, t.i = n_entries, where a step changes nothing — cheaper than masking
         // the wave per step.
 #pragma unroll
-        for (int s = 0; s < STEPS; ++s) trav_step<COUNT, QUADS, true>(t, r, E, cnt);
-        if (mode == 0 && t.i >= n_entries) mode = 1;
+        for (int s = 0; s < STEPS; ++s) trav_step<COUNT, QUADS, true, FIXED>(t, r, E, cnt);
+        if (mode == 0 && t.i >= 16 * n_entries) mode = 1;
         const uint64_t trav = __ballot(mode == 0);
         const uint64_t pend = __ballot(mode == 1 || mode == 2);
         if (COUNT) {
@@ -177,7 +177,7 @@ __global__ __launch_bounds__(64 * WX * WY, MINW) void render_wave(Params p) {
     PathRng rng{(uint32_t)p.seed, (uint32_t)(p.seed >> 32),
                 (p.y0 + p.rank + lr * p.world) * c.image_width + p.x0 + lx, 0};
     Trav t{};
-    t.i = p.n_entries;  // on the sentinel until its first ray
+    t.i = 16 * p.n_entries;  // on the sentinel until its first ray
     Counters cnt{0, 0, 0, 0, 0, 0};
     uint64_t wave_iters = 0, lane_steps = 0, shade_phases = 0, shade_lanes = 0;
     uint64_t trav_cycles = 0, shade_cycles = 0, clk = 0, idle_lanes = 0;  // COUNT only
@@ -316,10 +316,16 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
     extern __shared__ float4 lds_entries[];
     SceneRef E;
     if constexpr (USE_LDS) {
-        const uint32_t n4 = scene_float4s(p.n_entries, p.n_quads);
-        for (uint32_t t = threadIdx.x; t < n4; t += WAVE_BLOCK) lds_entries[t] = p.entries[t];
+        // scene_ref_fixed: the walk addresses LDS directly, so the copy must start at 0
+        if ((uint32_t)(uintptr_t)(__attribute__((address_space(3))) float4*)lds_entries != 0u) __builtin_trap();
+        const uint32_t m = p.n_entries + 1, nq4 = 4 * p.n_quads;
+        for (uint32_t t = threadIdx.x; t < m; t += WAVE_BLOCK) {
+            lds_entries[t] = p.entries[t];
+            lds_entries[LDS_B / 16 + t] = p.entries[m + t];
+        }
+        for (uint32_t t = threadIdx.x; t < nq4; t += WAVE_BLOCK) lds_entries[LDS_B / 16 + m + t] = p.entries[2 * m + t];
         __syncthreads();
-        E = scene_ref(lds_entries, p.n_entries);
+        E = scene_ref_fixed(lds_entries, p.n_entries);
     } else {
         E = scene_ref(p.entries, p.n_entries);
     }
@@ -344,7 +350,7 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
     Ray r{v3(0, 0, 0), v3(0, 0, 0)};
     PathRng rng{(uint32_t)p.seed, (uint32_t)(p.seed >> 32), 0u, 0u};
     Trav t{};
-    t.i = p.n_entries;  // on the sentinel until its first ray
+    t.i = 16 * p.n_entries;  // on the sentinel until its first ray
     Counters cnt{0, 0, 0, 0, 0, 0};
     uint64_t wave_iters = 0, lane_steps = 0, shade_phases = 0, shade_lanes = 0;
     uint64_t trav_cycles = 0, shade_cycles = 0, clk = 0, idle_lanes = 0;  // COUNT only
@@ -359,7 +365,7 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
 
     for (;;) {
         if (COUNT) clk = __builtin_amdgcn_s_memtime();
-        traverse_phase<COUNT, STEPS, QUADS>(mode, t, r, E, n_entries, thresh, cnt, wave_iters, lane_steps,
+        traverse_phase<COUNT, STEPS, QUADS, USE_LDS>(mode, t, r, E, n_entries, thresh, cnt, wave_iters, lane_steps,
                                             shade_phases, shade_lanes, idle_lanes);
         if (COUNT) {
             const uint64_t now = __builtin_amdgcn_s_memtime();
@@ -579,7 +585,7 @@ __global__ __launch_bounds__(POOL_BLOCK) void render_pool(Params p) {
     Ray r{v3(0, 0, 0), v3(0, 0, 0)};
     PathRng rng{(uint32_t)p.seed, (uint32_t)(p.seed >> 32), 0, 0};
     Trav t{};
-    t.i = p.n_entries;  // on the sentinel until its first ray
+    t.i = 16 * p.n_entries;  // on the sentinel until its first ray
     Counters cnt{0, 0, 0, 0, 0, 0};
     uint64_t samples = 0;
     uint64_t wave_iters = 0, lane_steps = 0, shade_phases = 0, shade_lanes = 0;
@@ -770,7 +776,7 @@ hipError_t launch_wave(const Params& p, uint32_t geom, bool use_lds, hipStream_t
 // resident-capacity grid of render_items and summed into p.out by reduce_samples.
 template <bool COUNT, bool QUADS, bool NOISE, int WAVES = 8, int MINW = 0>
 hipError_t launch_items(Params p, bool use_lds, hipStream_t stream) {
-    const size_t shmem = use_lds ? scene_lds_bytes(p) : 0;
+    const size_t shmem = use_lds ? lds_fixed_bytes(p.n_entries, p.n_quads) : 0;
     const auto kern = use_lds ? render_items<COUNT, true, QUADS, NOISE, WAVES, MINW>
                               : render_items<COUNT, false, QUADS, NOISE, WAVES, MINW>;
     constexpr int block = 64 * WAVES;
@@ -815,8 +821,9 @@ hipError_t launch_items_for(const Params& p, bool use_lds, hipStream_t stream) {
     if (p.item_waves == 4)  // A/B: 4 waves per LDS copy of the scene
         return p.n_quads ? launch_items<COUNT, true, false, 4>(p, use_lds, stream)
                          : launch_items<COUNT, false, false, 4>(p, use_lds, stream);
-    return p.n_quads ? launch_items<COUNT, true, false>(p, use_lds, stream)
-                     : launch_items<COUNT, false, false>(p, use_lds, stream);
+    // 6 waves per SIMD: at most 80 VGPRs (the allocation granule is 8)
+    return p.n_quads ? launch_items<COUNT, true, false, 8, COUNT ? 0 : 6>(p, use_lds, stream)
+                     : launch_items<COUNT, false, false, 8, COUNT ? 0 : 6>(p, use_lds, stream);
 }
 
 hipError_t launch_render(const Params& p, uint32_t flags, hipStream_t stream) {
@@ -826,6 +833,8 @@ hipError_t launch_render(const Params& p, uint32_t flags, hipStream_t stream) {
     const bool use_lds = !(flags & RTX_FLAG_NO_LDS) && scene_lds_bytes(p) <= LDS_MAX_BYTES;
     if (uses_items(p, flags)) {
         if (!p.scratch) return hipErrorInvalidValue;  // the caller sizes the v3 scratch
+        const bool use_lds = !(flags & RTX_FLAG_NO_LDS) && (p.n_entries + 1) * 16 <= LDS_B &&
+                             lds_fixed_bytes(p.n_entries, p.n_quads) <= LDS_MAX_BYTES;
         return count ? launch_items_for<true>(p, use_lds, stream) : launch_items_for<false>(p, use_lds, stream);
     }
     if (flags & RTX_FLAG_KERNEL_V0) {
