@@ -617,7 +617,11 @@ __device__ __forceinline__ void trav_step(Trav& t, const Ray& r, const SceneRef 
         // bound only shrinks, so one min < max test after all three axes equals the
         // reference's per-axis early exit.
         const float lo = __builtin_fmaxf(__builtin_fmaxf(__builtin_fmaxf(tmin, t0x), t0y), t0z);
-        const float hi = __builtin_fminf(__builtin_fminf(__builtin_fminf(t.closest, t1x), t1y), t1z);
+        // hi = fminf(fminf(fminf(closest, t1x), t1y), t1z) as v_min3 + v_min: the builtin
+        // would first canonicalize `closest` (one more VALU per box).  Same IEEE-mode
+        // result: the operands are arithmetic results or +inf, never signalling NaNs.
+        float hi;
+        asm("v_min3_f32 %0, %1, %2, %3\n\tv_min_f32 %0, %0, %4" : "=&v"(hi) : "v"(t.closest), "v"(t1x), "v"(t1y), "v"(t1z));
         // the next entry on a box hit, else the escape (stored as a walk position): a mask
         // select (a ?: here became a branch).
         const uint32_t take = 0u - (uint32_t)(lo < hi);
