@@ -605,8 +605,8 @@ __device__ __forceinline__ void trav_step(Trav& t, const Ray& r, const SceneRef 
     if (__float_as_int(eb.w) == RTX_E_NODE) {
         if (COUNT) ++cnt.node_visits;
         // Per axis: t0 = (min - o) * invD, t1 = (max - o) * invD, swapped if invD < 0.
-        // Both planes' distances are computed, x and y as packed pairs (v_pk_add_f32 /
-        // v_pk_mul_f32: the same two IEEE operations per lane), then selected.
+        // (Scalar FP32 throughout: a v_pk_mul_f32 / v_pk_add_f32 issues at a quarter of
+        // v_mul_f32's rate on gfx950, scripts/micro/pk_rate.hip, so packing loses 2x.)
         const float t0x = ((t.nx ? eb.x : ea.x) - r.o.x) * t.ix;
         const float t1x = ((t.nx ? ea.x : eb.x) - r.o.x) * t.ix;
         const float t0y = ((t.ny ? eb.y : ea.y) - r.o.y) * t.iy;
