@@ -12,6 +12,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <limits>
 #include <map>
 #include <mutex>
 #include <string>
@@ -196,17 +197,28 @@ int ensure_device(rtx_scene* s, int device, DeviceCopy** out) {
         for (size_t i = 0; i < n; ++i) {
             std::memcpy(&soa[4 * i], s->entries[i].a, 16);
             std::memcpy(&soa[4 * (m + i)], s->entries[i].b, 16);
-            int32_t tag, esc;
+            int32_t tag, esc;  // the device recoding, rtx_layout.h
             std::memcpy(&tag, &s->entries[i].b[3], 4);
-            if (tag == RTX_E_NODE) {  // escapes as walk positions (rtxd::Trav::i: 16 * index)
+            if (tag == RTX_E_NODE) {
                 std::memcpy(&esc, &s->entries[i].a[3], 4);
                 esc *= 16;
+                const int32_t next = (int32_t)(16 * (i + 1));
                 std::memcpy(&soa[4 * i + 3], &esc, 4);
+                std::memcpy(&soa[4 * (m + i) + 3], &next, 4);
+            } else if (tag >= 0) {
+                const int32_t sph = RTX_DEV_SPHERE(tag);
+                std::memcpy(&soa[4 * (m + i) + 3], &sph, 4);
             }
         }
-        const int32_t sent_a = (int32_t)(16 * n), sent_b = RTX_E_SENTINEL;
-        std::memcpy(&soa[4 * n + 3], &sent_a, 4);
-        std::memcpy(&soa[4 * (m + n) + 3], &sent_b, 4);
+        // the sentinel: box min +inf, max -inf, escape = next = its own position
+        const float inf = std::numeric_limits<float>::infinity();
+        const int32_t self = (int32_t)(16 * n);
+        for (int k = 0; k < 3; ++k) {
+            soa[4 * n + k] = inf;
+            soa[4 * (m + n) + k] = -inf;
+        }
+        std::memcpy(&soa[4 * n + 3], &self, 4);
+        std::memcpy(&soa[4 * (m + n) + 3], &self, 4);
         if (!s->quadtab.empty()) std::memcpy(&soa[8 * m], s->quadtab.data(), s->quadtab.size() * sizeof(float));
         HIP_TRY(hipMemcpy(c.entries, soa.data(), soa.size() * sizeof(float), hipMemcpyHostToDevice));
     }

@@ -458,7 +458,7 @@ template <bool QUADS>
 __device__ __forceinline__ uint32_t hit_material(const SceneRef E, uint32_t hit) {
     const float4 b = E.b[hit];
     if (QUADS && __float_as_int(b.w) == RTX_E_QUAD) return (uint32_t)__float_as_int(E.q[4u * __float_as_int(b.x)].w);
-    return (uint32_t)__float_as_int(b.w);
+    return RTX_DEV_SPHERE_MATERIAL(__float_as_int(b.w));
 }
 
 // Wave-cooperative rejection sampling for NewVec3UnitRandOnUnitSphere32 (vec3.go:182-190).
@@ -583,10 +583,8 @@ __device__ __forceinline__ void quad_test(Trav& t, const Ray& r, const SceneRef 
 }
 
 // QUADS: the scene holds quads (a third entry kind); false compiles the sphere-only step.
-// SENT: the step may land on the sentinel (rtx_layout.h), which it leaves unchanged
-// (spheres are then told apart by their material index, b.w >= 0).
 // FIXED: E is v3's LDS layout at LDS address 0 (scene_ref_fixed).
-template <bool COUNT, bool QUADS = false, bool SENT = false, bool FIXED = false>
+template <bool COUNT, bool QUADS = false, bool FIXED = false>
 __device__ __forceinline__ void trav_step(Trav& t, const Ray& r, const SceneRef E, Counters& cnt) {
     const float tmin = 0.001f;  // ray.go:37
     float4 ea, eb;
@@ -602,8 +600,9 @@ __device__ __forceinline__ void trav_step(Trav& t, const Ray& r, const SceneRef 
         // branch behind a second, dependent read.
         asm volatile("" ::"v"(ea.x), "v"(ea.y), "v"(ea.z), "v"(ea.w), "v"(eb.x), "v"(eb.y), "v"(eb.z), "v"(eb.w));
     }
-    if (__float_as_int(eb.w) == RTX_E_NODE) {
-        if (COUNT) ++cnt.node_visits;
+    const int32_t tag = __float_as_int(eb.w);  // device recoding, rtx_layout.h
+    if (tag >= 0) {  // a node (or the sentinel)
+        if (COUNT && __float_as_int(ea.w) != tag) ++cnt.node_visits;  // (not the sentinel: escape == next)
         // Per axis: t0 = (min - o) * invD, t1 = (max - o) * invD, swapped if invD < 0.
         // (Scalar FP32 throughout: a v_pk_mul_f32 / v_pk_add_f32 issues at a quarter of
         // v_mul_f32's rate on gfx950, scripts/micro/pk_rate.hip, so packing loses 2x.)
@@ -622,13 +621,13 @@ __device__ __forceinline__ void trav_step(Trav& t, const Ray& r, const SceneRef 
         // result: the operands are arithmetic results or +inf, never signalling NaNs.
         float hi;
         asm("v_min3_f32 %0, %1, %2, %3\n\tv_min_f32 %0, %0, %4" : "=&v"(hi) : "v"(t.closest), "v"(t1x), "v"(t1y), "v"(t1z));
-        // the next entry on a box hit, else the escape (stored as a walk position): a mask
-        // select (a ?: here became a branch).
+        // the next entry on a box hit, else the escape (both stored as walk positions): a
+        // mask select (a ?: here became a branch).
         const uint32_t take = 0u - (uint32_t)(lo < hi);
-        t.i = ((t.i + 16) & take) | ((uint32_t)__float_as_int(ea.w) & ~take);
-    } else if (QUADS && __float_as_int(eb.w) == RTX_E_QUAD) {
+        t.i = ((uint32_t)tag & take) | ((uint32_t)__float_as_int(ea.w) & ~take);
+    } else if (QUADS && tag == RTX_E_QUAD) {
         quad_test<COUNT>(t, r, E, ea, eb, cnt);
-    } else if (!SENT || __float_as_int(eb.w) >= 0) {
+    } else {
         if (COUNT) ++cnt.prim_tests;
         const float ox = r.o.x - ea.x, oy = r.o.y - ea.y, oz = r.o.z - ea.z;  // :97
         const float hb = r.d.x * ox + r.d.y * oy + r.d.z * oz;                 // :99
@@ -685,7 +684,7 @@ __device__ __forceinline__ bool shade(const Params& p, const SceneRef E, const T
         mi = (uint32_t)__float_as_int(q0.w);
         n = v3(sa.x, sa.y, sa.z);                               // q.normal
     } else {
-        mi = (uint32_t)__float_as_int(sb.w);
+        mi = RTX_DEV_SPHERE_MATERIAL(__float_as_int(sb.w));
         n = unit(scale(sub(pt, v3(sa.x, sa.y, sa.z)), sa.w));   // hittables.go:119-120
     }
     const bool front = dot(r.d, n) < 0.0f;                      // hittables.go:23

@@ -101,10 +101,10 @@ __device__ __forceinline__ void traverse_phase(uint32_t& mode, Trav& t, const Ra
                                                uint64_t& shade_lanes, uint64_t& idle_lanes) {
     for (;;) {
         // Every lane steps: one that is not traversing (or finishes early) waits on the
-        // sentinel, t.i = n_entries, where a step changes nothing — cheaper than masking
+        // sentinel, t.i = 16 * n_entries, where a step changes nothing — cheaper than masking
         // the wave per step.
 #pragma unroll
-        for (int s = 0; s < STEPS; ++s) trav_step<COUNT, QUADS, true, FIXED>(t, r, E, cnt);
+        for (int s = 0; s < STEPS; ++s) trav_step<COUNT, QUADS, FIXED>(t, r, E, cnt);
         if (mode == 0 && t.i >= 16 * n_entries) mode = 1;
         const uint64_t trav = __ballot(mode == 0);
         const uint64_t pend = __ballot(mode == 1 || mode == 2);

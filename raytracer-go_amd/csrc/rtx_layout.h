@@ -27,16 +27,24 @@
 // hittables.go:149-165, computed on the host.
 // radius*radius is the float32 product hittables.go:100 computes, precomputed.
 // On the device the halves live in two arrays (all a, then all b: rtxd::SceneRef), so
-// a wave's gathers spread over every LDS bank group.  Each array ends with one extra
-// entry, the sentinel at index n (b.w = RTX_E_SENTINEL): every walk ends there, and a
-// step on it changes nothing, so lanes that are not traversing can take the same steps
-// as those that are (rtxd::traverse_phase) instead of being masked off one step at a time.
+// a wave's gathers spread over every LDS bank group, and the integer words are recoded
+// so that a step needs no index arithmetic (rtx_capi.hip, ensure_device):
+//   positions are byte offsets, 16 * index (rtxd::Trav::i);
+//   node:   a.w = escape position, b.w = next position 16 * (i + 1)  (b.w >= 0 <=> node)
+//   sphere: b.w = RTX_DEV_SPHERE(material) = -3 - material
+//   quad:   b.w = RTX_E_QUAD
+// Each array ends with one extra entry, the sentinel at index n: a node with an empty
+// box whose escape and next are both its own position.  Every walk ends there and a
+// step on it changes nothing, whatever the ray (NaN included), so lanes that are not
+// traversing take the same steps as those that are (rtxd::traverse_phase) instead of
+// being masked off one step at a time.
 #pragma once
 #include <stdint.h>
 
 #define RTX_E_NODE (-1)
 #define RTX_E_QUAD (-2)
-#define RTX_E_SENTINEL (-3)
+#define RTX_DEV_SPHERE(material) (-3 - (int32_t)(material))
+#define RTX_DEV_SPHERE_MATERIAL(tag) ((uint32_t)(-3 - (tag)))
 
 struct rtx_entry {
     float a[4];
