@@ -275,12 +275,13 @@ __device__ __forceinline__ U4 philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c
             k0 += 0x9E3779B9u;
             k1 += 0xBB67AE85u;
         }
-        // One 32x32->64 product per word pair: a single v_mad_u64_u32 (quarter rate)
-        // instead of v_mul_lo_u32 + v_mul_hi_u32 (two quarter-rate instructions).
+        // One 32x32->64 product per word pair: a single v_mad_u64_u32 (near full rate on
+        // gfx950, scripts/micro/pk_rate.hip) instead of v_mul_lo_u32 + v_mul_hi_u32, and
+        // each three-way xor one v_bitop3_b32 (truth table 0x96) instead of two v_xor.
         const uint64_t p0 = (uint64_t)0xD2511F53u * c0;
         const uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
-        const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
-        const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+        const uint32_t n0 = __builtin_amdgcn_bitop3_b32((uint32_t)(p1 >> 32), c1, k0, 0x96);
+        const uint32_t n2 = __builtin_amdgcn_bitop3_b32((uint32_t)(p0 >> 32), c3, k1, 0x96);
         c0 = n0;
         c1 = (uint32_t)p1;
         c2 = n2;
