@@ -558,10 +558,27 @@ __device__ __forceinline__ void trav_begin(Trav& t, const Ray& r) {
 // Entry index of a walk position (a byte offset, 16 per entry: Trav::i).
 __device__ __forceinline__ int32_t entry_of(uint32_t pos) { return (int32_t)(pos >> 4); }
 
-// (Quad).Hit, hittables.go:167-194, of quad entry t.i = (ea, eb) against (tmin, closest).
+// The entry at walk position `pos`: its two halves in one LDS / memory round trip.
+template <bool FIXED>
+__device__ __forceinline__ void load_entry(const SceneRef E, uint32_t pos, float4& ea, float4& eb) {
+    if constexpr (FIXED) {
+        asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %2 offset:%3\n\ts_waitcnt lgkmcnt(0)"
+                     : "=&v"(ea), "=&v"(eb)
+                     : "v"(pos), "i"(LDS_B));
+    } else {
+        ea = *reinterpret_cast<const float4*>(reinterpret_cast<const char*>(E.a) + pos);
+        eb = *reinterpret_cast<const float4*>(reinterpret_cast<const char*>(E.b) + pos);
+        // Both halves are consumed here, so the whole entry arrives in one round trip (two
+        // 128-bit loads); otherwise the compiler sinks the node-only dwords into the box
+        // branch behind a second, dependent read.
+        asm volatile("" ::"v"(ea.x), "v"(ea.y), "v"(ea.z), "v"(ea.w), "v"(eb.x), "v"(eb.y), "v"(eb.z), "v"(eb.w));
+    }
+}
+
+// (Quad).Hit, hittables.go:167-194, of the quad entry (ea, eb) at `pos` against (tmin, closest).
 template <bool COUNT>
 __device__ __forceinline__ void quad_test(Trav& t, const Ray& r, const SceneRef E, const float4 ea, const float4 eb,
-                                          Counters& cnt) {
+                                          uint32_t pos, Counters& cnt) {
     const float tmin = 0.001f;  // ray.go:37
     if (COUNT) ++cnt.prim_tests;
     const float denom = r.d.x * ea.x + r.d.y * ea.y + r.d.z * ea.z;                 // :168
@@ -576,79 +593,86 @@ __device__ __forceinline__ void quad_test(Trav& t, const Ray& r, const SceneRef 
             const float beta = dot(w, cross(v3(q1.x, q1.y, q1.z), php));            // :183
             if (!(alpha < 0.0f || 1.0f < alpha || beta < 0.0f || 1.0f < beta)) {   // :185, :193
                 t.closest = tt;
-                t.hit = entry_of(t.i);
+                t.hit = entry_of(pos);
             }
         }
     }
-    t.i += 16;
 }
 
+// (*Sphere).Hit, hittables.go:96-116, of the sphere entry (ea, eb) at `pos` against (tmin, closest).
+template <bool COUNT>
+__device__ __forceinline__ void sphere_test(Trav& t, const Ray& r, const float4 ea, const float4 eb, uint32_t pos,
+                                            Counters& cnt) {
+    const float tmin = 0.001f;  // ray.go:37
+    if (COUNT) ++cnt.prim_tests;
+    const float ox = r.o.x - ea.x, oy = r.o.y - ea.y, oz = r.o.z - ea.z;  // :97
+    const float hb = r.d.x * ox + r.d.y * oy + r.d.z * oz;                 // :99
+    const float c = (ox * ox + oy * oy + oz * oz) - eb.x;                  // :100
+    const float disc = hb * hb - t.a * c;                                  // :102
+    if (disc >= 0.0f) {                                                    // :104 (NaN: miss either way)
+        const float sq = __builtin_sqrtf(disc);                            // :108
+        float tt = (-hb - sq) / t.a;                                       // :110
+        bool ok = tmin < tt && tt < t.closest;
+        // The second root (:112) only when the first is not beyond tmin (or NaN): a
+        // first root at or past closest makes the second, (-hb + sq) / a >= it, fail too.
+        if (!(tmin < tt)) {
+            tt = (-hb + sq) / t.a;                                         // :112
+            ok = tmin < tt && tt < t.closest;
+        }
+        if (ok) {
+            t.closest = tt;
+            t.hit = entry_of(pos);
+        }
+    }
+}
+
+// Aabb.Hit (bvh.go:52-61, 84-102) of the node entry (ea, eb) with next position `tag`:
+// the walk moves to the next entry on a hit, else to the escape.
+template <bool COUNT>
+__device__ __forceinline__ void box_step(Trav& t, const Ray& r, const float4 ea, const float4 eb, int32_t tag,
+                                         Counters& cnt) {
+    const float tmin = 0.001f;  // ray.go:37
+    if (COUNT && __float_as_int(ea.w) != tag) ++cnt.node_visits;  // (not the sentinel: escape == next)
+    // Per axis: t0 = (min - o) * invD, t1 = (max - o) * invD, swapped if invD < 0.
+    // (Scalar FP32 throughout: a v_pk_mul_f32 / v_pk_add_f32 issues at a quarter of
+    // v_mul_f32's rate on gfx950, scripts/micro/pk_rate.hip, so packing loses 2x.)
+    const float t0x = ((t.nx ? eb.x : ea.x) - r.o.x) * t.ix;
+    const float t1x = ((t.nx ? ea.x : eb.x) - r.o.x) * t.ix;
+    const float t0y = ((t.ny ? eb.y : ea.y) - r.o.y) * t.iy;
+    const float t1y = ((t.ny ? ea.y : eb.y) - r.o.y) * t.iy;
+    const float t0z = ((t.nz ? eb.z : ea.z) - r.o.z) * t.iz;
+    const float t1z = ((t.nz ? ea.z : eb.z) - r.o.z) * t.iz;
+    // `if t0 > min { min = t0 }` keeps min on NaN (0 * inf): fmaxf's NaN rule.  The
+    // bound only shrinks, so one min < max test after all three axes equals the
+    // reference's per-axis early exit.
+    const float lo = __builtin_fmaxf(__builtin_fmaxf(__builtin_fmaxf(tmin, t0x), t0y), t0z);
+    // hi = fminf(fminf(fminf(closest, t1x), t1y), t1z) as v_min3 + v_min: the builtin
+    // would first canonicalize `closest` (one more VALU per box).  Same IEEE-mode
+    // result: the operands are arithmetic results or +inf, never signalling NaNs.
+    float hi;
+    asm("v_min3_f32 %0, %1, %2, %3\n\tv_min_f32 %0, %0, %4" : "=&v"(hi) : "v"(t.closest), "v"(t1x), "v"(t1y), "v"(t1z));
+    // the next entry on a box hit, else the escape (both stored as walk positions): a
+    // mask select (a ?: here became a branch).
+    const uint32_t take = 0u - (uint32_t)(lo < hi);
+    t.i = ((uint32_t)tag & take) | ((uint32_t)__float_as_int(ea.w) & ~take);
+}
+
+// One step of the closest-hit walk over the threaded pre-order layout (rtx_layout.h):
+// entry i is a node (Aabb.Hit, bvh.go:52-61, 84-102) or a sphere (Sphere.Hit,
+// hittables.go:96-116).  The sequence of steps is the reference recursion's, with
+// running bound `closest` = the closest hit so far (bvh.go:227-232).
 // QUADS: the scene holds quads (a third entry kind); false compiles the sphere-only step.
 // FIXED: E is v3's LDS layout at LDS address 0 (scene_ref_fixed).
 template <bool COUNT, bool QUADS = false, bool FIXED = false>
 __device__ __forceinline__ void trav_step(Trav& t, const Ray& r, const SceneRef E, Counters& cnt) {
-    const float tmin = 0.001f;  // ray.go:37
     float4 ea, eb;
-    if constexpr (FIXED) {
-        asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %2 offset:%3\n\ts_waitcnt lgkmcnt(0)"
-                     : "=&v"(ea), "=&v"(eb)
-                     : "v"(t.i), "i"(LDS_B));
-    } else {
-        ea = *reinterpret_cast<const float4*>(reinterpret_cast<const char*>(E.a) + t.i);
-        eb = *reinterpret_cast<const float4*>(reinterpret_cast<const char*>(E.b) + t.i);
-        // Both halves are consumed here, so the whole entry arrives in one round trip (two
-        // 128-bit loads); otherwise the compiler sinks the node-only dwords into the box
-        // branch behind a second, dependent read.
-        asm volatile("" ::"v"(ea.x), "v"(ea.y), "v"(ea.z), "v"(ea.w), "v"(eb.x), "v"(eb.y), "v"(eb.z), "v"(eb.w));
-    }
+    load_entry<FIXED>(E, t.i, ea, eb);
     const int32_t tag = __float_as_int(eb.w);  // device recoding, rtx_layout.h
     if (tag >= 0) {  // a node (or the sentinel)
-        if (COUNT && __float_as_int(ea.w) != tag) ++cnt.node_visits;  // (not the sentinel: escape == next)
-        // Per axis: t0 = (min - o) * invD, t1 = (max - o) * invD, swapped if invD < 0.
-        // (Scalar FP32 throughout: a v_pk_mul_f32 / v_pk_add_f32 issues at a quarter of
-        // v_mul_f32's rate on gfx950, scripts/micro/pk_rate.hip, so packing loses 2x.)
-        const float t0x = ((t.nx ? eb.x : ea.x) - r.o.x) * t.ix;
-        const float t1x = ((t.nx ? ea.x : eb.x) - r.o.x) * t.ix;
-        const float t0y = ((t.ny ? eb.y : ea.y) - r.o.y) * t.iy;
-        const float t1y = ((t.ny ? ea.y : eb.y) - r.o.y) * t.iy;
-        const float t0z = ((t.nz ? eb.z : ea.z) - r.o.z) * t.iz;
-        const float t1z = ((t.nz ? ea.z : eb.z) - r.o.z) * t.iz;
-        // `if t0 > min { min = t0 }` keeps min on NaN (0 * inf): fmaxf's NaN rule.  The
-        // bound only shrinks, so one min < max test after all three axes equals the
-        // reference's per-axis early exit.
-        const float lo = __builtin_fmaxf(__builtin_fmaxf(__builtin_fmaxf(tmin, t0x), t0y), t0z);
-        // hi = fminf(fminf(fminf(closest, t1x), t1y), t1z) as v_min3 + v_min: the builtin
-        // would first canonicalize `closest` (one more VALU per box).  Same IEEE-mode
-        // result: the operands are arithmetic results or +inf, never signalling NaNs.
-        float hi;
-        asm("v_min3_f32 %0, %1, %2, %3\n\tv_min_f32 %0, %0, %4" : "=&v"(hi) : "v"(t.closest), "v"(t1x), "v"(t1y), "v"(t1z));
-        // the next entry on a box hit, else the escape (both stored as walk positions): a
-        // mask select (a ?: here became a branch).
-        const uint32_t take = 0u - (uint32_t)(lo < hi);
-        t.i = ((uint32_t)tag & take) | ((uint32_t)__float_as_int(ea.w) & ~take);
-    } else if (QUADS && tag == RTX_E_QUAD) {
-        quad_test<COUNT>(t, r, E, ea, eb, cnt);
+        box_step<COUNT>(t, r, ea, eb, tag, cnt);
     } else {
-        if (COUNT) ++cnt.prim_tests;
-        const float ox = r.o.x - ea.x, oy = r.o.y - ea.y, oz = r.o.z - ea.z;  // :97
-        const float hb = r.d.x * ox + r.d.y * oy + r.d.z * oz;                 // :99
-        const float c = (ox * ox + oy * oy + oz * oz) - eb.x;                  // :100
-        const float disc = hb * hb - t.a * c;                                  // :102
-        if (disc >= 0.0f) {                                                    // :104 (NaN: miss either way)
-            const float sq = __builtin_sqrtf(disc);                            // :108
-            float tt = (-hb - sq) / t.a;                                       // :110
-            bool ok = tmin < tt && tt < t.closest;
-            // The second root (:112) only when the first is not beyond tmin (or NaN): a
-            // first root at or past closest makes the second, (-hb + sq) / a >= it, fail too.
-            if (!(tmin < tt)) {
-                tt = (-hb + sq) / t.a;                                         // :112
-                ok = tmin < tt && tt < t.closest;
-            }
-            if (ok) {
-                t.closest = tt;
-                t.hit = entry_of(t.i);
-            }
-        }
+        if (QUADS && tag == RTX_E_QUAD) quad_test<COUNT>(t, r, E, ea, eb, t.i, cnt);
+        else sphere_test<COUNT>(t, r, ea, eb, t.i, cnt);
         t.i += 16;
     }
 }
