@@ -222,9 +222,19 @@ int ensure_device(rtx_scene* s, int device, DeviceCopy** out) {
         if (!s->quadtab.empty()) std::memcpy(&soa[8 * m], s->quadtab.data(), s->quadtab.size() * sizeof(float));
         HIP_TRY(hipMemcpy(c.entries, soa.data(), soa.size() * sizeof(float), hipMemcpyHostToDevice));
     }
-    HIP_TRY(hipMalloc(&c.materials, std::max<size_t>(1, s->materials.size()) * sizeof(rtx_material)));
-    if (!s->materials.empty())
-        HIP_TRY(hipMemcpy(c.materials, s->materials.data(), s->materials.size() * sizeof(rtx_material), hipMemcpyHostToDevice));
+    {  // device materials: a Lambertian or DiffuseLight with a SolidColor texture carries the
+       // colour itself (rtxd::RTX_DEV_TEX_INLINE), so shading reads no texture record
+        std::vector<rtx_material> dm(s->materials);
+        for (rtx_material& m : dm) {
+            if ((m.type == RTX_MAT_LAMBERTIAN || m.type == RTX_MAT_DIFFUSE_LIGHT) &&
+                s->textures[m.texture].type == RTX_TEX_SOLID) {
+                std::memcpy(m.albedo, s->textures[m.texture].even, sizeof(m.albedo));
+                m.texture = rtxd::RTX_DEV_TEX_INLINE;
+            }
+        }
+        HIP_TRY(hipMalloc(&c.materials, std::max<size_t>(1, dm.size()) * sizeof(rtx_material)));
+        if (!dm.empty()) HIP_TRY(hipMemcpy(c.materials, dm.data(), dm.size() * sizeof(rtx_material), hipMemcpyHostToDevice));
+    }
     HIP_TRY(hipMalloc(&c.textures, std::max<size_t>(1, s->textures.size()) * sizeof(rtx_texture)));
     if (!s->textures.empty())
         HIP_TRY(hipMemcpy(c.textures, s->textures.data(), s->textures.size() * sizeof(rtx_texture), hipMemcpyHostToDevice));

@@ -328,27 +328,40 @@ __device__ __forceinline__ uint32_t lane_pull(uint32_t src_lane, uint32_t v) {
 struct SceneRef {
     const float4* __restrict__ a;
     const float4* __restrict__ b;
-    const float4* __restrict__ q;  // quad table, 4 float4 per quad (rtx_layout.h)
+    const float4* __restrict__ q;          // quad table, 4 float4 per quad (rtx_layout.h)
+    const rtx_material* __restrict__ m;    // device materials (RTX_DEV_TEX_INLINE recoding)
 };
-__device__ __forceinline__ SceneRef scene_ref(const float4* base, uint32_t n_entries) {
+__device__ __forceinline__ SceneRef scene_ref(const float4* base, uint32_t n_entries, const rtx_material* mats) {
     const uint32_t m = n_entries + 1;  // + the sentinel
-    return SceneRef{base, base + m, base + 2 * m};
+    return SceneRef{base, base + m, base + 2 * m, mats};
 }
 // v3's LDS layout: the 'a' halves from LDS byte 0, the 'b' halves from byte LDS_B, the
 // quad table after them.  A walk position is then the LDS address of its 'a' half and
 // both halves load from one register (ds_read_b128 offset:0 / offset:LDS_B): no address
-// arithmetic per step.
+// arithmetic per step.  The material table goes into the gap after the 'a' halves when
+// it fits there (randSpheres: 15.9 KB of halves + 15.6 KB of materials < 32 KB), else
+// after the quad table.
 constexpr uint32_t LDS_B = 32768;
-__host__ __device__ __forceinline__ uint32_t lds_fixed_bytes(uint32_t n_entries, uint32_t n_quads) {
-    return LDS_B + (n_entries + 1) * 16 + n_quads * 64;
+__host__ __device__ __forceinline__ uint32_t lds_mat_offset(uint32_t n_entries, uint32_t n_quads, uint32_t n_mats) {
+    const uint32_t halves = (n_entries + 1) * 16;
+    return halves + n_mats * 32 <= LDS_B ? halves : LDS_B + halves + n_quads * 64;
 }
-__device__ __forceinline__ SceneRef scene_ref_fixed(const float4* lds, uint32_t n_entries) {
-    return SceneRef{lds, lds + LDS_B / 16, lds + LDS_B / 16 + n_entries + 1};
+__host__ __device__ __forceinline__ uint32_t lds_fixed_bytes(uint32_t n_entries, uint32_t n_quads, uint32_t n_mats) {
+    const uint32_t end = LDS_B + (n_entries + 1) * 16 + n_quads * 64, mo = lds_mat_offset(n_entries, n_quads, n_mats);
+    return mo < LDS_B ? end : mo + n_mats * 32;
+}
+__device__ __forceinline__ SceneRef scene_ref_fixed(const float4* lds, uint32_t n_entries, uint32_t n_quads,
+                                                    uint32_t n_mats) {
+    return SceneRef{lds, lds + LDS_B / 16, lds + LDS_B / 16 + n_entries + 1,
+                    reinterpret_cast<const rtx_material*>(lds + lds_mat_offset(n_entries, n_quads, n_mats) / 16)};
 }
 // float4s of a scene's device table: both halves with their sentinels, then the quads.
 __host__ __device__ __forceinline__ uint32_t scene_float4s(uint32_t n_entries, uint32_t n_quads) {
     return 2 * (n_entries + 1) + 4 * n_quads;
 }
+// Device material recoding (rtx_capi.hip ensure_device): a Lambertian / DiffuseLight
+// whose texture is a SolidColor holds the colour in `albedo` and this texture index.
+constexpr uint32_t RTX_DEV_TEX_INLINE = 0xFFFFFFFFu;
 
 // ---------------------------------------------------------------------------------
 // Kernel parameters
@@ -480,7 +493,7 @@ __device__ __forceinline__ Scatter coop_scatter(const Params& p, const SceneRef 
     if (hit >= 0) {
         const U4 b0 = rng.block(e, 0);
         const uint32_t mi = hit_material<QUADS>(E, (uint32_t)hit);
-        const uint32_t ty = p.materials[mi].type;
+        const uint32_t ty = E.m[mi].type;
         need = ty == RTX_MAT_LAMBERTIAN || ty == RTX_MAT_METAL;
         out.u0 = b0.x;
         x = signed_unit(b0.x);
@@ -713,9 +726,10 @@ __device__ __forceinline__ bool shade(const Params& p, const SceneRef E, const T
         n = unit(scale(sub(pt, v3(sa.x, sa.y, sa.z)), sa.w));   // hittables.go:119-120
     }
     const bool front = dot(r.d, n) < 0.0f;                      // hittables.go:23
-    const rtx_material m = p.materials[mi];
+    const rtx_material m = E.m[mi];
     float u = 0.0f, v = 0.0f;
-    if (p.has_uv && (m.type == RTX_MAT_LAMBERTIAN || m.type == RTX_MAT_DIFFUSE_LIGHT) &&
+    const bool inl = m.texture == RTX_DEV_TEX_INLINE;  // SolidColor, colour in m.albedo
+    if (p.has_uv && (m.type == RTX_MAT_LAMBERTIAN || m.type == RTX_MAT_DIFFUSE_LIGHT) && !inl &&
         p.textures[m.texture].type == RTX_TEX_IMAGE) {           // only an image texture reads UV
         if (quad) {  // (alpha, beta) of the hit, recomputed as quad_test did (hittables.go:181-183)
             const V3 php = sub(pt, v3(q0.x, q0.y, q0.z));
@@ -743,7 +757,8 @@ __device__ __forceinline__ bool shade(const Params& p, const SceneRef E, const T
         if (m.type == RTX_MAT_LAMBERTIAN) {                     // materials.go:33-42
             V3 dir = add(n, s);
             if (near_zero(dir)) dir = n;
-            const V3 att = texture_value<COUNT, NOISE>(p, m.texture, u, v, pt, cnt);
+            const V3 att = inl ? v3(m.albedo[0], m.albedo[1], m.albedo[2])
+                               : texture_value<COUNT, NOISE>(p, m.texture, u, v, pt, cnt);
             thr = mul(thr, att);
             r = Ray{pt, dir};
             return false;
@@ -776,7 +791,7 @@ __device__ __forceinline__ bool shade(const Params& p, const SceneRef E, const T
         return false;
     }
     // DiffuseLight: emit, never scatters (materials.go:303-313)
-    const V3 em = texture_value<COUNT, NOISE>(p, m.texture, u, v, pt, cnt);
+    const V3 em = inl ? v3(m.albedo[0], m.albedo[1], m.albedo[2]) : texture_value<COUNT, NOISE>(p, m.texture, u, v, pt, cnt);
     color = add(acc, mul(thr, em));
     return true;
 }

@@ -60,7 +60,7 @@ __global__ __launch_bounds__(BLOCK) void render_pixels(Params p) {
     const V3 base = pixel_base(c, x, y);
     PathRng rng{(uint32_t)p.seed, (uint32_t)(p.seed >> 32), y * c.image_width + x, 0};
     Counters cnt{0, 0, 0, 0, 0, 0};
-    const SceneRef E = scene_ref(p.entries, p.n_entries);
+    const SceneRef E = scene_ref(p.entries, p.n_entries, p.materials);
     V3 sum = v3(0.0f, 0.0f, 0.0f);
     for (uint32_t k = 0; k < c.samples_per_pixel; ++k) {
         rng.sample = k;
@@ -151,9 +151,9 @@ __global__ __launch_bounds__(64 * WX * WY, MINW) void render_wave(Params p) {
         const uint32_t n4 = scene_float4s(p.n_entries, p.n_quads);  // entries, then the quad table
         for (uint32_t t = threadIdx.x; t < n4; t += WAVE_BLOCK) lds_entries[t] = p.entries[t];
         __syncthreads();
-        E = scene_ref(lds_entries, p.n_entries);
+        E = scene_ref(lds_entries, p.n_entries, p.materials);
     } else {
-        E = scene_ref(p.entries, p.n_entries);
+        E = scene_ref(p.entries, p.n_entries, p.materials);
     }
     const uint32_t n_entries = p.n_entries;
     const uint32_t thresh = p.shade_thresh;
@@ -324,10 +324,13 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
             lds_entries[LDS_B / 16 + t] = p.entries[m + t];
         }
         for (uint32_t t = threadIdx.x; t < nq4; t += WAVE_BLOCK) lds_entries[LDS_B / 16 + m + t] = p.entries[2 * m + t];
+        const uint32_t mo = lds_mat_offset(p.n_entries, p.n_quads, p.n_materials) / 16;
+        const float4* mg = reinterpret_cast<const float4*>(p.materials);
+        for (uint32_t t = threadIdx.x; t < 2 * p.n_materials; t += WAVE_BLOCK) lds_entries[mo + t] = mg[t];
         __syncthreads();
-        E = scene_ref_fixed(lds_entries, p.n_entries);
+        E = scene_ref_fixed(lds_entries, p.n_entries, p.n_quads, p.n_materials);
     } else {
-        E = scene_ref(p.entries, p.n_entries);
+        E = scene_ref(p.entries, p.n_entries, p.materials);
     }
     const uint32_t n_entries = p.n_entries;
     const uint32_t thresh = p.shade_thresh;
@@ -542,9 +545,9 @@ __global__ __launch_bounds__(POOL_BLOCK) void render_pool(Params p) {
         float4* scene = lds_dyn + (POOL_WAVES * sizeof(Pool)) / 16;
         const uint32_t n4 = scene_float4s(p.n_entries, 0);
         for (uint32_t t = threadIdx.x; t < n4; t += POOL_BLOCK) scene[t] = p.entries[t];
-        E = scene_ref(scene, p.n_entries);
+        E = scene_ref(scene, p.n_entries, p.materials);
     } else {
-        E = scene_ref(p.entries, p.n_entries);
+        E = scene_ref(p.entries, p.n_entries, p.materials);
     }
     const uint32_t n_entries = p.n_entries;
     const uint32_t thresh = p.shade_thresh;
@@ -776,7 +779,7 @@ hipError_t launch_wave(const Params& p, uint32_t geom, bool use_lds, hipStream_t
 // resident-capacity grid of render_items and summed into p.out by reduce_samples.
 template <bool COUNT, bool QUADS, bool NOISE, int WAVES = 8, int MINW = 0>
 hipError_t launch_items(Params p, bool use_lds, hipStream_t stream) {
-    const size_t shmem = use_lds ? lds_fixed_bytes(p.n_entries, p.n_quads) : 0;
+    const size_t shmem = use_lds ? lds_fixed_bytes(p.n_entries, p.n_quads, p.n_materials) : 0;
     const auto kern = use_lds ? render_items<COUNT, true, QUADS, NOISE, WAVES, MINW>
                               : render_items<COUNT, false, QUADS, NOISE, WAVES, MINW>;
     constexpr int block = 64 * WAVES;
@@ -834,7 +837,7 @@ hipError_t launch_render(const Params& p, uint32_t flags, hipStream_t stream) {
     if (uses_items(p, flags)) {
         if (!p.scratch) return hipErrorInvalidValue;  // the caller sizes the v3 scratch
         const bool use_lds = !(flags & RTX_FLAG_NO_LDS) && (p.n_entries + 1) * 16 <= LDS_B &&
-                             lds_fixed_bytes(p.n_entries, p.n_quads) <= LDS_MAX_BYTES;
+                             lds_fixed_bytes(p.n_entries, p.n_quads, p.n_materials) <= LDS_MAX_BYTES;
         return count ? launch_items_for<true>(p, use_lds, stream) : launch_items_for<false>(p, use_lds, stream);
     }
     if (flags & RTX_FLAG_KERNEL_V0) {
