@@ -29,12 +29,13 @@ ap.add_argument("--scene", default="random_spheres")
 ap.add_argument("--width", type=int, default=1920)
 ap.add_argument("--spp", type=int, default=100)
 ap.add_argument("--rounds", type=int, default=3)
+ap.add_argument("--depth", type=int, default=0, help="max depth (0: the scene's)")
 ap.add_argument("--variants", default="v1,v0")
 args = ap.parse_args()
 
 torch.cuda.set_device(0)
 scene = rtx.HostScene(args.scene, 1)
-cam = scene.camera(width=args.width, spp=args.spp)
+cam = scene.camera(width=args.width, spp=args.spp, depth=args.depth)
 dev = rtx.DeviceScene(scene.desc)
 reg = rtx.Region(0, 0, cam.image_width, cam.image_height, 0, 1)
 names = args.variants.split(",")
@@ -43,12 +44,28 @@ for n in names:  # "a+b" = the flags of a and b together
         VARIANTS[n] = 0
         for part in n.split("+"):
             VARIANTS[n] |= VARIANTS[part]
+ENV = {}  # "name@K=V;K2=V2": the flags of name with those environment knobs (read per render)
+for n in names:
+    if "@" in n:
+        base, kv = n.split("@", 1)
+        VARIANTS[n] = VARIANTS[base]
+        ENV[n] = dict(x.split("=", 1) for x in kv.split(";"))
+KNOBS = sorted({k for e in ENV.values() for k in e})
+
+
+def setenv(n):
+    for k in KNOBS:
+        os.environ.pop(k, None)
+    os.environ.update(ENV.get(n, {}))
+
+
 outs = {n: torch.zeros((cam.image_height, cam.image_width, 3), device="cuda") for n in names}
 stream = torch.cuda.current_stream().cuda_stream
 st = dev.render_region(cam, 1, reg, outs[names[0]].data_ptr(), stream, counters=True, timed=True)
 times = {n: [] for n in names}
 for rnd in range(args.rounds + 1):
     for n in names:
+        setenv(n)
         s = dev.render_region(cam, 1, reg, outs[n].data_ptr(), stream, timed=True, flags=VARIANTS[n])
         if rnd > 0:
             times[n].append(s.kernel_ms)
@@ -59,6 +76,7 @@ for n in names:
     print(f"{n:8s} median {med:9.2f} ms  min {min(times[n]):9.2f}  Gsamples/s {st.samples / med / 1e6:7.3f}  "
           f"Mray/s {st.segments / med / 1e3:9.1f}  identical={same}", flush=True)
 # scheduling counters of each variant (a separate counting launch)
+setenv("")
 for n in names:
     c = dev.render_region(cam, 1, reg, outs[n].data_ptr(), stream, counters=True, timed=True, flags=VARIANTS[n])
     if c.wave_iters:

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Summarise rocprofv3 --pmc CSVs: per kernel name, the mean of each counter over its
-dispatches.  python scripts/pmc_summary.py gpurun_out/pmc"""
+dispatches and the sum over them.  python scripts/pmc_summary.py gpurun_out/pmc"""
 import csv
 import glob
 import sys
@@ -11,7 +11,7 @@ vals = defaultdict(lambda: defaultdict(list))
 for f in sorted(glob.glob(f"{root}/**/*counter_collection.csv", recursive=True)):
     for row in csv.DictReader(open(f)):
         name = row["Kernel_Name"].replace("(rtxd::Params)", "").replace("void rtxd::", "")
-        if "render" not in name:
+        if not any(k in name for k in ("render", "trace_paths", "shade_paths", "reduce")):
             continue
         key = (row["Dispatch_Id"], f)
         vals[name][row["Counter_Name"]].append(float(row["Counter_Value"]))
@@ -19,4 +19,4 @@ for name, cs in vals.items():
     print(name)
     for c in sorted(cs):
         v = cs[c]
-        print(f"   {c:24s} {sum(v) / len(v):16.4g}  (n={len(v)})")
+        print(f"   {c:24s} {sum(v) / len(v):16.4g}  sum {sum(v):14.4g}  (n={len(v)})")
