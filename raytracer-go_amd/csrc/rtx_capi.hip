@@ -374,7 +374,7 @@ int enqueue_on(rtx_scene* s, DeviceCopy* c, const rtx_camera* cam, uint64_t seed
         HIP_TRY(hipStreamWaitEvent(stream, scr->last, 0));
         p.scratch = scr->ptr;
         p.kn = (uint32_t)chunk;
-        p.sub = env_knob("RTX_ITEM_SUB", 16, 1, 4096);
+        p.sub = env_knob("RTX_ITEM_SUB", 0, 0, 4096);  // 0: chosen per chunk by launch_items
         p.item_waves = env_knob("RTX_ITEM_WAVES", 8, 4, 8) >= 8 ? 8u : 4u;
     }
     if (flags & RTX_FLAG_COUNTERS) HIP_TRY(hipMemsetAsync(c->counters, 0, 16 * sizeof(unsigned long long), stream));

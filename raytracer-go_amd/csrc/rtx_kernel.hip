@@ -789,12 +789,19 @@ hipError_t launch_items(Params p, bool use_lds, hipStream_t stream) {
     if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, block, shmem);
     if (e != hipSuccess) return e;
     if (per_cu < 1) per_cu = 1;
-    const uint32_t spp = p.cam.samples_per_pixel, chunk = p.kn;
+    const uint32_t spp = p.cam.samples_per_pixel, chunk = p.kn, sub = p.sub;
     const uint64_t tiles = (uint64_t)((p.width + 7) / 8) * ((p.rows + 7) / 8);
     const uint64_t npix = (uint64_t)p.width * p.rows;
     for (uint32_t k0 = 0; k0 < spp; k0 += chunk) {
         p.k0 = k0;
         p.kn = spp - k0 < chunk ? spp - k0 : chunk;
+        if (sub == 0) {
+            // Samples per unit: 8, or fewer when that leaves under 8 units per resident wave
+            // (a small image's last units would run on a near-empty GPU).  Measured at 100 spp:
+            // 1920x1080 8 -1.6 % vs 16; 400x225 2 -42 % vs 16; Cornell 600x600 8 -3 % vs 16.
+            const uint64_t per_wave = tiles * p.kn / (8ull * WAVES * (uint64_t)per_cu * cus);
+            p.sub = per_wave >= 8 ? 8u : (per_wave >= 4 ? 4u : (per_wave >= 2 ? 2u : 1u));
+        }
         const uint64_t units = tiles * ((p.kn + p.sub - 1) / p.sub);
         uint64_t blocks = (uint64_t)per_cu * cus;
         if (blocks > (units + WAVES - 1) / WAVES) blocks = (units + WAVES - 1) / WAVES;  // no wave starts idle
