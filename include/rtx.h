@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define RTX_ABI_VERSION 2
+#define RTX_ABI_VERSION 3
 
 /* ---- status codes ------------------------------------------------------------ */
 enum {
@@ -201,6 +201,9 @@ typedef struct rtx_stats {
     uint64_t trav_cycles;  /* v1: shader cycles (s_memtime) in traversal, summed over waves */
     uint64_t shade_cycles; /* v1: shader cycles in shading phases, summed over waves  */
     uint64_t idle_lanes;   /* v1: lanes whose pixel is finished, summed over iterations */
+    uint64_t cache_hits;   /* v3, scenes too big for LDS: entries (of node_visits + prim_tests and
+                              the steps on the end sentinel) read from the LDS cache of the top
+                              levels */
 } rtx_stats;
 
 #define RTX_FLAG_COUNTERS 1u /* count work units (separate kernel instantiation) */

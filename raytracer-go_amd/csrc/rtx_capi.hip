@@ -55,6 +55,7 @@ struct DeviceCopy {
     uint32_t* texels = nullptr;
     unsigned long long* counters = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    uint32_t hot = 0;  // entries stored first and cached in LDS by v3 (scenes too big for the LDS copy)
 };
 
 // v3 sample-colour scratch, one per device, shared by all scenes (grown on demand and
@@ -180,6 +181,8 @@ int emit(const rtx_scene_desc* d, int32_t root, std::vector<rtx_entry>& out) {
     return RTX_OK;
 }
 
+uint32_t env_knob(const char* name, long dflt, long lo, long hi);
+
 int ensure_device(rtx_scene* s, int device, DeviceCopy** out) {
     auto it = s->copies.find(device);
     if (it != s->copies.end()) {
@@ -191,23 +194,55 @@ int ensure_device(rtx_scene* s, int device, DeviceCopy** out) {
     HIP_TRY(hipSetDevice(device));
     HIP_TRY(hipMalloc(&c.entries, (s->entries.size() + 1) * sizeof(rtx_entry) + s->quadtab.size() * sizeof(float)));
     {  // device layout: all 'a' halves, then all 'b' halves (rtxd::SceneRef), each ending
-       // with the sentinel entry (rtx_layout.h)
+       // with the sentinel entry (rtx_layout.h).  Every entry names its successor (node: next
+       // and escape, primitive: next), so the storage order is free: a scene too big for the
+       // LDS copy stores its top levels first (c.hot entries), which v3 caches in LDS.
         const size_t n = s->entries.size(), m = n + 1;
+        std::vector<uint32_t> pos(m);  // storage index of entry i; the sentinel stays last
+        for (size_t i = 0; i <= n; ++i) pos[i] = (uint32_t)i;
+        if (m * 16 > rtxd::LDS_B) {
+            std::vector<uint32_t> depth(n), ends, per_depth;
+            for (size_t i = 0; i < n; ++i) {  // depth = nodes whose subtree holds entry i
+                while (!ends.empty() && ends.back() <= i) ends.pop_back();
+                depth[i] = (uint32_t)ends.size();
+                if (per_depth.size() <= depth[i]) per_depth.resize(depth[i] + 1, 0);
+                ++per_depth[depth[i]];
+                int32_t tag, esc;
+                std::memcpy(&tag, &s->entries[i].b[3], 4);
+                if (tag == RTX_E_NODE) {
+                    std::memcpy(&esc, &s->entries[i].a[3], 4);
+                    ends.push_back((uint32_t)esc);
+                }
+            }
+            const uint32_t cap = env_knob("RTX_HOT_ENTRIES", rtxd::HOT_ENTRIES_MAX, 0, rtxd::HOT_ENTRIES_MAX);
+            uint32_t levels = 0, hot = 0;
+            while (levels < per_depth.size() && hot + per_depth[levels] <= cap) hot += per_depth[levels++];
+            uint32_t k = 0;
+            for (size_t i = 0; i < n; ++i)
+                if (depth[i] < levels) pos[i] = k++;
+            for (size_t i = 0; i < n; ++i)
+                if (depth[i] >= levels) pos[i] = k++;
+            c.hot = hot;
+        }
         std::vector<float> soa(m * 8 + s->quadtab.size(), 0.0f);
         for (size_t i = 0; i < n; ++i) {
-            std::memcpy(&soa[4 * i], s->entries[i].a, 16);
-            std::memcpy(&soa[4 * (m + i)], s->entries[i].b, 16);
+            const size_t j = pos[i];
+            std::memcpy(&soa[4 * j], s->entries[i].a, 16);
+            std::memcpy(&soa[4 * (m + j)], s->entries[i].b, 16);
             int32_t tag, esc;  // the device recoding, rtx_layout.h
             std::memcpy(&tag, &s->entries[i].b[3], 4);
+            const int32_t next = (int32_t)(16 * pos[i + 1]);
             if (tag == RTX_E_NODE) {
                 std::memcpy(&esc, &s->entries[i].a[3], 4);
-                esc *= 16;
-                const int32_t next = (int32_t)(16 * (i + 1));
-                std::memcpy(&soa[4 * i + 3], &esc, 4);
-                std::memcpy(&soa[4 * (m + i) + 3], &next, 4);
-            } else if (tag >= 0) {
-                const int32_t sph = RTX_DEV_SPHERE(tag);
-                std::memcpy(&soa[4 * (m + i) + 3], &sph, 4);
+                esc = (int32_t)(16 * pos[esc]);
+                std::memcpy(&soa[4 * j + 3], &esc, 4);
+                std::memcpy(&soa[4 * (m + j) + 3], &next, 4);
+            } else {
+                std::memcpy(&soa[4 * (m + j) + 2], &next, 4);  // a primitive's successor
+                if (tag >= 0) {
+                    const int32_t sph = RTX_DEV_SPHERE(tag);
+                    std::memcpy(&soa[4 * (m + j) + 3], &sph, 4);
+                }
             }
         }
         // the sentinel: box min +inf, max -inf, escape = next = its own position
@@ -340,6 +375,7 @@ rtxd::Params make_params(const rtx_scene* s, const DeviceCopy* c, const rtx_came
     p.shade_thresh = shade_thresh();
     p.has_uv = s->has_image ? 1u : 0u;
     p.has_noise = s->has_noise ? 1u : 0u;
+    p.n_hot = c->hot;
     return p;
 }
 
@@ -408,6 +444,7 @@ int collect_on(DeviceCopy* c, bool count, uint64_t samples, rtx_stats* st) {
     st->trav_cycles = h[12];
     st->shade_cycles = h[13];
     st->idle_lanes = h[14];
+    st->cache_hits = h[15];
     st->kernel_ms = ms;
     return RTX_OK;
 }

@@ -330,10 +330,15 @@ struct SceneRef {
     const float4* __restrict__ b;
     const float4* __restrict__ q;          // quad table, 4 float4 per quad (rtx_layout.h)
     const rtx_material* __restrict__ m;    // device materials (RTX_DEV_TEX_INLINE recoding)
+    // v3 on a scene too big for LDS: its first `hot` bytes of positions (the top levels,
+    // stored first) are also in LDS, halves at la / lb (load_entry<HYB>)
+    const float4* la;
+    const float4* lb;
+    uint32_t hot;
 };
 __device__ __forceinline__ SceneRef scene_ref(const float4* base, uint32_t n_entries, const rtx_material* mats) {
     const uint32_t m = n_entries + 1;  // + the sentinel
-    return SceneRef{base, base + m, base + 2 * m, mats};
+    return SceneRef{base, base + m, base + 2 * m, mats, nullptr, nullptr, 0u};
 }
 // v3's LDS layout: the 'a' halves from LDS byte 0, the 'b' halves from byte LDS_B, the
 // quad table after them.  A walk position is then the LDS address of its 'a' half and
@@ -353,8 +358,14 @@ __host__ __device__ __forceinline__ uint32_t lds_fixed_bytes(uint32_t n_entries,
 __device__ __forceinline__ SceneRef scene_ref_fixed(const float4* lds, uint32_t n_entries, uint32_t n_quads,
                                                     uint32_t n_mats) {
     return SceneRef{lds, lds + LDS_B / 16, lds + LDS_B / 16 + n_entries + 1,
-                    reinterpret_cast<const rtx_material*>(lds + lds_mat_offset(n_entries, n_quads, n_mats) / 16)};
+                    reinterpret_cast<const rtx_material*>(lds + lds_mat_offset(n_entries, n_quads, n_mats) / 16),
+                    nullptr, nullptr, 0u};
 }
+// The LDS cache of a scene too big for the fixed layout: its first HOT_ENTRIES_MAX entries
+// (the top levels, rtx_capi.hip ensure_device) in the fixed layout's places, 52 KB per
+// workgroup, so three 8-wave workgroups still share a CU.
+constexpr uint32_t HOT_ENTRIES_MAX = 1280;
+__host__ __device__ __forceinline__ uint32_t lds_hot_bytes(uint32_t n_hot) { return LDS_B + n_hot * 16; }
 // float4s of a scene's device table: both halves with their sentinels, then the quads.
 __host__ __device__ __forceinline__ uint32_t scene_float4s(uint32_t n_entries, uint32_t n_quads) {
     return 2 * (n_entries + 1) + 4 * n_quads;
@@ -390,6 +401,7 @@ struct Params {
     float* scratch;
     uint32_t k0, kn, sub;
     uint32_t item_waves;  // v3 waves per workgroup: 8 (one LDS scene copy each), or 4 for A/B
+    uint32_t n_hot;       // entries stored first and cached in LDS by v3 when the scene does not fit
 };
 
 struct Ray {
@@ -398,6 +410,7 @@ struct Ray {
 
 struct Counters {
     uint32_t segments, node_visits, prim_tests, hits, texel_fetches, draws;
+    uint32_t cache_hits;  // entries read from the LDS cache of a big scene (load_entry<HYB>)
 };
 
 // GetRay + sampleUnitSquare, camera.go:265-299, event 0.  base = (pixel00 + du*i) + dv*j.
@@ -572,9 +585,16 @@ __device__ __forceinline__ void trav_begin(Trav& t, const Ray& r) {
 __device__ __forceinline__ int32_t entry_of(uint32_t pos) { return (int32_t)(pos >> 4); }
 
 // The entry at walk position `pos`: its two halves in one LDS / memory round trip.
-template <bool FIXED>
+template <bool FIXED, bool HYB = false>
 __device__ __forceinline__ void load_entry(const SceneRef E, uint32_t pos, float4& ea, float4& eb) {
-    if constexpr (FIXED) {
+    if constexpr (HYB) {  // the top levels from the LDS cache, the rest from HBM: one flat load each
+        const bool hot = pos < E.hot;
+        const float4* pa = hot ? E.la : E.a;
+        const float4* pb = hot ? E.lb : E.b;
+        ea = *reinterpret_cast<const float4*>(reinterpret_cast<const char*>(pa) + pos);
+        eb = *reinterpret_cast<const float4*>(reinterpret_cast<const char*>(pb) + pos);
+        asm volatile("" ::"v"(ea.x), "v"(ea.y), "v"(ea.z), "v"(ea.w), "v"(eb.x), "v"(eb.y), "v"(eb.z), "v"(eb.w));
+    } else if constexpr (FIXED) {
         asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %2 offset:%3\n\ts_waitcnt lgkmcnt(0)"
                      : "=&v"(ea), "=&v"(eb)
                      : "v"(pos), "i"(LDS_B));
@@ -676,17 +696,18 @@ __device__ __forceinline__ void box_step(Trav& t, const Ray& r, const float4 ea,
 // running bound `closest` = the closest hit so far (bvh.go:227-232).
 // QUADS: the scene holds quads (a third entry kind); false compiles the sphere-only step.
 // FIXED: E is v3's LDS layout at LDS address 0 (scene_ref_fixed).
-template <bool COUNT, bool QUADS = false, bool FIXED = false>
+template <bool COUNT, bool QUADS = false, bool FIXED = false, bool HYB = false>
 __device__ __forceinline__ void trav_step(Trav& t, const Ray& r, const SceneRef E, Counters& cnt) {
     float4 ea, eb;
-    load_entry<FIXED>(E, t.i, ea, eb);
+    load_entry<FIXED, HYB>(E, t.i, ea, eb);
+    if (COUNT && HYB && t.i < E.hot) ++cnt.cache_hits;
     const int32_t tag = __float_as_int(eb.w);  // device recoding, rtx_layout.h
     if (tag >= 0) {  // a node (or the sentinel)
         box_step<COUNT>(t, r, ea, eb, tag, cnt);
     } else {
         if (QUADS && tag == RTX_E_QUAD) quad_test<COUNT>(t, r, E, ea, eb, t.i, cnt);
         else sphere_test<COUNT>(t, r, ea, eb, t.i, cnt);
-        t.i += 16;
+        t.i = (uint32_t)__float_as_int(eb.z);  // the primitive's successor
     }
 }
 

@@ -33,6 +33,7 @@ __device__ __forceinline__ void flush_counters(const Params& p, uint64_t samples
     atomicAdd(&p.counters[4], (unsigned long long)cnt.hits);
     atomicAdd(&p.counters[5], (unsigned long long)cnt.texel_fetches);
     atomicAdd(&p.counters[6], (unsigned long long)cnt.draws);
+    if (cnt.cache_hits) atomicAdd(&p.counters[15], (unsigned long long)cnt.cache_hits);
 }
 
 __device__ __forceinline__ void flush_sched(const Params& p, uint64_t wi, uint64_t ls, uint64_t sp, uint64_t sl) {
@@ -94,7 +95,7 @@ __global__ __launch_bounds__(BLOCK) void render_pixels(Params p) {
 // STEPS > 1 takes up to STEPS entries per lane between two wave votes.  (A branch-free
 // step that evaluates the box and the sphere test on every lane measured 8 % slower:
 // most waves hold only box entries at a step, and the branch skips the sphere test.)
-template <bool COUNT, int STEPS = 1, bool QUADS = false, bool FIXED = false>
+template <bool COUNT, int STEPS = 1, bool QUADS = false, bool FIXED = false, bool HYB = false>
 __device__ __forceinline__ void traverse_phase(uint32_t& mode, Trav& t, const Ray& r, const SceneRef E,
                                                uint32_t n_entries, uint32_t thresh, Counters& cnt,
                                                uint64_t& wave_iters, uint64_t& lane_steps, uint64_t& shade_phases,
@@ -104,7 +105,7 @@ __device__ __forceinline__ void traverse_phase(uint32_t& mode, Trav& t, const Ra
         // sentinel, t.i = 16 * n_entries, where a step changes nothing — cheaper than masking
         // the wave per step.
 #pragma unroll
-        for (int s = 0; s < STEPS; ++s) trav_step<COUNT, QUADS, FIXED>(t, r, E, cnt);
+        for (int s = 0; s < STEPS; ++s) trav_step<COUNT, QUADS, FIXED, HYB>(t, r, E, cnt);
         if (mode == 0 && t.i >= 16 * n_entries) mode = 1;
         const uint64_t trav = __ballot(mode == 0);
         const uint64_t pend = __ballot(mode == 1 || mode == 2);
@@ -310,7 +311,7 @@ __global__ __launch_bounds__(64 * WX * WY, MINW) void render_wave(Params p) {
 // Samples beyond the scratch budget run in chunks [k0, k0 + kn); the running sum of a
 // pixel is carried in the output between chunks.
 // ------------------------------------------------------------------------------------
-template <bool COUNT, bool USE_LDS, bool QUADS, bool NOISE, int WAVES = 8, int MINW = 0>
+template <bool COUNT, bool USE_LDS, bool QUADS, bool NOISE, int WAVES = 8, int MINW = 0, bool HYB = false>
 __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
     constexpr uint32_t WAVE_BLOCK = 64 * WAVES, STEPS = 8;  // walk steps between two wave votes (A/B: 3 +2.2 %, 5 +0.9 %, 12 +1.3 %)
     extern __shared__ float4 lds_entries[];
@@ -331,6 +332,17 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
         E = scene_ref_fixed(lds_entries, p.n_entries, p.n_quads, p.n_materials);
     } else {
         E = scene_ref(p.entries, p.n_entries, p.materials);
+        if constexpr (HYB) {  // the scene's top levels, stored first, cached in LDS (fixed layout)
+            const uint32_t m = p.n_entries + 1;
+            for (uint32_t t = threadIdx.x; t < p.n_hot; t += WAVE_BLOCK) {
+                lds_entries[t] = p.entries[t];
+                lds_entries[LDS_B / 16 + t] = p.entries[m + t];
+            }
+            __syncthreads();
+            E.la = lds_entries;
+            E.lb = lds_entries + LDS_B / 16;
+            E.hot = 16 * p.n_hot;
+        }
     }
     const uint32_t n_entries = p.n_entries;
     const uint32_t thresh = p.shade_thresh;
@@ -368,7 +380,7 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
 
     for (;;) {
         if (COUNT) clk = __builtin_amdgcn_s_memtime();
-        traverse_phase<COUNT, STEPS, QUADS, USE_LDS>(mode, t, r, E, n_entries, thresh, cnt, wave_iters, lane_steps,
+        traverse_phase<COUNT, STEPS, QUADS, USE_LDS, HYB>(mode, t, r, E, n_entries, thresh, cnt, wave_iters, lane_steps,
                                             shade_phases, shade_lanes, idle_lanes);
         if (COUNT) {
             const uint64_t now = __builtin_amdgcn_s_memtime();
@@ -779,9 +791,14 @@ hipError_t launch_wave(const Params& p, uint32_t geom, bool use_lds, hipStream_t
 // resident-capacity grid of render_items and summed into p.out by reduce_samples.
 template <bool COUNT, bool QUADS, bool NOISE, int WAVES = 8, int MINW = 0>
 hipError_t launch_items(Params p, bool use_lds, hipStream_t stream) {
-    const size_t shmem = use_lds ? lds_fixed_bytes(p.n_entries, p.n_quads, p.n_materials) : 0;
+    // a scene too big for LDS: its top levels (p.n_hot entries) cached in LDS when the
+    // device layout stored them first (RTX_HOT_ENTRIES=0 turns that off)
+    const bool hyb = !use_lds && p.n_hot > 0 && !NOISE;
+    const size_t shmem = use_lds ? lds_fixed_bytes(p.n_entries, p.n_quads, p.n_materials)
+                                 : (hyb ? lds_hot_bytes(p.n_hot) : 0);
     const auto kern = use_lds ? render_items<COUNT, true, QUADS, NOISE, WAVES, MINW>
-                              : render_items<COUNT, false, QUADS, NOISE, WAVES, MINW>;
+                              : (hyb ? render_items<COUNT, false, QUADS, NOISE, WAVES, MINW, !NOISE>
+                                     : render_items<COUNT, false, QUADS, NOISE, WAVES, MINW>);
     constexpr int block = 64 * WAVES;
     int dev = 0, cus = 0, per_cu = 0;
     hipError_t e = hipGetDevice(&dev);

@@ -30,9 +30,12 @@
 // a wave's gathers spread over every LDS bank group, and the integer words are recoded
 // so that a step needs no index arithmetic (rtx_capi.hip, ensure_device):
 //   positions are byte offsets, 16 * index (rtxd::Trav::i);
-//   node:   a.w = escape position, b.w = next position 16 * (i + 1)  (b.w >= 0 <=> node)
-//   sphere: b.w = RTX_DEV_SPHERE(material) = -3 - material
-//   quad:   b.w = RTX_E_QUAD
+//   node:   a.w = escape position, b.w = next position  (b.w >= 0 <=> node)
+//   sphere: b.z = next position, b.w = RTX_DEV_SPHERE(material) = -3 - material
+//   quad:   b.z = next position, b.w = RTX_E_QUAD
+// Since every entry names its successor, the storage order is free: it is the walk order,
+// except that a scene too big for the LDS copy stores its top levels first (v3 caches those
+// in LDS; ensure_device).  The walk order, and so every test and its result, is unchanged.
 // Each array ends with one extra entry, the sentinel at index n: a node with an empty
 // box whose escape and next are both its own position.  Every walk ends there and a
 // step on it changes nothing, whatever the ray (NaN included), so lanes that are not

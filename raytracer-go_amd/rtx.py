@@ -99,7 +99,7 @@ class Stats(ctypes.Structure):
                 ("rng_draws", c_uint64), ("kernel_ms", c_double), ("gather_ms", c_double),
                 ("wave_iters", c_uint64), ("lane_steps", c_uint64), ("shade_phases", c_uint64),
                 ("shade_lanes", c_uint64), ("trav_cycles", c_uint64), ("shade_cycles", c_uint64),
-                ("idle_lanes", c_uint64)]
+                ("idle_lanes", c_uint64), ("cache_hits", c_uint64)]
 
     def as_dict(self) -> dict:
         return {name: getattr(self, name) for name, _ in self._fields_}

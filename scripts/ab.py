@@ -79,6 +79,9 @@ for n in names:
 setenv("")
 for n in names:
     c = dev.render_region(cam, 1, reg, outs[n].data_ptr(), stream, counters=True, timed=True, flags=VARIANTS[n])
+    if c.cache_hits:
+        print(f"{n:8s} LDS-cache hits {c.cache_hits / (c.node_visits + c.prim_tests):.3f} of the entries read "
+              f"(node visits + primitive tests {(c.node_visits + c.prim_tests) / c.segments:.1f} per segment)", flush=True)
     if c.wave_iters:
         print(f"{n:8s} trav-lane util {c.lane_steps / (64 * c.wave_iters):.3f}  iters/segment(wave) "
               f"{c.wave_iters * 64 / c.segments:.1f}  entries/segment {(c.node_visits + c.prim_tests) / c.segments:.1f}"
