@@ -764,6 +764,13 @@ __device__ __forceinline__ bool shade(const Params& p, const SceneRef E, const T
         }
     }
     if (!front) n = scale(n, -1.0f);                            // hittables.go:24-26
+    // Metal and Dielectric both start from Unit(dir) and its mirror direction: computed once,
+    // so a wave holding both materials runs the sqrt, divide and reflect once, not twice.
+    V3 ud = v3(0.0f, 0.0f, 0.0f), mirror = ud;
+    if (m.type == RTX_MAT_METAL || m.type == RTX_MAT_DIELECTRIC) {
+        ud = unit(r.d);                                         // materials.go:61, 96
+        mirror = reflect(ud, n);                                // materials.go:62, 108
+    }
 
     if (m.type == RTX_MAT_LAMBERTIAN || m.type == RTX_MAT_METAL) {
         uint32_t draws = 0;
@@ -784,7 +791,7 @@ __device__ __forceinline__ bool shade(const Params& p, const SceneRef E, const T
             r = Ray{pt, dir};
             return false;
         }
-        const V3 refl = reflect(unit(r.d), n);                  // materials.go:60-75
+        const V3 refl = mirror;                                 // materials.go:60-75
         const V3 sc = add(refl, scale(s, m.fuzz));
         if (!(dot(sc, n) > 0.0f)) {                             // absorbed: Emit() = 0
             color = acc;
@@ -796,7 +803,6 @@ __device__ __forceinline__ bool shade(const Params& p, const SceneRef E, const T
     }
     if (m.type == RTX_MAT_DIELECTRIC) {                         // materials.go:91-113
         const float eta = front ? 1.0f / m.ior : m.ior;
-        const V3 ud = unit(r.d);
         const float d = dot(scale(ud, -1.0f), n);
         const float cos_t = d < 1.0f ? d : (d != d ? d : 1.0f); // float32(math.Min(float64(d), 1))
         const float sin_t = (float)__builtin_sqrt(1.0 - (double)(cos_t * cos_t));
@@ -808,7 +814,7 @@ __device__ __forceinline__ bool shade(const Params& p, const SceneRef E, const T
             refl = rf > unit_f32(b0.x);
             if (COUNT) cnt.draws += 1;
         }
-        r = Ray{pt, refl ? reflect(ud, n) : refract(ud, n, eta)};  // attenuation (1,1,1)
+        r = Ray{pt, refl ? mirror : refract(ud, n, eta)};          // attenuation (1,1,1)
         return false;
     }
     // DiffuseLight: emit, never scatters (materials.go:303-313)
