@@ -40,6 +40,7 @@ def parse():
     ap.add_argument("--cpu-target-s", type=float, default=15.0, help="CPU baseline budget (seconds)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
+    ap.add_argument("--valu", default=os.path.join(ROOT, "profiles", "valu_r01.json"))
     return ap.parse_args()
 
 
@@ -164,6 +165,13 @@ def main():
                 tr = json.load(f)
             if tr.get("workload") == f"{args.scene}:{W}x{H}x{cam.samples_per_pixel}" and world == 1:
                 traffic = tr.get("hbm_bytes_per_launch")
+        valu = None  # the kernel's actual bound: VALU issue, from the committed PMC pass (scripts/pmc_valu.py)
+        if os.path.exists(args.valu):
+            with open(args.valu) as f:
+                vr = json.load(f)
+            if vr.get("workload") == f"{args.scene}:{W}x{H}x{cam.samples_per_pixel}" and world == 1:
+                valu = {"issue_frac": vr["valu_issue_frac"], "lane_frac": vr["valu_lane_frac"],
+                        "source": "profiles/valu_r01.json (rocprofv3 PMC of the same launch)"}
         headline = args.scene == "random_spheres" and (W, H, cam.samples_per_pixel) == (1920, 1080, 500)
         metric = ("Mray/s on 1920x1080x500spp random-spheres; achieved HBM GB/s vs peak" if headline else
                   f"Mray/s on {W}x{H}x{cam.samples_per_pixel}spp {args.scene} (not the headline config)")
@@ -202,7 +210,9 @@ def main():
                 "traffic": traffic,
                 "alg_bytes_per_launch": launch_bytes,
                 "note": "algorithmic bytes (SURVEY §8d) of rank 0's launch / its HIP-event time; the 32 KB "
-                        "scene is LDS-resident, so real HBM traffic (PMC: the v3 sample scratch) is ~300x lower",
+                        "scene is LDS-resident, so real HBM traffic (PMC: the v3 sample scratch) is ~300x lower "
+                        "and the kernel is bound by VALU issue instead (valu)",
+                "valu": valu,
             },
         }
         if world == 1 and not args.no_cpu:

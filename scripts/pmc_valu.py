@@ -1,0 +1,46 @@
+#!/usr/bin/env python3
+"""VALU issue utilisation of the bench kernel from rocprofv3 --pmc passes.
+
+  python scripts/pmc_valu.py <pmc_dir> <out.json> --workload random_spheres:1920x1080x500
+
+The render is VALU-issue bound, so this is its meaningful roofline:
+SQ_INSTS_VALU wave64 instructions x 2 issue cycles each per SIMD, over the SIMD-cycles of
+the launch (GRBM_GUI_ACTIVE is summed over the 8 XCDs: / 8 = shader clocks; x 1024 SIMDs).
+"""
+import argparse
+import csv
+import glob
+import json
+import os
+
+ap = argparse.ArgumentParser()
+ap.add_argument("pmc_dir")
+ap.add_argument("out")
+ap.add_argument("--workload", required=True)
+ap.add_argument("--kernel", default="render_items<false")
+ap.add_argument("--simds", type=int, default=1024)
+args = ap.parse_args()
+
+vals = {}
+for f in glob.glob(os.path.join(args.pmc_dir, "**", "*counter_collection.csv"), recursive=True):
+    with open(f) as fh:
+        for r in csv.DictReader(fh):
+            if args.kernel in r["Kernel_Name"]:
+                vals.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
+need = ["SQ_INSTS_VALU", "GRBM_GUI_ACTIVE", "SQ_THREAD_CYCLES_VALU"]
+assert all(k in vals for k in need), f"missing {need} for {args.kernel} under {args.pmc_dir}"
+insts = vals["SQ_INSTS_VALU"][0]
+cycles = vals["GRBM_GUI_ACTIVE"][0] / 8.0
+out = {
+    "workload": args.workload,
+    "kernel": args.kernel,
+    "valu_insts_per_launch": insts,
+    "shader_cycles_per_launch": cycles,
+    "valu_issue_frac": round(insts * 2.0 / (cycles * args.simds), 4),
+    "valu_lane_frac": round(vals["SQ_THREAD_CYCLES_VALU"][0] / (64.0 * insts), 4),
+    "method": "rocprofv3 --kernel-trace --pmc SQ_INSTS_VALU SQ_THREAD_CYCLES_VALU GRBM_GUI_ACTIVE ...; "
+              "issue frac = 2 cycles x SQ_INSTS_VALU / (GRBM_GUI_ACTIVE / 8 XCDs x 1024 SIMDs)",
+}
+with open(args.out, "w") as f:
+    json.dump(out, f, indent=1)
+print(json.dumps(out))
