@@ -333,6 +333,7 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
     } else {
         E = scene_ref(p.entries, p.n_entries, p.materials);
         if constexpr (HYB) {  // the scene's top levels, stored first, cached in LDS (fixed layout)
+            if ((uint32_t)(uintptr_t)(__attribute__((address_space(3))) float4*)lds_entries != 0u) __builtin_trap();
             const uint32_t m = p.n_entries + 1;
             for (uint32_t t = threadIdx.x; t < p.n_hot; t += WAVE_BLOCK) {
                 lds_entries[t] = p.entries[t];
