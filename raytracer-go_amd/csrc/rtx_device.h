@@ -361,10 +361,12 @@ __device__ __forceinline__ SceneRef scene_ref_fixed(const float4* lds, uint32_t 
                     reinterpret_cast<const rtx_material*>(lds + lds_mat_offset(n_entries, n_quads, n_mats) / 16),
                     nullptr, nullptr, 0u};
 }
-// The LDS cache of a scene too big for the fixed layout: its first HOT_ENTRIES_MAX entries
-// (the top levels, rtx_capi.hip ensure_device) in the fixed layout's places, 52 KB per
-// workgroup, so three 8-wave workgroups still share a CU.
-constexpr uint32_t HOT_ENTRIES_MAX = 1280;
+// The LDS cache of a scene too big for the fixed layout: its first entries (whole top
+// levels, rtx_capi.hip ensure_device) in the fixed layout's places.  Up to HOT_ENTRIES_8W
+// (52 KB) three 8-wave workgroups share a CU; up to HOT_ENTRIES_MAX (64 KB, the workgroup
+// limit) two 12-wave ones do — 6 waves per SIMD either way.
+constexpr uint32_t HOT_ENTRIES_8W = 1280;
+constexpr uint32_t HOT_ENTRIES_MAX = 2048;
 __host__ __device__ __forceinline__ uint32_t lds_hot_bytes(uint32_t n_hot) { return LDS_B + n_hot * 16; }
 // float4s of a scene's device table: both halves with their sentinels, then the quads.
 __host__ __device__ __forceinline__ uint32_t scene_float4s(uint32_t n_entries, uint32_t n_quads) {

@@ -850,6 +850,9 @@ hipError_t launch_items_for(const Params& p, bool use_lds, hipStream_t stream) {
         return p.n_quads ? launch_items<COUNT, true, false, 4>(p, use_lds, stream)
                          : launch_items<COUNT, false, false, 4>(p, use_lds, stream);
     // 6 waves per SIMD: at most 80 VGPRs (the allocation granule is 8)
+    if (!use_lds && p.n_hot > HOT_ENTRIES_8W)  // a 64 KB LDS cache: 12-wave workgroups, two per CU
+        return p.n_quads ? launch_items<COUNT, true, false, 12, COUNT ? 0 : 6>(p, use_lds, stream)
+                         : launch_items<COUNT, false, false, 12, COUNT ? 0 : 6>(p, use_lds, stream);
     return p.n_quads ? launch_items<COUNT, true, false, 8, COUNT ? 0 : 6>(p, use_lds, stream)
                      : launch_items<COUNT, false, false, 8, COUNT ? 0 : 6>(p, use_lds, stream);
 }
