@@ -416,6 +416,10 @@ struct Counters {
 };
 
 // GetRay + sampleUnitSquare, camera.go:265-299, event 0.  base = (pixel00 + du*i) + dv*j.
+// SKIP_DISK: without defocus the unit-disk sample is drawn but never used (camera.go:279-281)
+// and no later draw depends on it (every event has its own Philox blocks), so a kernel that
+// does not count draws may leave its rejection loop out (Cornell box -1.7 %).
+template <bool SKIP_DISK = false>
 __device__ __forceinline__ Ray camera_ray(const rtx_camera& c, V3 base, const PathRng& rng, uint32_t& draws) {
     U4 b = rng.block(0, 0);
     const V3 du = v3(c.pixel_du[0], c.pixel_du[1], c.pixel_du[2]);
@@ -425,7 +429,7 @@ __device__ __forceinline__ Ray camera_ray(const rtx_camera& c, V3 base, const Pa
     const V3 pc = add(base, add(scale(du, dx), scale(dv, dy)));   // :275
     float x = signed_unit(b.z), y = signed_unit(b.w);             // :277 disk, always drawn
     draws += 4;
-    for (uint32_t a = 1; !(x * x + y * y < 1.0f); ++a) {          // vec3.go:203-210
+    for (uint32_t a = 1; !(SKIP_DISK && !(c.defocus_angle > 0.0f)) && !(x * x + y * y < 1.0f); ++a) {  // vec3.go:203-210
         b = rng.block(0, a);
         x = signed_unit(b.x);
         y = signed_unit(b.y);

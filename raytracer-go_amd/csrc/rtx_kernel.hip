@@ -448,7 +448,7 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
             const uint32_t taken = (uint32_t)__popcll(wm);
             cursor = cursor + taken > u_items ? u_items : cursor + taken;
             if (got) {
-                r = camera_ray(c, base, rng, cnt.draws);  // GetRay, camera.go:257
+                r = camera_ray<!COUNT>(c, base, rng, cnt.draws);  // GetRay, camera.go:257
                 thr = v3(1.0f, 1.0f, 1.0f);
                 acc = v3(0.0f, 0.0f, 0.0f);
                 seg = 0;
