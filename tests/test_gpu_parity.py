@@ -301,3 +301,23 @@ def test_full_frame_bitwise(torch_cuda, built, scene, width, spp):
     reg = rtx.Region(0, 0, cam.image_width, cam.image_height, 0, 1)
     gpu, st = gpu_region(torch_cuda, dev, cam, 23, reg)
     check_parity(gpu, s.desc, cam, 23, reg, st)
+
+
+@pytest.mark.parametrize("hot", ["0", "1", "1280", "2048"])
+def test_stress_100k_lds_cache(torch_cuda, built, monkeypatch, hot):
+    """Config 4 with its top BVH levels stored first and cached in LDS (RTX_HOT_ENTRIES, read at
+    upload): none, the root only, 8-wave and 12-wave workgroups.  The timed kernel's image is
+    the oracle's bit for bit, and the counting kernel reports the cache hits."""
+    monkeypatch.setenv("RTX_HOT_ENTRIES", hot)
+    scene = rtx.HostScene("stress_100k", 1)
+    dev = rtx.DeviceScene(scene.desc)
+    cam = scene.camera(width=1920, spp=2, depth=50)
+    reg = rtx.Region(700, 380, 40, 24, 0, 1)
+    gpu, _ = gpu_region(torch_cuda, dev, cam, 13, reg, counters=False)
+    it, _ = ob.render(scene.desc, cam, 13, reg, ob.ORDER_ITERATIVE)
+    assert np.array_equal(gpu, it)
+    _, st = gpu_region(torch_cuda, dev, cam, 13, reg, counters=True)
+    if hot == "0":
+        assert st.cache_hits == 0
+    else:
+        assert 0 < st.cache_hits < st.node_visits + st.prim_tests
