@@ -714,7 +714,8 @@ __device__ __forceinline__ void trav_step(Trav& t, const Ray& r, const SceneRef 
     load_entry<FIXED, HYB>(E, t.i, ea, eb);
     if (COUNT && HYB && t.i < E.hot) ++cnt.cache_hits;
     const int32_t tag = __float_as_int(eb.w);  // device recoding, rtx_layout.h
-    if (tag >= 0) {  // a node (or the sentinel)
+    // (tag > -2, not tag >= 0: a sign test became a 64-bit compare of eb.z:eb.w)
+    if (tag > -2) {  // a node (or the sentinel)
         box_step<COUNT>(t, r, ea, eb, tag, cnt);
     } else {
         if (QUADS && tag == RTX_E_QUAD) quad_test<COUNT>(t, r, E, ea, eb, t.i, cnt);
