@@ -404,6 +404,7 @@ struct Params {
     uint32_t k0, kn, sub;
     uint32_t item_waves;  // v3 waves per workgroup: 8 (one LDS scene copy each), or 4 for A/B
     uint32_t n_hot;       // entries stored first and cached in LDS by v3 when the scene does not fit
+    uint32_t prim_batch;  // v3: primitive tests wait for this many lanes (trav_step_batched); 0 = off
 };
 
 struct Ray {
@@ -721,6 +722,35 @@ __device__ __forceinline__ void trav_step(Trav& t, const Ray& r, const SceneRef 
         if (QUADS && tag == RTX_E_QUAD) quad_test<COUNT>(t, r, E, ea, eb, t.i, cnt);
         else sphere_test<COUNT>(t, r, ea, eb, t.i, cnt);
         t.i = (uint32_t)__float_as_int(eb.z);  // the primitive's successor
+    }
+}
+
+// The walk step with primitive batching (v3, RTX_PRIM_BATCH = kmin > 0): every lane reads its
+// entry, then the wave runs EITHER the box tests of its lanes on nodes OR the primitive tests of
+// its lanes on primitives — the primitive tests once at least `kmin` lanes wait on one (or no
+// lane has a node to test).  Lanes of the other kind keep their position and read the entry
+// again next step.  Each lane still takes the reference's steps in the reference's order with
+// the current bound, so every result is unchanged; the wave no longer pays both paths in the
+// ~75 % of steps where a few lanes sit on primitives.
+template <bool COUNT, bool QUADS, bool FIXED, bool HYB>
+__device__ __forceinline__ void trav_step_batched(Trav& t, const Ray& r, const SceneRef E, Counters& cnt,
+                                                  uint32_t end, uint32_t kmin) {
+    float4 ea, eb;
+    load_entry<FIXED, HYB>(E, t.i, ea, eb);
+    const int32_t tag = __float_as_int(eb.w);
+    const bool prim = tag < -1;
+    const uint64_t pm = __ballot(prim);
+    const uint64_t bm = __ballot(!prim && t.i < end);
+    if ((uint32_t)__popcll(pm) >= kmin || bm == 0) {
+        if (prim) {
+            if (COUNT && HYB && t.i < E.hot) ++cnt.cache_hits;
+            if (QUADS && tag == RTX_E_QUAD) quad_test<COUNT>(t, r, E, ea, eb, t.i, cnt);
+            else sphere_test<COUNT>(t, r, ea, eb, t.i, cnt);
+            t.i = (uint32_t)__float_as_int(eb.z);
+        }
+    } else if (!prim) {
+        if (COUNT && HYB && t.i < E.hot && t.i < end) ++cnt.cache_hits;
+        box_step<COUNT>(t, r, ea, eb, tag, cnt);
     }
 }
 

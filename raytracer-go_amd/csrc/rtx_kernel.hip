@@ -95,17 +95,23 @@ __global__ __launch_bounds__(BLOCK) void render_pixels(Params p) {
 // STEPS > 1 takes up to STEPS entries per lane between two wave votes.  (A branch-free
 // step that evaluates the box and the sphere test on every lane measured 8 % slower:
 // most waves hold only box entries at a step, and the branch skips the sphere test.)
-template <bool COUNT, int STEPS = 1, bool QUADS = false, bool FIXED = false, bool HYB = false>
+template <bool COUNT, int STEPS = 1, bool QUADS = false, bool FIXED = false, bool HYB = false, bool BATCH = false>
 __device__ __forceinline__ void traverse_phase(uint32_t& mode, Trav& t, const Ray& r, const SceneRef E,
                                                uint32_t n_entries, uint32_t thresh, Counters& cnt,
                                                uint64_t& wave_iters, uint64_t& lane_steps, uint64_t& shade_phases,
-                                               uint64_t& shade_lanes, uint64_t& idle_lanes) {
+                                               uint64_t& shade_lanes, uint64_t& idle_lanes, uint32_t prim_batch = 0) {
     for (;;) {
         // Every lane steps: one that is not traversing (or finishes early) waits on the
         // sentinel, t.i = 16 * n_entries, where a step changes nothing — cheaper than masking
         // the wave per step.
+        if constexpr (BATCH) {
 #pragma unroll
-        for (int s = 0; s < STEPS; ++s) trav_step<COUNT, QUADS, FIXED, HYB>(t, r, E, cnt);
+            for (int s = 0; s < STEPS; ++s)
+                trav_step_batched<COUNT, QUADS, FIXED, HYB>(t, r, E, cnt, 16 * n_entries, prim_batch);
+        } else {
+#pragma unroll
+            for (int s = 0; s < STEPS; ++s) trav_step<COUNT, QUADS, FIXED, HYB>(t, r, E, cnt);
+        }
         if (mode == 0 && t.i >= 16 * n_entries) mode = 1;
         const uint64_t trav = __ballot(mode == 0);
         const uint64_t pend = __ballot(mode == 1 || mode == 2);
@@ -381,8 +387,9 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
 
     for (;;) {
         if (COUNT) clk = __builtin_amdgcn_s_memtime();
-        traverse_phase<COUNT, STEPS, QUADS, USE_LDS, HYB>(mode, t, r, E, n_entries, thresh, cnt, wave_iters, lane_steps,
-                                            shade_phases, shade_lanes, idle_lanes);
+        traverse_phase<COUNT, STEPS, QUADS, USE_LDS, HYB, true>(mode, t, r, E, n_entries, thresh, cnt, wave_iters,
+                                                              lane_steps, shade_phases, shade_lanes, idle_lanes,
+                                                              p.prim_batch);
         if (COUNT) {
             const uint64_t now = __builtin_amdgcn_s_memtime();
             trav_cycles += now - clk;
