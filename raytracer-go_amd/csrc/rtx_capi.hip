@@ -325,12 +325,13 @@ uint32_t env_knob(const char* name, long dflt, long lo, long hi) {
     return (uint32_t)(x < lo ? lo : (x > hi ? hi : x));
 }
 
-// Lanes of a wave that wait before it shades (v1-v3); RTX_SHADE_THRESH.  52 measured
-// best for v3 at the headline config (48 for v1).
+// Lanes of a wave that wait before it shades (v1-v3); RTX_SHADE_THRESH.  48 measured
+// best for v3 at the headline config with primitive batching (44 the same, 40 +1.3 %,
+// 56 +4.6 %) and for v1.
 uint32_t shade_thresh() {
     static const uint32_t v = [] {
         const char* e = std::getenv("RTX_SHADE_THRESH");
-        const long x = e ? std::strtol(e, nullptr, 10) : 52;
+        const long x = e ? std::strtol(e, nullptr, 10) : 48;
         return (uint32_t)(x < 1 ? 1 : (x > 64 ? 64 : x));
     }();
     return v;

@@ -319,7 +319,7 @@ __global__ __launch_bounds__(64 * WX * WY, MINW) void render_wave(Params p) {
 // ------------------------------------------------------------------------------------
 template <bool COUNT, bool USE_LDS, bool QUADS, bool NOISE, int WAVES = 8, int MINW = 0, bool HYB = false>
 __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
-    constexpr uint32_t WAVE_BLOCK = 64 * WAVES, STEPS = 8;  // walk steps between two wave votes (A/B: 3 +2.2 %, 5 +0.9 %, 12 +1.3 %)
+    constexpr uint32_t WAVE_BLOCK = 64 * WAVES, STEPS = 6;  // walk steps between two wave votes (A/B with primitive batching: 4 +0.7 %, 8 +0.8 %, 12 +1.3 %)
     extern __shared__ float4 lds_entries[];
     SceneRef E;
     if constexpr (USE_LDS) {

@@ -20,7 +20,7 @@ VARIANTS = {"v3": 0, "v1": V1, "v2": POOL, "v0": rtx.RTX_FLAG_KERNEL_V0, "nolds"
             "v1nolds": V1 | rtx.RTX_FLAG_NO_LDS, "p4": POOL | 16}
 for _g in range(8):
     VARIANTS[f"g{_g}"] = V1 | rtx.RTX_FLAG_WAVE_GEOM(_g)
-for _t in (1, 4, 8, 12, 16, 20, 24, 32, 40, 44, 48, 52, 56, 60, 64):
+for _t in range(1, 65):
     VARIANTS[f"t{_t}"] = _t << 8  # RTX_FLAG_SHADE_THRESH (default schedule)
     VARIANTS[f"v2t{_t}"] = (_t << 8) | POOL
 
