@@ -387,7 +387,9 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
 
     for (;;) {
         if (COUNT) clk = __builtin_amdgcn_s_memtime();
-        traverse_phase<COUNT, STEPS, QUADS, USE_LDS, HYB, true>(mode, t, r, E, n_entries, thresh, cnt, wave_iters,
+        // primitive batching only for a scene in LDS: a lane that waits re-reads its entry, which
+        // from HBM cost config 4 +34 %
+        traverse_phase<COUNT, STEPS, QUADS, USE_LDS, HYB, USE_LDS>(mode, t, r, E, n_entries, thresh, cnt, wave_iters,
                                                               lane_steps, shade_phases, shade_lanes, idle_lanes,
                                                               p.prim_batch);
         if (COUNT) {
