@@ -851,6 +851,11 @@ bool uses_items(const Params& p, uint32_t flags) {
     return work;
 }
 
+#ifndef RTX_V3_WAVES  // workgroup size and waves per SIMD of the default v3 kernel (A/B builds override)
+#define RTX_V3_WAVES 8
+#define RTX_V3_MINW 6
+#endif
+
 template <bool COUNT>
 hipError_t launch_items_for(const Params& p, bool use_lds, hipStream_t stream) {
     if (p.has_noise) return p.n_quads ? launch_items<COUNT, true, true>(p, use_lds, stream)
@@ -862,8 +867,8 @@ hipError_t launch_items_for(const Params& p, bool use_lds, hipStream_t stream) {
     if (!use_lds && p.n_hot > HOT_ENTRIES_8W)  // a 64 KB LDS cache: 12-wave workgroups, two per CU
         return p.n_quads ? launch_items<COUNT, true, false, 12, COUNT ? 0 : 6>(p, use_lds, stream)
                          : launch_items<COUNT, false, false, 12, COUNT ? 0 : 6>(p, use_lds, stream);
-    return p.n_quads ? launch_items<COUNT, true, false, 8, COUNT ? 0 : 6>(p, use_lds, stream)
-                     : launch_items<COUNT, false, false, 8, COUNT ? 0 : 6>(p, use_lds, stream);
+    return p.n_quads ? launch_items<COUNT, true, false, RTX_V3_WAVES, COUNT ? 0 : RTX_V3_MINW>(p, use_lds, stream)
+                     : launch_items<COUNT, false, false, RTX_V3_WAVES, COUNT ? 0 : RTX_V3_MINW>(p, use_lds, stream);
 }
 
 hipError_t launch_render(const Params& p, uint32_t flags, hipStream_t stream) {
