@@ -89,6 +89,23 @@ def cpu_baseline(scene, cam, seed: int, target_s: float) -> dict:
     }
 
 
+def schedule(st: dict) -> dict:
+    """Wave-schedule counters of rank 0's untimed counting launch (same decisions as the timed
+    kernel): traversal active-lane fraction, lanes idle for want of work, shading's share of
+    wave cycles and, for scenes too big for the LDS copy, the LDS-cache hit rate."""
+    out = {}
+    if st.get("wave_iters"):
+        it = 64.0 * st["wave_iters"]
+        out["trav_lane_util"] = round(st["lane_steps"] / it, 4)
+        out["idle_lane_frac"] = round(st["idle_lanes"] / it, 4)
+        cyc = st["trav_cycles"] + st["shade_cycles"]
+        out["shade_cycle_share"] = round(st["shade_cycles"] / cyc, 4) if cyc else None
+    reads = st.get("node_visits", 0) + st.get("prim_tests", 0)
+    if st.get("cache_hits") and reads:
+        out["lds_cache_hit_frac"] = round(st["cache_hits"] / reads, 4)
+    return out
+
+
 def main():
     args = parse()
     import torch
@@ -201,6 +218,7 @@ def main():
             "segments_per_sample": round(tot["segments"] / tot["samples"], 4),
             "node_visits_per_segment": round(tot["node_visits"] / tot["segments"], 3),
             "kernel_ms_avg": round(avg_kernel_s * 1e3, 3),
+            "schedule": schedule(st),
             "roofline": {
                 "bound": "hbm",
                 "achieved": round(achieved, 2),

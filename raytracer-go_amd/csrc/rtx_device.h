@@ -404,6 +404,7 @@ struct Params {
     uint32_t k0, kn, sub;
     uint32_t item_waves;  // v3 waves per workgroup: 8 (one LDS scene copy each), or 4 for A/B
     uint32_t n_hot;       // entries stored first and cached in LDS by v3 when the scene does not fit
+    uint32_t grid_pct;    // v3: percent of the resident grid launched (A/B knob; 100 = all resident waves)
     uint32_t prim_batch;  // v3: primitive tests wait for this many lanes (trav_step_batched); 0 = off
 };
 
@@ -732,16 +733,18 @@ __device__ __forceinline__ void trav_step(Trav& t, const Ray& r, const SceneRef 
 // again next step.  Each lane still takes the reference's steps in the reference's order with
 // the current bound, so every result is unchanged; the wave no longer pays both paths in the
 // ~75 % of steps where a few lanes sit on primitives.
+// Returns (COUNT only) the lanes whose entry the step processed, wave-uniform.
 template <bool COUNT, bool QUADS, bool FIXED, bool HYB>
-__device__ __forceinline__ void trav_step_batched(Trav& t, const Ray& r, const SceneRef E, Counters& cnt,
-                                                  uint32_t end, uint32_t kmin) {
+__device__ __forceinline__ uint32_t trav_step_batched(Trav& t, const Ray& r, const SceneRef E, Counters& cnt,
+                                                      uint32_t end, uint32_t kmin) {
     float4 ea, eb;
     load_entry<FIXED, HYB>(E, t.i, ea, eb);
     const int32_t tag = __float_as_int(eb.w);
     const bool prim = tag < -1;
     const uint64_t pm = __ballot(prim);
     const uint64_t bm = __ballot(!prim && t.i < end);
-    if ((uint32_t)__popcll(pm) >= kmin || bm == 0) {
+    const bool prims = (uint32_t)__popcll(pm) >= kmin || bm == 0;
+    if (prims) {
         if (prim) {
             if (COUNT && HYB && t.i < E.hot) ++cnt.cache_hits;
             if (QUADS && tag == RTX_E_QUAD) quad_test<COUNT>(t, r, E, ea, eb, t.i, cnt);
@@ -752,6 +755,7 @@ __device__ __forceinline__ void trav_step_batched(Trav& t, const Ray& r, const S
         if (COUNT && HYB && t.i < E.hot && t.i < end) ++cnt.cache_hits;
         box_step<COUNT>(t, r, ea, eb, tag, cnt);
     }
+    return COUNT ? (uint32_t)__popcll(prims ? pm : bm) : 0u;
 }
 
 // Shade the result of segment `seg` (ray.go:36-53, materials.go:33-113).  Returns true

@@ -104,20 +104,24 @@ __device__ __forceinline__ void traverse_phase(uint32_t& mode, Trav& t, const Ra
         // Every lane steps: one that is not traversing (or finishes early) waits on the
         // sentinel, t.i = 16 * n_entries, where a step changes nothing — cheaper than masking
         // the wave per step.
+        uint32_t done = 0;  // COUNT: lane-steps that tested an entry (a lane on the sentinel idles)
         if constexpr (BATCH) {
 #pragma unroll
             for (int s = 0; s < STEPS; ++s)
-                trav_step_batched<COUNT, QUADS, FIXED, HYB>(t, r, E, cnt, 16 * n_entries, prim_batch);
+                done += trav_step_batched<COUNT, QUADS, FIXED, HYB>(t, r, E, cnt, 16 * n_entries, prim_batch);
         } else {
 #pragma unroll
-            for (int s = 0; s < STEPS; ++s) trav_step<COUNT, QUADS, FIXED, HYB>(t, r, E, cnt);
+            for (int s = 0; s < STEPS; ++s) {
+                if (COUNT) done += (uint32_t)__popcll(__ballot(t.i < 16 * n_entries));
+                trav_step<COUNT, QUADS, FIXED, HYB>(t, r, E, cnt);
+            }
         }
         if (mode == 0 && t.i >= 16 * n_entries) mode = 1;
         const uint64_t trav = __ballot(mode == 0);
         const uint64_t pend = __ballot(mode == 1 || mode == 2);
         if (COUNT) {
             ++wave_iters;
-            lane_steps += (uint64_t)__popcll(trav);
+            lane_steps += done;
             idle_lanes += (uint64_t)__popcll(__ballot(mode == 3));
         }
         if (trav == 0 || (uint32_t)__popcll(pend) >= thresh) {
@@ -293,7 +297,7 @@ __global__ __launch_bounds__(64 * WX * WY, MINW) void render_wave(Params p) {
     if (COUNT) {
         flush_counters(p, (uint64_t)pixels_done * spp, cnt);
         if (lane == 0) {
-            flush_sched(p, wave_iters, lane_steps, shade_phases, shade_lanes);
+            flush_sched(p, wave_iters, lane_steps / STEPS, shade_phases, shade_lanes);
             atomicAdd(&p.counters[12], (unsigned long long)trav_cycles);
             atomicAdd(&p.counters[13], (unsigned long long)shade_cycles);
             atomicAdd(&p.counters[14], (unsigned long long)idle_lanes);
@@ -479,7 +483,7 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
     if (COUNT) {
         flush_counters(p, items_done, cnt);
         if (lane == 0) {
-            flush_sched(p, wave_iters, lane_steps, shade_phases, shade_lanes);
+            flush_sched(p, wave_iters, lane_steps / STEPS, shade_phases, shade_lanes);
             atomicAdd(&p.counters[12], (unsigned long long)trav_cycles);
             atomicAdd(&p.counters[13], (unsigned long long)shade_cycles);
             atomicAdd(&p.counters[14], (unsigned long long)idle_lanes);
@@ -717,7 +721,7 @@ __global__ __launch_bounds__(POOL_BLOCK) void render_pool(Params p) {
 
     if (COUNT) {
         flush_counters(p, samples, cnt);
-        if (lane == 0) flush_sched(p, wave_iters, lane_steps, shade_phases, shade_lanes);
+        if (lane == 0) flush_sched(p, wave_iters, lane_steps / 3, shade_phases, shade_lanes);
     }
 }
 
@@ -770,6 +774,7 @@ hipError_t launch_wave_geom(const Params& p, bool use_lds, hipStream_t stream) {
         if (per_cu < 1) per_cu = 1;
         const uint64_t tiles = (uint64_t)((p.width + 7) / 8) * ((p.rows + 7) / 8);
         uint64_t blocks = (uint64_t)per_cu * cus;
+        if (p.grid_pct > 0 && p.grid_pct < 100) blocks = (blocks * p.grid_pct + 99) / 100;
         const uint64_t need = (tiles + WX * WY - 1) / (WX * WY);  // no wave starts without a tile
         if (blocks > need) blocks = need;
         if (blocks == 0) blocks = 1;
