@@ -856,6 +856,10 @@ bool uses_items(const Params& p, uint32_t flags) {
     return work;
 }
 
+#ifndef RTX_HYB_WAVES  // the same for scenes in HBM with a 64 KB LDS cache of their top levels
+#define RTX_HYB_WAVES 12
+#define RTX_HYB_MINW 6
+#endif
 #ifndef RTX_V3_WAVES  // workgroup size and waves per SIMD of the default v3 kernel (A/B builds override)
 #define RTX_V3_WAVES 8
 #define RTX_V3_MINW 6
@@ -870,8 +874,8 @@ hipError_t launch_items_for(const Params& p, bool use_lds, hipStream_t stream) {
                          : launch_items<COUNT, false, false, 4>(p, use_lds, stream);
     // 6 waves per SIMD: at most 80 VGPRs (the allocation granule is 8)
     if (!use_lds && p.n_hot > HOT_ENTRIES_8W)  // a 64 KB LDS cache: 12-wave workgroups, two per CU
-        return p.n_quads ? launch_items<COUNT, true, false, 12, COUNT ? 0 : 6>(p, use_lds, stream)
-                         : launch_items<COUNT, false, false, 12, COUNT ? 0 : 6>(p, use_lds, stream);
+        return p.n_quads ? launch_items<COUNT, true, false, RTX_HYB_WAVES, COUNT ? 0 : RTX_HYB_MINW>(p, use_lds, stream)
+                         : launch_items<COUNT, false, false, RTX_HYB_WAVES, COUNT ? 0 : RTX_HYB_MINW>(p, use_lds, stream);
     return p.n_quads ? launch_items<COUNT, true, false, RTX_V3_WAVES, COUNT ? 0 : RTX_V3_MINW>(p, use_lds, stream)
                      : launch_items<COUNT, false, false, RTX_V3_WAVES, COUNT ? 0 : RTX_V3_MINW>(p, use_lds, stream);
 }
