@@ -414,6 +414,7 @@ int enqueue_on(rtx_scene* s, DeviceCopy* c, const rtx_camera* cam, uint64_t seed
         p.sub = env_knob("RTX_ITEM_SUB", 0, 0, 4096);  // 0: chosen per chunk by launch_items
         p.item_waves = env_knob("RTX_ITEM_WAVES", 8, 4, 8) >= 8 ? 8u : 4u;
         p.grid_pct = env_knob("RTX_ITEM_GRID", 100, 1, 100);
+        p.debug_launch = env_knob("RTX_DEBUG_LAUNCH", 0, 0, 1);
         p.prim_batch = env_knob("RTX_PRIM_BATCH", 16, 1, 65);  // 65: primitive tests only when no node is left
     }
     if (flags & RTX_FLAG_COUNTERS) HIP_TRY(hipMemsetAsync(c->counters, 0, 16 * sizeof(unsigned long long), stream));

@@ -404,6 +404,7 @@ struct Params {
     uint32_t k0, kn, sub;
     uint32_t item_waves;  // v3 waves per workgroup: 8 (one LDS scene copy each), or 4 for A/B
     uint32_t n_hot;       // entries stored first and cached in LDS by v3 when the scene does not fit
+    uint32_t debug_launch;  // RTX_DEBUG_LAUNCH=1: v3 prints its launch shape to stderr
     uint32_t grid_pct;    // v3: percent of the resident grid launched (A/B knob; 100 = all resident waves)
     uint32_t prim_batch;  // v3: primitive tests wait for this many lanes (trav_step_batched); 0 = off
 };

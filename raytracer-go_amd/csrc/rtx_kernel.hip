@@ -20,6 +20,8 @@
 // waiting lanes shade together, so shading and its Philox blocks run in lockstep.
 #include <hip/hip_runtime.h>
 
+#include <cstdio>
+
 #include "rtx_device.h"
 #include "rtx_kernel.h"
 
@@ -837,6 +839,9 @@ hipError_t launch_items(Params p, bool use_lds, hipStream_t stream) {
         const uint64_t units = tiles * ((p.kn + p.sub - 1) / p.sub);
         uint64_t blocks = (uint64_t)per_cu * cus;
         if (blocks > (units + WAVES - 1) / WAVES) blocks = (units + WAVES - 1) / WAVES;  // no wave starts idle
+        if (p.debug_launch)
+            fprintf(stderr, "rtx v3: waves/wg %d, wgs/CU %d, CUs %d, grid %llu, sub %u, units %llu, lds %zu B\n", WAVES,
+                    per_cu, cus, (unsigned long long)blocks, p.sub, (unsigned long long)units, shmem);
         e = hipMemsetAsync(p.tile_counter, 0, 2 * sizeof(uint32_t), stream);
         if (e != hipSuccess) return e;
         hipLaunchKernelGGL(kern, dim3((uint32_t)blocks), dim3(block), shmem, stream, p);
