@@ -50,7 +50,7 @@ def worker(rank, world, port, out_path):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])  # 8: the driver's one-node scaling run (C3)
 def test_sharded_gather_equals_single_render(built, tmp_path, world):
     out = str(tmp_path / "full.npy")
     mp.start_processes(worker, args=(world, free_port(), out), nprocs=world, join=True, start_method="spawn")
