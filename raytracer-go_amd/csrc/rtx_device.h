@@ -17,6 +17,9 @@
 
 namespace rtxd {
 
+// Wave vote on a bool (HIP's __ballot takes an int).
+__device__ __forceinline__ uint64_t ballot(bool c) { return __builtin_amdgcn_ballot_w64(c); }
+
 struct V3 {
     float x, y, z;
 };
@@ -523,7 +526,7 @@ __device__ __forceinline__ Scatter coop_scatter(const Params& p, const SceneRef 
         z = signed_unit(b0.z);
     }
     uint32_t att = 0;
-    uint64_t pend = __ballot(need && !(x * x + y * y + z * z < 1.0f));  // lensq(v) < 1
+    uint64_t pend = ballot(need) & ~ballot(x * x + y * y + z * z < 1.0f);  // lensq(v) < 1
     const uint32_t lane = __lane_id();
     const uint64_t below_mask = (1ull << lane) - 1ull;
     for (uint32_t base = 1; pend != 0;) {
@@ -541,7 +544,7 @@ __device__ __forceinline__ Scatter coop_scatter(const Params& p, const SceneRef 
         const uint32_t oe = lane_pull(owner, e);
         const U4 b = philox4x32_10(opix, osmp, oe, base + k, rng.k0, rng.k1);
         const float bx = signed_unit(b.x), by = signed_unit(b.y), bz = signed_unit(b.z);
-        const uint64_t good = __ballot(slot && bx * bx + by * by + bz * bz < 1.0f);
+        const uint64_t good = ballot(slot) & ballot(bx * bx + by * by + bz * bz < 1.0f);
         const uint64_t kmask = K >= 64u ? ~0ull : ((1ull << K) - 1ull);
         const uint64_t mine_good = mine ? ((good >> (below * K)) & kmask) : 0ull;
         const uint32_t kk = mine_good ? (uint32_t)__builtin_ctzll(mine_good) : 0u;
@@ -555,7 +558,7 @@ __device__ __forceinline__ Scatter coop_scatter(const Params& p, const SceneRef 
             z = fz;
             att = base + kk;
         }
-        pend = __ballot(mine && !mine_good);
+        pend = ballot(mine) & ~ballot(mine_good != 0ull);
         base += K;
     }
     if (need) {
@@ -742,18 +745,20 @@ __device__ __forceinline__ uint32_t trav_step_batched(Trav& t, const Ray& r, con
     load_entry<FIXED, HYB>(E, t.i, ea, eb);
     const int32_t tag = __float_as_int(eb.w);
     const bool prim = tag < -1;
-    const uint64_t pm = __ballot(prim);
-    const uint64_t bm = __ballot(!prim && t.i < end);
+    const uint64_t pm = ballot(prim);
+    // lanes on a node: SALU on two compare masks (a vote on `!prim && t.i < end` itself was
+    // materialised as v_cndmask + v_cmp, two VALU per step)
+    const uint64_t bm = ballot(t.i < end) & ~pm;
     const bool prims = (uint32_t)__popcll(pm) >= kmin || bm == 0;
     if (prims) {
-        if (prim) {
+        if (__builtin_amdgcn_inverse_ballot_w64(pm)) {  // = prim, as the vote's mask (no second compare)
             if (COUNT && HYB && t.i < E.hot) ++cnt.cache_hits;
             if (QUADS && tag == RTX_E_QUAD) quad_test<COUNT>(t, r, E, ea, eb, t.i, cnt);
             else sphere_test<COUNT>(t, r, ea, eb, t.i, cnt);
             t.i = (uint32_t)__float_as_int(eb.z);
         }
-    } else if (!prim) {
-        if (COUNT && HYB && t.i < E.hot && t.i < end) ++cnt.cache_hits;
+    } else if (__builtin_amdgcn_inverse_ballot_w64(bm)) {  // lanes on a node (the sentinel's step is a no-op)
+        if (COUNT && HYB && t.i < E.hot) ++cnt.cache_hits;
         box_step<COUNT>(t, r, ea, eb, tag, cnt);
     }
     return COUNT ? (uint32_t)__popcll(prims ? pm : bm) : 0u;

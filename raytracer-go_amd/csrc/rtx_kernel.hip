@@ -114,17 +114,20 @@ __device__ __forceinline__ void traverse_phase(uint32_t& mode, Trav& t, const Ra
         } else {
 #pragma unroll
             for (int s = 0; s < STEPS; ++s) {
-                if (COUNT) done += (uint32_t)__popcll(__ballot(t.i < 16 * n_entries));
+                if (COUNT) done += (uint32_t)__popcll(ballot(t.i < 16 * n_entries));
                 trav_step<COUNT, QUADS, FIXED, HYB>(t, r, E, cnt);
             }
         }
+        // votes on single compares, combined with SALU (a vote on a combined condition was
+        // materialised with two extra VALU)
+        const uint64_t walking = ballot(mode == 0), at_end = ballot(t.i >= 16 * n_entries);
         if (mode == 0 && t.i >= 16 * n_entries) mode = 1;
-        const uint64_t trav = __ballot(mode == 0);
-        const uint64_t pend = __ballot(mode == 1 || mode == 2);
+        const uint64_t trav = walking & ~at_end;
+        const uint64_t pend = ballot(mode - 1u < 2u);  // mode 1 or 2
         if (COUNT) {
             ++wave_iters;
             lane_steps += done;
-            idle_lanes += (uint64_t)__popcll(__ballot(mode == 3));
+            idle_lanes += (uint64_t)__popcll(ballot(mode == 3));
         }
         if (trav == 0 || (uint32_t)__popcll(pend) >= thresh) {
             if (COUNT) {
@@ -204,7 +207,7 @@ __global__ __launch_bounds__(64 * WX * WY, MINW) void render_wave(Params p) {
             trav_cycles += now - clk;
             clk = now;
         }
-        if (__ballot(mode != M_DONE) == 0) break;
+        if (ballot(mode != M_DONE) == 0) break;
 
         // ---- shading phase ----------------------------------------------------------
         // The scatter samples of this phase, drawn by the whole wave together.
@@ -242,7 +245,7 @@ __global__ __launch_bounds__(64 * WX * WY, MINW) void render_wave(Params p) {
             }
             if constexpr (PERSIST) {  // lanes without a pixel take the next ones of the wave's tile
                 for (;;) {
-                    const uint64_t wm = __ballot(mode == M_CLAIM);
+                    const uint64_t wm = ballot(mode == M_CLAIM);
                     if (wm == 0) break;
                     if (cursor >= 64u && !exhausted) {  // claim the next 8x8 tile (wave-uniform)
                         uint32_t tl = 0;
@@ -287,7 +290,7 @@ __global__ __launch_bounds__(64 * WX * WY, MINW) void render_wave(Params p) {
                     ++rng.sample;
                 }
             }
-            if (__ballot(fresh) == 0) break;
+            if (ballot(fresh) == 0) break;
         }
         if (ready) {  // begin a segment: world.Hit (ray.go:36)
             if (COUNT) ++cnt.segments;
@@ -403,7 +406,7 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
             trav_cycles += now - clk;
             clk = now;
         }
-        if (__ballot(mode != M_DONE) == 0) break;
+        if (ballot(mode != M_DONE) == 0) break;
 
         // ---- shading phase ----------------------------------------------------------
         const Scatter sc = coop_scatter<QUADS>(p, E, rng, seg + 1, mode == M_SHADE ? t.hit : -1);
@@ -426,7 +429,7 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
         // Lanes without an item take the next ones of the wave's unit; new camera rays
         // at one program point.  Loops only for max depth 0 and ragged tiles.
         for (;;) {
-            const uint64_t wm = __ballot(mode == M_CLAIM);
+            const uint64_t wm = ballot(mode == M_CLAIM);
             if (wm == 0) break;
             if (cursor >= u_items && !exhausted) {  // claim the next unit (wave-uniform)
                 uint32_t un = 0;
@@ -598,7 +601,7 @@ __global__ __launch_bounds__(POOL_BLOCK) void render_pool(Params p) {
         wp->sy[s] = 0.0f;
         wp->sz[s] = 0.0f;
         wp->st[s] = valid ? 0u : ST_INVALID;
-        const uint32_t nvalid = (uint32_t)__popcll(__ballot(valid));
+        const uint32_t nvalid = (uint32_t)__popcll(ballot(valid));
         if (lane == 0) {
             wp->tile[ch] = has ? (int32_t)tl : -1;
             wp->remaining[ch] = nvalid;
@@ -677,10 +680,10 @@ __global__ __launch_bounds__(POOL_BLOCK) void render_pool(Params p) {
             }
             any_chunk |= wp->tile[ch] >= 0;
         }
-        if (!any_chunk && __ballot(mode == Q_TRAV || mode == Q_SHADE) == 0) break;
+        if (!any_chunk && ballot(mode == Q_TRAV || mode == Q_SHADE) == 0) break;
 
         // ---- claim idle pixels for free lanes ------------------------------------------------
-        const uint64_t freem = __ballot(mode == Q_FREE || mode == Q_IDLE);
+        const uint64_t freem = ballot(mode == Q_FREE || mode == Q_IDLE);
         if (mode == Q_FREE || mode == Q_IDLE) {
             const uint32_t rank = (uint32_t)__popcll(freem & ((1ull << lane) - 1ull));
             const uint32_t cand = (cursor + rank) % POOL_SLOTS;
