@@ -266,6 +266,15 @@ int ensure_device(rtx_scene* s, int device, DeviceCopy** out) {
                 std::memcpy(m.albedo, s->textures[m.texture].even, sizeof(m.albedo));
                 m.texture = rtxd::RTX_DEV_TEX_INLINE;
             }
+            if (m.type == RTX_MAT_DIELECTRIC) {  // (albedo unused: attenuation is (1,1,1))
+                // per-material float32 quotients of materials.go:98, 116-117, computed once here
+                // (IEEE division: the same bits the kernel's correctly rounded divide gave)
+                const float inv = 1.0f / m.ior;
+                const float rf = (1.0f - inv) / (1.0f + inv), rb = (1.0f - m.ior) / (1.0f + m.ior);
+                m.albedo[0] = inv;      // eta of a front-face hit
+                m.albedo[1] = rf * rf;  // r0 for eta = 1/ior
+                m.albedo[2] = rb * rb;  // r0 for eta = ior
+            }
         }
         HIP_TRY(hipMalloc(&c.materials, std::max<size_t>(1, dm.size()) * sizeof(rtx_material)));
         if (!dm.empty()) HIP_TRY(hipMemcpy(c.materials, dm.data(), dm.size() * sizeof(rtx_material), hipMemcpyHostToDevice));

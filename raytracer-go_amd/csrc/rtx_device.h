@@ -855,14 +855,14 @@ __device__ __forceinline__ bool shade(const Params& p, const SceneRef E, const T
         return false;
     }
     if (m.type == RTX_MAT_DIELECTRIC) {                         // materials.go:91-113
-        const float eta = front ? 1.0f / m.ior : m.ior;
+        // 1/ior and both r0 values precomputed per material (ensure_device, rtx_capi.hip)
+        const float eta = front ? m.albedo[0] : m.ior;
         const float d = dot(scale(ud, -1.0f), n);
         const float cos_t = d < 1.0f ? d : (d != d ? d : 1.0f); // float32(math.Min(float64(d), 1))
         const float sin_t = (float)__builtin_sqrt(1.0 - (double)(cos_t * cos_t));
         bool refl = sin_t * eta > 1.0f;
         if (!refl) {                                            // short-circuit: draw only here
-            float r0 = (1.0f - eta) / (1.0f + eta);             // materials.go:116-118
-            r0 *= r0;
+            const float r0 = front ? m.albedo[1] : m.albedo[2];  // ((1-eta)/(1+eta))^2, materials.go:116-118
             const float rf = r0 + (1.0f - r0) * (float)go_pow5(1.0 - (double)cos_t);
             refl = rf > unit_f32(b0.x);
             if (COUNT) cnt.draws += 1;
