@@ -366,8 +366,9 @@ __device__ __forceinline__ SceneRef scene_ref_fixed(const float4* lds, uint32_t 
 }
 // The LDS cache of a scene too big for the fixed layout: its first entries (whole top
 // levels, rtx_capi.hip ensure_device) in the fixed layout's places.  Up to HOT_ENTRIES_8W
-// (52 KB) three 8-wave workgroups share a CU; up to HOT_ENTRIES_MAX (64 KB, the workgroup
-// limit) two 12-wave ones do — 6 waves per SIMD either way.
+// (52 KB) three 8-wave workgroups share a CU; up to HOT_ENTRIES_MAX (64 KB: the fixed layout's
+// two 32 KB halves, reached by the ds_read offset field) two 12-wave ones do — 6 waves per
+// SIMD either way.
 constexpr uint32_t HOT_ENTRIES_8W = 1280;
 constexpr uint32_t HOT_ENTRIES_MAX = 2048;
 __host__ __device__ __forceinline__ uint32_t lds_hot_bytes(uint32_t n_hot) { return LDS_B + n_hot * 16; }
