@@ -1,20 +1,26 @@
 #!/usr/bin/env python3
-"""Headline benchmark: Mray/s on 1920x1080x500spp random-spheres (BASELINE.json
-configs[1]) on N MI355X, with the HBM-roofline fraction of the megakernel and the CPU
-oracle timed on the host beside it.
+"""Headline benchmark: Mray/s on 1920x1080x500spp random-spheres (BASELINE.json configs[1])
+on N MI355X, with the roofline of the megakernel and the CPU oracle timed on the host beside it.
 
-A step = one render of the whole 1920x1080x500 image of randSpheres (main.go:227-289,
-seeded), row-interleaved over the N ranks (one process per GPU), plus the RCCL gather
-of the shards to rank 0 when N > 1.  Scene tables are uploaded to HBM before timing.
+A step = one render of the whole image of randSpheres (main.go:227-289, seeded),
+row-interleaved over the N ranks (one process per GPU), plus the RCCL gather of the shards
+to rank 0 when N > 1.  Scene tables are uploaded to HBM before timing.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W]
-  N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--spp S]
+  --spp 2000 is configs[2] (1920x1080x2000, meant for 8 GPUs).
+  N > 1 either under torch.distributed.run (RANK/WORLD_SIZE in the environment), or plain
+  `python bench.py --gpus N`: the process then starts N rank processes itself (before any
+  GPU call) and exits with their status.
 """
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
+import platform
+import socket
+import subprocess
 import sys
 import time
 
@@ -23,7 +29,12 @@ PKG = os.path.join(ROOT, "raytracer-go_amd")
 sys.path.insert(0, PKG)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
-VALU_PEAK_TFLOPS = 157.3
+SIMDS = 1024  # 256 CUs x 4 SIMD-32
+CLOCK_MAX_GHZ = 2.4
+# VALU issue peak: one wave64 instruction per 2 cycles per SIMD (MI355X_MICROARCH.md, wave scheduling)
+VALU_PEAK_GINST = SIMDS * CLOCK_MAX_GHZ / 2.0
+LDS_READ_PEAK_GBS = 150000.0  # ds_read_b128 aggregate with every CU streaming (MI355X_MICROARCH.md §LDS)
+CPU_SHARE_PER_GPU = 16  # the host's cores per GPU (gpurun: "size worker pools to the box's CPU share")
 
 
 def parse():
@@ -38,12 +49,53 @@ def parse():
     ap.add_argument("--scene-seed", type=int, default=1)
     ap.add_argument("--seed", type=int, default=2024)
     ap.add_argument("--cpu-target-s", type=float, default=15.0, help="CPU baseline budget (seconds)")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0: the host's CPU share per GPU")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
-    ap.add_argument("--valu", default=os.path.join(ROOT, "profiles", "valu_r01.json"))
+    ap.add_argument("--no-hash", action="store_true", help="skip the framebuffer hash")
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_r02.json"))
+    ap.add_argument("--valu", default=os.path.join(ROOT, "profiles", "valu_r02.json"))
+    # launcher self-test on the CPU (tests/test_bench_launcher.py): gloo, no GPU, shards filled
+    # with a known function of the global pixel instead of rendered
+    ap.add_argument("--selftest-gloo", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--selftest-fail-rank", type=int, default=-1, help=argparse.SUPPRESS)
     return ap.parse_args()
 
 
+# ---- launcher: N rank processes without torchrun ------------------------------------------
+def free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n: int) -> int:
+    """Start n copies of this script as ranks 0..n-1 (torch.distributed env contract) and
+    wait for them; if one fails, stop the others.  Touches no GPU itself."""
+    port = free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                for q in live:  # a failed rank leaves the others waiting in a collective
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
+
+
+# ---- measurement helpers -----------------------------------------------------------------
 def alg_bytes(st: dict, pixels: int) -> float:
     """32 B per node visit, 20 B per primitive test (16 B sphere +
     4 B material id), 20 B per hit (material record), 4 B per texel fetch, plus the
@@ -52,14 +104,27 @@ def alg_bytes(st: dict, pixels: int) -> float:
             + 12.0 * pixels)
 
 
-def cpu_baseline(scene, cam, seed: int, target_s: float) -> dict:
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or "unknown"
+
+
+def cpu_baseline(scene, cam, seed: int, target_s: float, threads: int) -> dict:
     """The oracle (oracle/liboracle.so, a scalar C restatement) on host threads over a
     bounded sample of the same workload: full-width rows at a fixed stride, all spp."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_binding as ob
     import rtx
 
-    threads = max(1, min(16, os.cpu_count() or 1))
+    logical = len(os.sched_getaffinity(0))
+    if threads <= 0:
+        threads = min(CPU_SHARE_PER_GPU, logical)
     H = cam.image_height
     # Calibrate on 2 rows per thread (every thread busy), then size the sample to
     # ~target_s of wall time on those threads.
@@ -83,9 +148,11 @@ def cpu_baseline(scene, cam, seed: int, target_s: float) -> dict:
         "kind": "port",
         "samples_per_s": c["samples"] / dt,
         "seconds": dt,
+        "cpu_model": cpu_model(),
+        "host_logical_cpus": logical,
         "sample": f"{nrows} full-width rows (every {stride}th) of the same {cam.image_width}x{H}x{cam.samples_per_pixel} "
-                  f"render, {c['samples']} samples, C oracle on {threads} threads "
-                  f"(Go absent on the host: the C restatement stands in for the Go reference)",
+                  f"render, {c['samples']} samples, C oracle on {threads} threads = one GPU's share of the host's "
+                  f"{logical} logical CPUs (Go absent on the host: the C restatement stands in for the Go reference)",
     }
 
 
@@ -106,27 +173,81 @@ def schedule(st: dict) -> dict:
     return out
 
 
+def load_profile(path: str, workload: str):
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        d = json.load(f)
+    return d if d.get("workload") == workload else None
+
+
+def roofline(st: dict, pixels: int, kernel_s: float, workload: str, traffic_path: str, valu_path: str) -> dict:
+    """The render kernel's roof is VALU issue: its scene and materials are
+    LDS-resident, HBM carries only the sample scratch.  achieved = the committed PMC pass's VALU
+    wave-instructions per launch (same kernel, same workload) / this run's HIP-event time of
+    the launch; peak = 1024 SIMDs x 2.4 GHz / 2 cycles per wave64 instruction.  The SURVEY §8(d)
+    algorithmic bytes (LDS-served, not HBM) and the measured HBM bytes are reported beside it."""
+    launch_bytes = alg_bytes(st, pixels)
+    tr = load_profile(traffic_path, workload)
+    vr = load_profile(valu_path, workload)
+    out = {"bound": "valu", "achieved": None, "peak": round(VALU_PEAK_GINST, 1), "unit": "Gwave-inst/s",
+           "frac": None, "traffic": tr.get("hbm_bytes_per_launch") if tr else None}
+    if vr:
+        achieved = vr["valu_insts_per_launch"] / kernel_s / 1e9
+        out.update(achieved=round(achieved, 1), frac=round(achieved / VALU_PEAK_GINST, 4),
+                   lane_frac=vr["valu_lane_frac"], pmc_issue_frac=vr["valu_issue_frac"],
+                   valu_insts_per_launch=vr["valu_insts_per_launch"], source=os.path.relpath(valu_path, ROOT))
+    out["alg_bytes"] = {
+        "per_launch": launch_bytes,
+        "achieved_gbs": round(launch_bytes / kernel_s / 1e9, 1),
+        "served_from": "LDS (scene + material table copied per workgroup)",
+        "frac_of_lds_read_peak": round(launch_bytes / kernel_s / 1e9 / LDS_READ_PEAK_GBS, 4),
+        "frac_of_hbm_peak_if_it_were_hbm": round(launch_bytes / kernel_s / 1e9 / HBM_PEAK_GBS, 4),
+    }
+    if tr:
+        out["hbm"] = {"bytes_per_launch": tr["hbm_bytes_per_launch"],
+                      "achieved_gbs": round(tr["hbm_bytes_per_launch"] / kernel_s / 1e9, 1),
+                      "frac": round(tr["hbm_bytes_per_launch"] / kernel_s / 1e9 / HBM_PEAK_GBS, 4),
+                      "source": os.path.relpath(traffic_path, ROOT)}
+    return out
+
+
+def framebuffer_hash(img) -> str:
+    import numpy as np
+
+    a = np.ascontiguousarray(img.detach().cpu().numpy(), dtype=np.float32)
+    return hashlib.sha256(a.tobytes()).hexdigest()[:16]
+
+
+# ---- the run -------------------------------------------------------------------------------
 def main():
     args = parse()
+    if args.gpus > 1 and "RANK" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))  # before anything touches a GPU
     import torch
     import torch.distributed as dist
 
-    import rtx
     from dist import gather_image, max_shard_rows
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run (one process per GPU)")
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.selftest_gloo:
+        return selftest_gloo(args, rank, world)
+
+    import rtx
+
     torch.cuda.set_device(local_rank)
+    backend = None
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        backend = "nccl"  # RCCL on ROCm
+        dist.init_process_group(backend, device_id=torch.device("cuda", local_rank))
 
     scene = rtx.HostScene(args.scene, seed=args.scene_seed)
     cam = scene.camera(width=args.width, spp=args.spp, depth=args.depth)
-    W, H = cam.image_width, cam.image_height
+    W, H, S = cam.image_width, cam.image_height, cam.samples_per_pixel
     dev = rtx.DeviceScene(scene.desc)  # one-time upload to this rank's HBM
     reg = rtx.Region(0, 0, W, H, rank, world)
     R = max_shard_rows(H, world)
@@ -141,18 +262,16 @@ def main():
     # Untimed counting pass (separate kernel instantiation): the work units of a step.
     st = dev.render_region(cam, args.seed, reg, shard.data_ptr(), stream, counters=True, timed=True).as_dict()
     my_rows = rtx.region_rows(reg)
-    counts = torch.tensor([st["samples"], st["segments"], st["node_visits"], st["prim_tests"], st["hits"],
-                           st["texel_fetches"], st["rng_draws"]], dtype=torch.float64, device="cuda")
+    keys = ["samples", "segments", "node_visits", "prim_tests", "hits", "texel_fetches", "rng_draws"]
+    counts = torch.tensor([st[k] for k in keys], dtype=torch.float64, device="cuda")
     if world > 1:
         dist.all_reduce(counts)
-    tot = dict(zip(["samples", "segments", "node_visits", "prim_tests", "hits", "texel_fetches", "rng_draws"],
-                   counts.tolist()))
+    tot = dict(zip(keys, counts.tolist()))
 
     def step(times):
         s = dev.render_region(cam, args.seed, reg, shard.data_ptr(), stream, counters=False, timed=True)
         times.append(s.kernel_ms)
-        img = gather_image(shard, H, rank, world)
-        return img
+        return gather_image(shard, H, rank, world)
 
     for _ in range(args.warmup):
         step([])
@@ -174,24 +293,12 @@ def main():
         mray = tot["segments"] * args.steps / elapsed / 1e6
         samples_s = tot["samples"] * args.steps / elapsed
         avg_kernel_s = sum(kms) / len(kms) / 1e3
-        launch_bytes = alg_bytes(st, my_rows * W)  # rank 0's launch
-        achieved = launch_bytes / avg_kernel_s / 1e9
-        traffic = None
-        if os.path.exists(args.traffic):
-            with open(args.traffic) as f:
-                tr = json.load(f)
-            if tr.get("workload") == f"{args.scene}:{W}x{H}x{cam.samples_per_pixel}" and world == 1:
-                traffic = tr.get("hbm_bytes_per_launch")
-        valu = None  # the kernel's actual bound: VALU issue, from the committed PMC pass (scripts/pmc_valu.py)
-        if os.path.exists(args.valu):
-            with open(args.valu) as f:
-                vr = json.load(f)
-            if vr.get("workload") == f"{args.scene}:{W}x{H}x{cam.samples_per_pixel}" and world == 1:
-                valu = {"issue_frac": vr["valu_issue_frac"], "lane_frac": vr["valu_lane_frac"],
-                        "source": "profiles/valu_r01.json (rocprofv3 PMC of the same launch)"}
-        headline = args.scene == "random_spheres" and (W, H, cam.samples_per_pixel) == (1920, 1080, 500)
+        headline = args.scene == "random_spheres" and (W, H, S) == (1920, 1080, 500)
+        c3 = args.scene == "random_spheres" and (W, H, S) == (1920, 1080, 2000)
         metric = ("Mray/s on 1920x1080x500spp random-spheres; achieved HBM GB/s vs peak" if headline else
-                  f"Mray/s on {W}x{H}x{cam.samples_per_pixel}spp {args.scene} (not the headline config)")
+                  f"Mray/s on {W}x{H}x{S}spp {args.scene}" + (" (configs[2])" if c3 else " (not the headline config)"))
+        tag = " (configs[1])" if headline else (" (configs[2])" if c3 else "")
+        profile_workload = f"{args.scene}:{W}x{H}x{S}"
         out = {
             "metric": metric,
             "value": round(mray, 3),
@@ -207,11 +314,12 @@ def main():
             "data": f"synthetic (seeded {args.scene} scene built by the host mirror of main.go; "
                     "RNG contract Philox4x32-10)",
             "config": {
-                "workload": f"{args.scene} {W}x{H}x{cam.samples_per_pixel}spp depth {cam.max_depth}"
-                            + (" (configs[1])" if headline else ""),
+                "workload": f"{args.scene} {W}x{H}x{S}spp depth {cam.max_depth}{tag}",
                 "scene_seed": args.scene_seed,
                 "render_seed": args.seed,
                 "parallelism": f"row-interleave x{world}" + (" + RCCL gather" if world > 1 else ""),
+                "world_size": dist.get_world_size() if world > 1 else 1,
+                "backend": backend,
             },
             "samples_per_s": round(samples_s, 1),
             "gsamples_per_s": round(samples_s / 1e9, 4),
@@ -219,23 +327,46 @@ def main():
             "node_visits_per_segment": round(tot["node_visits"] / tot["segments"], 3),
             "kernel_ms_avg": round(avg_kernel_s * 1e3, 3),
             "schedule": schedule(st),
-            "roofline": {
-                "bound": "hbm",
-                "achieved": round(achieved, 2),
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": traffic,
-                "alg_bytes_per_launch": launch_bytes,
-                "note": "algorithmic bytes (SURVEY §8d) of rank 0's launch / its HIP-event time; the 32 KB "
-                        "scene is LDS-resident, so real HBM traffic (PMC: the v3 sample scratch) is ~300x lower "
-                        "and the kernel is bound by VALU issue instead (valu)",
-                "valu": valu,
-            },
+            "roofline": roofline(st, my_rows * W, avg_kernel_s, profile_workload if world == 1 else "-",
+                                 args.traffic, args.valu),
         }
+        if not args.no_hash:
+            out["framebuffer_sha256_16"] = framebuffer_hash(img)  # bitwise-comparable across N
         if world == 1 and not args.no_cpu:
-            out["cpu_baseline"] = cpu_baseline(scene, cam, args.seed, args.cpu_target_s)
+            out["cpu_baseline"] = cpu_baseline(scene, cam, args.seed, args.cpu_target_s, args.cpu_threads)
         print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def selftest_gloo(args, rank: int, world: int) -> None:
+    """The multi-rank plumbing of main() on the CPU: gloo process group, row-interleaved shards
+    of a width x height image (height from the scene's 16:9 aspect), each filled with its global
+    pixel index instead of a render, the same gather + de-interleave, and rank 0's JSON line
+    with the framebuffer hash (tests/test_bench_launcher.py recomputes it)."""
+    import torch
+    import torch.distributed as dist
+
+    from dist import gather_image, max_shard_rows, shard_rows
+
+    if rank == args.selftest_fail_rank:
+        raise SystemExit(f"rank {rank}: failing on purpose (--selftest-fail-rank)")
+    if world > 1:
+        dist.init_process_group("gloo")
+    W = args.width
+    H = int(W * 9 // 16)
+    R = max_shard_rows(H, world)
+    shard = torch.zeros((R, W, 3), dtype=torch.float32)
+    for i in range(shard_rows(H, rank, world)):
+        y = rank + i * world
+        idx = torch.arange(W, dtype=torch.float32) + float(y * W)
+        shard[i] = idx[:, None].expand(W, 3)
+    img = gather_image(shard, H, rank, world)
+    if rank == 0:
+        print(json.dumps({"selftest": True, "n_gpus": world, "world_size": dist.get_world_size() if world > 1 else 1,
+                          "backend": "gloo" if world > 1 else None, "height": H,
+                          "framebuffer_sha256_16": framebuffer_hash(img)}), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

@@ -1,0 +1,299 @@
+// render_gpu.go — the Go side of the drop-in boundary: (*Camera).RenderGPU, a cgo binding of
+// librtx.so (include/rtx.h) for TwFlem/raytracer-go.
+//
+// A maintainer copies this file into the reference's package `internal` (next to
+// internal/camera.go; the Hittable/Material/Texture fields it flattens are unexported, so it
+// must live in that package) and points the cgo flags at a build of this repository
+// (`make -C raytracer-go_amd`).  It replaces nothing: Render (internal/camera.go:180) stays as
+// the CPU path, and RenderGPU falls back to it for anything the GPU path does not carry.
+//
+// Go is not installed in the image this repository is built in, so this file has not been
+// compiled; the same flattening is built and tested in C++ (raytracer-go_amd/host/flatten.cpp)
+// and through ctypes (tests/).
+package internal
+
+/*
+#cgo CFLAGS: -I${SRCDIR}/../../raytracer-mi355x/include
+#cgo LDFLAGS: -L${SRCDIR}/../../raytracer-mi355x/raytracer-go_amd -lrtx -Wl,-rpath,${SRCDIR}/../../raytracer-mi355x/raytracer-go_amd
+#include <stdlib.h>
+#include "rtx.h"
+*/
+import "C"
+
+import (
+	"errors"
+	"fmt"
+	"io"
+	"math"
+	"strconv"
+	"strings"
+	"unsafe"
+)
+
+// gpuTables is the flattened Hittable tree (rtx.h).  The slices hold no Go pointers, so
+// passing them to C is legal under the cgo rules; librtx copies them and never keeps them.
+type gpuTables struct {
+	nodes     []C.rtx_bvh_node
+	roots     []C.int32_t
+	spheres   []C.rtx_sphere
+	quads     []C.rtx_quad
+	materials []C.rtx_material
+	textures  []C.rtx_texture
+	texels    []C.uint32_t
+	matIdx    map[Material]C.uint32_t
+	texIdx    map[Texture]C.uint32_t
+}
+
+// errUnsupported: a scene part the GPU path does not carry (RenderGPU then uses Render).
+var errUnsupported = errors.New("rtx: scene type not on the GPU path")
+
+func primRef(typ, idx int) C.int32_t { return C.int32_t(^int32(uint32(typ)<<28 | uint32(idx)&0x0FFFFFFF)) }
+
+func vec(v Vec3) [3]C.float { return [3]C.float{C.float(v.X), C.float(v.Y), C.float(v.Z)} }
+
+// putRGBA16 appends one RTX_TEX_IMAGE texel: Go's 16-bit Color.RGBA() channels, two words.
+func (t *gpuTables) putRGBA16(r, g, b, a uint32) {
+	t.texels = append(t.texels, C.uint32_t(r&0xFFFF|(g&0xFFFF)<<16), C.uint32_t(b&0xFFFF|(a&0xFFFF)<<16))
+}
+
+func (t *gpuTables) texture(tex Texture) (C.uint32_t, error) {
+	if i, ok := t.texIdx[tex]; ok {
+		return i, nil
+	}
+	var r C.rtx_texture
+	switch v := tex.(type) {
+	case SolidColor:
+		r._type, r.even = C.RTX_TEX_SOLID, vec(v.albedo.GetColor())
+	case *SolidColor:
+		r._type, r.even = C.RTX_TEX_SOLID, vec(v.albedo.GetColor())
+	case *Checkered:
+		r._type, r.scale = C.RTX_TEX_CHECKERED, C.float(v.scale)
+		r.even, r.odd = vec(v.even.GetColor()), vec(v.odd.GetColor())
+	case *ImageTexture: // materials.go:175-193: At(int(u*Dx), int(v*Dy)).RGBA(), 16 bits per channel
+		b := v.img.Bounds()
+		r._type = C.RTX_TEX_IMAGE
+		if b.Dy() > 0 {
+			// GetTexture indexes At from 0; the table (and its border texel) is exact for bounds
+			// at the origin, which jpeg.Decode and image.New* return.
+			if b.Min.X != 0 || b.Min.Y != 0 {
+				return 0, errUnsupported
+			}
+			r.width, r.height = C.uint32_t(b.Dx()), C.uint32_t(b.Dy())
+			if len(t.texels)%2 != 0 { // 8-byte texels at an even word offset
+				t.texels = append(t.texels, 0)
+			}
+			r.texel_offset = C.uint32_t(len(t.texels))
+			for y := 0; y < b.Dy(); y++ {
+				for x := 0; x < b.Dx(); x++ {
+					t.putRGBA16(v.img.At(x, y).RGBA())
+				}
+			}
+			// The border texel: what At returns outside the bounds (u == 1, v == 0, NaN) —
+			// color.YCbCr{} = (0, 34678, 0) for jpeg.Decode's *image.YCbCr, 0 for *image.RGBA.
+			t.putRGBA16(v.img.At(b.Max.X, b.Min.Y).RGBA())
+		} else {
+			r.width = C.uint32_t(max(b.Dx(), 0)) // Dy() <= 0: the debug colour (0, 1, 1), no texels
+		}
+	case *NoiseTexture: // RTX_NOISE_TEXELS: gradients (float32 bits), then permX, permY, permZ
+		r._type, r.scale = C.RTX_TEX_NOISE, C.float(v.scale)
+		r.texel_offset = C.uint32_t(len(t.texels))
+		for _, g := range v.perlin.randVec3 {
+			for _, c := range [3]float32{g.X, g.Y, g.Z} {
+				t.texels = append(t.texels, C.uint32_t(math.Float32bits(c)))
+			}
+		}
+		for _, perm := range [][]int{v.perlin.permX, v.perlin.permY, v.perlin.permZ} {
+			for _, p := range perm {
+				t.texels = append(t.texels, C.uint32_t(p))
+			}
+		}
+	default:
+		return 0, errUnsupported
+	}
+	i := C.uint32_t(len(t.textures))
+	t.textures = append(t.textures, r)
+	t.texIdx[tex] = i
+	return i, nil
+}
+
+func (t *gpuTables) material(m Material) (C.uint32_t, error) {
+	if i, ok := t.matIdx[m]; ok {
+		return i, nil
+	}
+	var r C.rtx_material
+	switch v := m.(type) {
+	case *Lambertian:
+		ti, err := t.texture(v.albedo)
+		if err != nil {
+			return 0, err
+		}
+		r._type, r.texture = C.RTX_MAT_LAMBERTIAN, ti
+	case *Metal:
+		r._type, r.fuzz, r.albedo = C.RTX_MAT_METAL, C.float(v.fuzz), vec(v.albedo.GetColor())
+	case *Dielectric:
+		r._type, r.ior = C.RTX_MAT_DIELECTRIC, C.float(v.refractiveIndex)
+	case DiffuseLight, *DiffuseLight:
+		d, ok := v.(DiffuseLight)
+		if !ok {
+			d = *v.(*DiffuseLight)
+		}
+		ti, err := t.texture(d.emit)
+		if err != nil {
+			return 0, err
+		}
+		r._type, r.texture = C.RTX_MAT_DIFFUSE_LIGHT, ti
+	default:
+		return 0, errUnsupported
+	}
+	i := C.uint32_t(len(t.materials))
+	t.materials = append(t.materials, r)
+	t.matIdx[m] = i
+	return i, nil
+}
+
+// ref walks the tree in pre-order (a node before its children, left before right), the
+// order NewBVH (bvh.go:142-185) creates it in.
+func (t *gpuTables) ref(h Hittable) (C.int32_t, error) {
+	switch v := h.(type) {
+	case *BVH:
+		me := len(t.nodes)
+		b := v.bBox
+		t.nodes = append(t.nodes, C.rtx_bvh_node{
+			bmin: [3]C.float{C.float(b.x.min), C.float(b.y.min), C.float(b.z.min)},
+			bmax: [3]C.float{C.float(b.x.max), C.float(b.y.max), C.float(b.z.max)},
+		})
+		l, err := t.ref(v.left)
+		if err != nil {
+			return 0, err
+		}
+		r := l
+		if v.right != v.left { // one-element split: left == right (bvh.go:162-165)
+			if r, err = t.ref(v.right); err != nil {
+				return 0, err
+			}
+		}
+		t.nodes[me].left, t.nodes[me].right = l, r
+		return C.int32_t(me), nil
+	case *Sphere:
+		mi, err := t.material(v.Material)
+		if err != nil {
+			return 0, err
+		}
+		t.spheres = append(t.spheres, C.rtx_sphere{center: vec(v.Center), radius: C.float(v.Radius), material: mi})
+		return primRef(C.RTX_PRIM_SPHERE, len(t.spheres)-1), nil
+	case Quad, *Quad: // fields as NewQuad derived them (hittables.go:149-165)
+		q, ok := v.(Quad)
+		if !ok {
+			q = *v.(*Quad)
+		}
+		mi, err := t.material(q.material)
+		if err != nil {
+			return 0, err
+		}
+		t.quads = append(t.quads, C.rtx_quad{
+			q: vec(q.Q), material: mi, u: vec(q.u), d: C.float(q.D), v: vec(q.v), w: vec(q.w), normal: vec(q.normal),
+		})
+		return primRef(C.RTX_PRIM_QUAD, len(t.quads)-1), nil
+	default: // a World nested inside a BVH (hittables.go:55-72 as a child): the CPU path
+		return 0, errUnsupported
+	}
+}
+
+func rtxErr(rc C.int) error {
+	return fmt.Errorf("rtx error %d: %s", int(rc), C.GoString(C.rtx_last_error()))
+}
+
+// flatten: the tree Render receives as rtx.h tables; a plain *World gives one root per item
+// (its linear closest-hit scan, hittables.go:55-72).
+func flatten(world Hittable) (*gpuTables, error) {
+	t := &gpuTables{matIdx: map[Material]C.uint32_t{}, texIdx: map[Texture]C.uint32_t{}}
+	items := []Hittable{world}
+	if wl, ok := world.(*World); ok {
+		items = wl.hittables
+	}
+	for _, it := range items {
+		r, err := t.ref(it)
+		if err != nil {
+			return nil, err
+		}
+		t.roots = append(t.roots, r)
+	}
+	if len(t.roots) == 0 || len(t.materials) == 0 {
+		return nil, errUnsupported
+	}
+	return t, nil
+}
+
+// RenderGPU is Render (camera.go:180) on the MI355X path: same P3 bytes to writer, same
+// error return.  seed keys the counter-based RNG (the GPU path is reproducible); gpus > 1
+// row-interleaves the image over that many devices of this process (RCCL gather, rtx.h).
+func (c *Camera) RenderGPU(world Hittable, writer io.Writer, seed uint64, gpus int) error {
+	c.init() // Camera.init (idempotent, sync.Once): the derived state below (camera.go:128-165)
+	t, err := flatten(world)
+	if errors.Is(err, errUnsupported) {
+		return c.Render(world, writer)
+	}
+	if err != nil {
+		return err
+	}
+	var desc C.rtx_scene_desc
+	if len(t.nodes) > 0 {
+		desc.nodes, desc.n_nodes = &t.nodes[0], C.uint32_t(len(t.nodes))
+	}
+	desc.roots, desc.n_roots = &t.roots[0], C.uint32_t(len(t.roots))
+	if len(t.spheres) > 0 {
+		desc.spheres, desc.n_spheres = &t.spheres[0], C.uint32_t(len(t.spheres))
+	}
+	if len(t.quads) > 0 {
+		desc.quads, desc.n_quads = &t.quads[0], C.uint32_t(len(t.quads))
+	}
+	desc.materials, desc.n_materials = &t.materials[0], C.uint32_t(len(t.materials))
+	if len(t.textures) > 0 {
+		desc.textures, desc.n_textures = &t.textures[0], C.uint32_t(len(t.textures))
+	}
+	if len(t.texels) > 0 {
+		desc.texels, desc.n_texels = &t.texels[0], C.uint64_t(len(t.texels))
+	}
+	var scene *C.rtx_scene
+	if rc := C.rtx_scene_create(&desc, &scene); rc != 0 {
+		return rtxErr(rc)
+	}
+	// Destroying the last scene on a device also frees the library's sample scratch there, so
+	// nothing stays pinned in HBM after Render returns.
+	defer C.rtx_scene_destroy(scene)
+
+	w, h := int(c.imageWidth), int(c.imageHeight)
+	cam := C.rtx_camera{
+		image_width: C.uint32_t(w), image_height: C.uint32_t(h),
+		samples_per_pixel: C.uint32_t(c.samplesPerPixel), max_depth: C.uint32_t(max(c.bounceDepth, 0)),
+		center: vec(c.center), defocus_angle: C.float(c.defocusAngleRadians),
+		pixel00: vec(c.pixel00), pixel_du: vec(c.pixelDu), pixel_dv: vec(c.pixelDv),
+		defocus_disk_u: vec(c.defocusDiskU), defocus_disk_v: vec(c.defocusDiskV),
+		background: vec(c.background.GetColor()),
+	}
+	if gpus <= 1 { // render + the P3 text (header included) on the device: rtx_render_ppm
+		text := make([]byte, int(C.rtx_ppm_max_bytes(C.uint32_t(w), C.uint32_t(h))))
+		var n C.uint64_t
+		if rc := C.rtx_render_ppm(scene, &cam, C.uint64_t(seed), (*C.char)(unsafe.Pointer(&text[0])),
+			C.uint64_t(len(text)), &n, nil); rc != 0 {
+			return rtxErr(rc)
+		}
+		_, err := writer.Write(text[:int(n)])
+		return err
+	}
+	rgb := make([]float32, w*h*3) // several GPUs: float32 image gathered to device 0, text here
+	if rc := C.rtx_render(scene, &cam, C.uint64_t(seed), C.int(gpus), (*C.float)(unsafe.Pointer(&rgb[0])), nil); rc != 0 {
+		return rtxErr(rc)
+	}
+	var sb strings.Builder
+	sb.WriteString("P3\n" + strconv.Itoa(w) + " " + strconv.Itoa(h) + "\n255\n") // camera.go:183-188
+	for p := 0; p < w*h; p++ {                                                   // camera.go:212-215
+		col := NewVec3(rgb[3*p], rgb[3*p+1], rgb[3*p+2])
+		col.ToGamma2()
+		col.ToRGB()
+		sb.WriteString(col.String())
+		sb.WriteByte('\n')
+	}
+	_, err = io.WriteString(writer, sb.String())
+	return err
+}

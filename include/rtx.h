@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define RTX_ABI_VERSION 3
+#define RTX_ABI_VERSION 4
 
 /* ---- status codes ------------------------------------------------------------ */
 enum {
@@ -108,13 +108,25 @@ typedef struct rtx_material { /* 32 B */
 enum {
     RTX_TEX_SOLID = 0,     /* even[3] = colour                       materials.go:151-163 */
     RTX_TEX_CHECKERED = 1, /* scale, even[3], odd[3]                 materials.go:121-145 */
-    RTX_TEX_IMAGE = 2,     /* width x height RGBA8 texels at texel_offset (row-major,
-                              y down, as image.RGBA.At)             materials.go:165-193 */
+    RTX_TEX_IMAGE = 2,     /* width x height RGBA16 texels at texel_offset (row-major,
+                              y down), then ONE border texel: see below materials.go:165-193 */
     RTX_TEX_NOISE = 3      /* Perlin: scale, and RTX_NOISE_TEXELS words at texel_offset:
                               256 gradient vectors (x, y, z float32 bits), then permX,
                               permY, permZ (256 indices each)        materials.go:195-295 */
 };
 #define RTX_NOISE_TEXELS 1536u
+/* RTX_TEX_IMAGE texels are Go's `img.At(x, y).RGBA()` (materials.go:188), 16 bits per
+ * channel, two uint32 words per texel: word 0 = r | g << 16, word 1 = b | a << 16.
+ * The texel at index width*height (after the raster) is the colour At() returns OUTSIDE
+ * the image's bounds, which GetTexture reads when int(u*Dx) == Dx or int(v*Dy) == Dy
+ * (u == 1, v == 0) or a NaN coordinate (int(NaN) = MinInt64 on amd64): for the
+ * *image.YCbCr that jpeg.Decode returns that is color.YCbCr{} = (0, 34678, 0)
+ * (image/ycbcr.go YCbCrAt, image/color/ycbcr.go RGBA), for *image.RGBA it is 0.
+ * The host fills it with At(Bounds().Max.X, Bounds().Min.Y).RGBA().  Exact for every
+ * image whose Bounds().Min is (0, 0) (jpeg.Decode, image.New*); texel_offset is even
+ * and n_texels counts uint32 words.  Texels are fetched as
+ * float32(r16) * float32(1/65535) (materials.go:187-191).                        */
+#define RTX_IMAGE_TEXEL_WORDS 2u
 typedef struct rtx_texture { /* 48 B */
     uint32_t type;
     float scale;
@@ -141,7 +153,7 @@ typedef struct rtx_scene_desc {
     uint32_t n_materials;
     uint32_t n_textures;
     const rtx_texture* textures;
-    const uint32_t* texels; /* RGBA8, r in the low byte */
+    const uint32_t* texels; /* image RGBA16 texels and Perlin tables (uint32 words) */
     uint64_t n_texels;
 } rtx_scene_desc;
 
@@ -191,42 +203,32 @@ typedef struct rtx_stats {
     uint64_t hits;         /* segments that hit a primitive                          */
     uint64_t texel_fetches;
     uint64_t rng_draws;
-    double kernel_ms;      /* device time of the render kernel(s), HIP events       */
-    double gather_ms;      /* multi-GPU gather (rtx_render with n_gpus > 1)         */
-    /* scheduling counters of the persistent kernels (RTX_FLAG_COUNTERS):            */
+    double kernel_ms;      /* device time of the render kernels, HIP events on the render
+                              stream (n_gpus > 1: the slowest device)                */
+    double gather_ms;      /* rtx_render with n_gpus > 1: the RCCL gather of the bands to
+                              device 0 plus the de-interleave, HIP events on device 0  */
+    /* scheduling counters of the persistent kernel (RTX_FLAG_COUNTERS):             */
     uint64_t wave_iters;   /* traversal-loop iterations, summed over waves           */
     uint64_t lane_steps;   /* lanes stepping a BVH entry, summed over iterations     */
     uint64_t shade_phases; /* shading phases, summed over waves                      */
     uint64_t shade_lanes;  /* lanes shaded or claiming, summed over shading phases   */
-    uint64_t trav_cycles;  /* v1: shader cycles (s_memtime) in traversal, summed over waves */
-    uint64_t shade_cycles; /* v1: shader cycles in shading phases, summed over waves  */
-    uint64_t idle_lanes;   /* v1: lanes whose pixel is finished, summed over iterations */
-    uint64_t cache_hits;   /* v3, scenes too big for LDS: entries (of node_visits + prim_tests and
+    uint64_t trav_cycles;  /* shader cycles (s_memtime) in traversal, summed over waves */
+    uint64_t shade_cycles; /* shader cycles in shading phases, summed over waves      */
+    uint64_t idle_lanes;   /* lanes with no item left, summed over iterations         */
+    uint64_t cache_hits;   /* scenes too big for LDS: entries (of node_visits + prim_tests and
                               the steps on the end sentinel) read from the LDS cache of the top
                               levels */
+    uint64_t sample_chunks; /* launches of the render kernel: the samples of every pixel run in
+                               chunks that fit the per-device colour scratch (always filled) */
 } rtx_stats;
 
 #define RTX_FLAG_COUNTERS 1u /* count work units (separate kernel instantiation) */
-#define RTX_FLAG_KERNEL_V0 2u /* A/B: the first thread-per-pixel kernel instead of the
-                                 persistent wave kernel (identical output) */
-#define RTX_FLAG_NO_LDS 4u    /* A/B: read the scene from global memory even if it fits LDS */
-#define RTX_FLAG_KERNEL_POOL 8u /* A/B: the pixel-pool persistent kernel (v2) instead of
-                                   the default one-pixel-per-lane wave kernel (v1) */
-#define RTX_FLAG_POOL4 16u      /* A/B: v2 with 4 instead of 2 pixel chunks per wave */
-#define RTX_FLAG_KERNEL_ITEMS 32u /* v3 (the default schedule when no other is chosen):
-                                     (pixel, sample) items, colours stored in HBM and summed
-                                     in sample order afterwards (RTX_SCRATCH_MB bounds the
-                                     per-device scratch, default 16 GiB; identical output) */
-#define RTX_FLAG_KERNEL_V1 64u    /* A/B: v1, one 8x8 tile per wave, one lane per pixel */
+#define RTX_FLAG_NO_LDS 4u   /* A/B: read the scene from global memory even if it fits LDS */
+/* Bits 2u, 8u, 16u, 32u, 64u and RTX_FLAG_WAVE_GEOM (bits 24-26) selected the A/B schedules
+ * v0/v1/v2 of ABI 3; they were removed in ABI 4 and are ignored. */
 /* Tuning: lanes of a wave that must wait before it shades (1..64; 0 = default, or the
  * RTX_SHADE_THRESH environment variable). */
 #define RTX_FLAG_SHADE_THRESH(n) (((uint32_t)(n)&0x7Fu) << 8)
-/* Tuning: variant of the wave kernel (identical output): 0 = one 8x8 tile per wave,
- * 4 waves per block, 3 BVH steps per wave vote (default); 1 = persistent waves that
- * claim tiles; 2 = persistent, 1 step per vote; 3 = persistent, 4 steps; 4 = persistent,
- * 8 waves per block; 5 = as 4 with a >= 8 waves/SIMD register budget; 6 = persistent,
- * 1 wave per block. */
-#define RTX_FLAG_WAVE_GEOM(n) (((uint32_t)(n)&7u) << 24)
 
 typedef struct rtx_scene rtx_scene;
 
@@ -257,9 +259,22 @@ uint64_t rtx_scene_device_bytes(const rtx_scene* scene);
  * of the image, averaged over samples_per_pixel, linear (pre-gamma) float32 RGB,
  * row-major, rows top to bottom, into caller-owned host memory out_rgb[W*H*3].
  * n_gpus > 1 row-interleaves the image over devices 0..n_gpus-1 of this process
- * and gathers the bands to device 0 with RCCL before the copy to the host.       */
+ * (rank d renders rows y = d, d + n, ...), gathers the equal-sized bands to device 0
+ * with one RCCL ncclGather over xGMI (communicators from ncclCommInitAll, cached per
+ * device set; librccl is loaded on first use), de-interleaves them on device 0 and
+ * copies the image to the host.  RTX_ERR_RCCL if RCCL cannot be loaded or fails.    */
 int rtx_render(rtx_scene* scene, const rtx_camera* cam, uint64_t seed, int n_gpus, float* out_rgb,
                rtx_stats* stats);
+
+/* Free the device memory the library keeps between renders on `device` (-1: every
+ * device): the per-device sample-colour scratch (up to RTX_SCRATCH_MB, 12 B per
+ * sample of a chunk) and the cached RCCL communicators.  Scenes are not affected;
+ * the next render allocates again.  The scratch of a device is also freed when the
+ * last scene with a copy on that device is destroyed.  Blocking.                   */
+int rtx_release_device_memory(int device);
+
+/* Bytes of the per-device scratch currently held on `device` (for tests and tools). */
+uint64_t rtx_device_scratch_bytes(int device);
 
 /* Render one region/shard on the CURRENT device into device memory d_out (float32
  * RGB, compacted shard rows, see rtx_region) on the given HIP stream (hipStream_t,

@@ -19,13 +19,23 @@ extern "C" {
 typedef struct rtxhost_scene rtxhost_scene;
 
 /* Build a scene of main.go by name: "random_spheres" (main.go:227-289),
- * "stress_100k" (config 4), "earth_dielectric" (config 5), "earth" (main.go:80-104).
+ * "stress_100k" (config 4), "earth_dielectric" (config 5), "earth" (main.go:80-104; its
+ * map as jpeg.Decode's *image.YCbCr), "earth_rgba" (the same map as an *image.RGBA),
+ * "earth_far_side" (main.go's earth seen from z = -12), "quad_demo", "cornell_box",
+ * "perlin_demo", "simple_light_demo".
  * The BVH is built by the NewBVH restatement (bvh.go:142-185) and flattened. */
 int rtxhost_build_scene(const char* name, uint64_t seed, rtxhost_scene** out);
 void rtxhost_scene_free(rtxhost_scene* s);
 
 /* The flattened tables (valid until rtxhost_scene_free). */
 const rtx_scene_desc* rtxhost_scene_desc(const rtxhost_scene* s);
+
+/* The planes of SyntheticEarth(seed, w, h), the *image.YCbCr 4:2:0 map the earth scenes
+ * texture with: y[w*h], cb and cr [((w+1)/2) * ((h+1)/2)] each (strides w and (w+1)/2). */
+int rtxhost_synthetic_earth_ycbcr(uint64_t seed, int32_t w, int32_t h, uint8_t* y, uint8_t* cb, uint8_t* cr);
+
+/* color.YCbCr{y, cb, cr}.RGBA() as the mirror computes it: out = r, g, b, a. */
+void rtxhost_ycbcr_rgba(uint8_t y, uint8_t cb, uint8_t cr, uint32_t out[4]);
 
 /* The scene's camera (NewCamera with main.go's options), with overrides; a value
  * <= 0 keeps the scene's own setting. */

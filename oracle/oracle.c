@@ -648,7 +648,7 @@ static vec3 texture_value(const ctx_t* cx, uint32_t ti, float u, float v, vec3 p
         return v3(t->odd[0], t->odd[1], t->odd[2]);
     }
     case RTX_TEX_IMAGE: {                                                   /* :175-193 */
-        if ((int32_t)t->height <= 0) return v3(0.0f, 1.0f, 1.0f);
+        if ((int32_t)t->height <= 0) return v3(0.0f, 1.0f, 1.0f);          /* Dy() <= 0 */
         /* Clamp(0, 1, x) passes NaN through (math.go:20-28). */
         float uu = u < 0.0f ? 0.0f : (u > 1.0f ? 1.0f : u);
         float vc = v < 0.0f ? 0.0f : (v > 1.0f ? 1.0f : v);
@@ -659,13 +659,18 @@ static vec3 texture_value(const ctx_t* cx, uint32_t ti, float u, float v, vec3 p
         /* int(float32): truncation; NaN/out-of-range -> 0x8000000000000000 on amd64. */
         int64_t i = isnan(fi) ? INT64_MIN : (int64_t)fi;
         int64_t j = isnan(fj) ? INT64_MIN : (int64_t)fj;
-        /* image.RGBA.At outside Rect returns color.RGBA{} = black. */
-        if (i < 0 || j < 0 || i >= (int64_t)t->width || j >= (int64_t)t->height) return v3(0.0f, 0.0f, 0.0f);
-        uint32_t px = cx->s->texels[t->texel_offset + (uint64_t)j * t->width + (uint64_t)i];
-        /* color.RGBA.RGBA(): r |= r << 8; colScale = float32(1.0 / 65535.0). */
+        /* At(i, j) outside Bounds = [0, Dx) x [0, Dy): the image type's zero colour, held
+         * as the border texel after the raster (rtx.h RTX_TEX_IMAGE). */
+        uint64_t idx = (uint64_t)t->width * t->height;
+        if (i >= 0 && j >= 0 && i < (int64_t)t->width && j < (int64_t)t->height)
+            idx = (uint64_t)j * t->width + (uint64_t)i;
+        else
+            cx->c->texel_border++;
+        const uint32_t* px = &cx->s->texels[t->texel_offset + 2 * idx];
+        /* r, g, b, _ := pixel.RGBA(); colScale = float32(1.0 / 65535.0). */
         const float col_scale = 1.0f / 65535.0f;
-        uint32_t r8 = px & 0xFFu, g8 = (px >> 8) & 0xFFu, b8 = (px >> 16) & 0xFFu;
-        return v3((float)(r8 * 257u) * col_scale, (float)(g8 * 257u) * col_scale, (float)(b8 * 257u) * col_scale);
+        return v3((float)(px[0] & 0xFFFFu) * col_scale, (float)(px[0] >> 16) * col_scale,
+                  (float)(px[1] & 0xFFFFu) * col_scale);
     }
     case RTX_TEX_NOISE: {                                                   /* :267-288 */
         const float g = noise_texture(&cx->s->texels[t->texel_offset], t->scale, p);
@@ -855,8 +860,13 @@ static int scene_supported(const rtx_scene_desc* s) {
     if (!s || !s->roots || s->n_roots == 0) return 0;
     for (uint32_t i = 0; i < s->n_materials; ++i)
         if (s->materials[i].type > RTX_MAT_DIFFUSE_LIGHT) return 0;
-    for (uint32_t i = 0; i < s->n_textures; ++i)
-        if (s->textures[i].type > RTX_TEX_NOISE) return 0;
+    for (uint32_t i = 0; i < s->n_textures; ++i) {
+        const rtx_texture* t = &s->textures[i];
+        if (t->type > RTX_TEX_NOISE) return 0;
+        if (t->type == RTX_TEX_IMAGE && (int32_t)t->height > 0 &&
+            (uint64_t)t->texel_offset + 2ull * ((uint64_t)t->width * t->height + 1) > s->n_texels)
+            return 0; /* RGBA16 raster + border texel (rtx.h) */
+    }
     if (s->n_quads && !s->quads) return 0;
     return 1;
 }
@@ -899,6 +909,7 @@ static void* worker(void* arg) {
     jb->total.prim_tests += local.prim_tests;
     jb->total.hits += local.hits;
     jb->total.texel_fetches += local.texel_fetches;
+    jb->total.texel_border += local.texel_border;
     jb->total.rng_draws += local.rng_draws;
     pthread_mutex_unlock(&jb->mu);
     return NULL;
@@ -1224,4 +1235,59 @@ void oracle_scene_free(oracle_scene* s) {
     free(s->textures);
     free(s->sphere_box);
     free(s);
+}
+
+/* ============================================================================
+ * Go's image.YCbCr (image/ycbcr.go) and color.YCbCr.RGBA (image/color/ycbcr.go),
+ * Go 1.21 — the *image.YCbCr jpeg.Decode returns for the earth texture (file.go:20-28,
+ * main.go:97-100), restated independently of the host mirror.
+ * ========================================================================== */
+void oracle_ycbcr_rgba(uint8_t y, uint8_t cb, uint8_t cr, uint32_t out[3]) {
+    const int32_t yy1 = (int32_t)y * 0x10101;   /* 65536*Y' + adjustment Y'*0x0101 */
+    const int32_t cb1 = (int32_t)cb - 128;
+    const int32_t cr1 = (int32_t)cr - 128;
+    int32_t v[3];
+    v[0] = yy1 + 91881 * cr1;
+    v[1] = yy1 - 22554 * cb1 - 46802 * cr1;
+    v[2] = yy1 + 116130 * cb1;
+    for (int k = 0; k < 3; ++k) {
+        if (((uint32_t)v[k] & 0xff000000u) == 0)
+            out[k] = (uint32_t)(v[k] >> 8);
+        else
+            out[k] = (uint32_t)(~(v[k] >> 31)) & 0xffffu;
+    }
+}
+
+void oracle_ycbcr_rgba_all(uint32_t* out) {
+    for (uint32_t k = 0; k < (1u << 24); ++k)
+        oracle_ycbcr_rgba((uint8_t)(k >> 16), (uint8_t)(k >> 8), (uint8_t)k, &out[3 * (size_t)k]);
+}
+
+int oracle_ycbcr_texels(const uint8_t* Y, const uint8_t* Cb, const uint8_t* Cr, int64_t w, int64_t h,
+                        int64_t ystride, int64_t cstride, int ratio, uint32_t* out) {
+    if (w <= 0 || h <= 0) return -1;
+    for (int64_t y = 0; y < h; ++y) {
+        for (int64_t x = 0; x < w; ++x) {
+            int64_t ci;
+            switch (ratio) { /* COffset, Rect.Min = (0, 0) */
+            case 1: ci = y * cstride + x / 2; break;           /* 4:2:2 */
+            case 2: ci = (y / 2) * cstride + x / 2; break;     /* 4:2:0 */
+            case 3: ci = (y / 2) * cstride + x; break;         /* 4:4:0 */
+            case 4: ci = y * cstride + x / 4; break;           /* 4:1:1 */
+            case 5: ci = (y / 2) * cstride + x / 4; break;     /* 4:1:0 */
+            default: ci = y * cstride + x; break;              /* 4:4:4 */
+            }
+            uint32_t c[3];
+            oracle_ycbcr_rgba(Y[y * ystride + x], Cb[ci], Cr[ci], c);
+            uint32_t* o = &out[2 * (size_t)(y * w + x)];
+            o[0] = c[0] | c[1] << 16;
+            o[1] = c[2] | 0xffffu << 16;
+        }
+    }
+    uint32_t c[3]; /* outside Bounds: color.YCbCr{} */
+    oracle_ycbcr_rgba(0, 0, 0, c);
+    uint32_t* o = &out[2 * (size_t)(w * h)];
+    o[0] = c[0] | c[1] << 16;
+    o[1] = c[2] | 0xffffu << 16;
+    return 0;
 }

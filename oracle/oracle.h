@@ -46,6 +46,7 @@ typedef struct oracle_counters {
     uint64_t hits;
     uint64_t texel_fetches;
     uint64_t rng_draws;
+    uint64_t texel_border;    /* image fetches outside the bounds (the border texel)   */
 } oracle_counters;
 
 /* Philox4x32-10 (Salmon et al., SC'11; Random123). */
@@ -103,6 +104,16 @@ double oracle_go_acos(double x);
 double oracle_go_sin(double x); /* Go 1.21 math.Sin (sin.go + trig_reduce.go) */
 /* NoiseTexture.GetTexture (materials.go:280-288) over an RTX_NOISE_TEXELS table. */
 float oracle_noise_texture(const uint32_t* tab, float scale, const float p[3]);
+
+/* color.YCbCr{y, cb, cr}.RGBA() (Go image/color/ycbcr.go): out = r, g, b (16-bit). */
+void oracle_ycbcr_rgba(uint8_t y, uint8_t cb, uint8_t cr, uint32_t out[3]);
+/* ... for every (y, cb, cr), k = y << 16 | cb << 8 | cr: out[3 * k + c] (3 * 2^24 words). */
+void oracle_ycbcr_rgba_all(uint32_t* out);
+/* The RTX_TEX_IMAGE texels (RGBA16 raster + border) of an *image.YCbCr with Bounds
+ * (0,0)-(w,h): At(x, y).RGBA() via YCbCrAt / COffset (image/ycbcr.go); ratio 0..5 =
+ * 4:4:4, 4:2:2, 4:2:0, 4:4:0, 4:1:1, 4:1:0.  out: 2 * (w * h + 1) words. */
+int oracle_ycbcr_texels(const uint8_t* Y, const uint8_t* Cb, const uint8_t* Cr, int64_t w, int64_t h,
+                        int64_t ystride, int64_t cstride, int ratio, uint32_t* out);
 
 /* Independent recompute of rtx_region_rows. */
 uint32_t oracle_region_rows(const rtx_region* r);

@@ -5,7 +5,9 @@
 // threaded pre-order device layout (rtx_layout.h), keeps it resident in HBM per
 // device, and launches the megakernel.  Errors are returned as codes with a
 // thread-local message; nothing throws across the ABI.
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>  // types only: librccl is loaded on first use (rccl_api)
 
 #include <algorithm>
 #include <cstdarg>
@@ -58,16 +60,95 @@ struct DeviceCopy {
     uint32_t hot = 0;  // entries stored first and cached in LDS by v3 (scenes too big for the LDS copy)
 };
 
-// v3 sample-colour scratch, one per device, shared by all scenes (grown on demand and
-// kept for the process).  `last` marks its latest use, so a render on another stream
-// waits for the previous one before reusing it.
+// Sample-colour scratch, one per device, shared by all scenes (grown on demand).  `last`
+// marks its latest use, so a render on another stream waits for the previous one before
+// reusing it — which also serialises every render on a device on the GPU (the per-scene
+// counters and unit queue rely on that).  `scenes` counts the scene copies on the
+// device: the last rtx_scene_destroy there frees the scratch (rtx_release_device_memory
+// frees it at any time).
 struct Scratch {
     float* ptr = nullptr;
     size_t bytes = 0;
     hipEvent_t last = nullptr;
+    int scenes = 0;
 };
 std::mutex g_scratch_mu;
 std::map<int, Scratch> g_scratch;
+
+// The PPM encoder's per-device scratch (line lengths and offsets), reused across calls;
+// g_ppm_mu is held for a whole (blocking) encode.
+struct PpmScratch {
+    void* ptr = nullptr;
+    size_t bytes = 0;
+};
+std::mutex g_ppm_mu;
+std::map<int, PpmScratch> g_ppm;
+
+// Free a device's scratch buffers (g_scratch_mu held).
+void release_scratch_locked(int device) {
+    auto it = g_scratch.find(device);
+    if (it == g_scratch.end()) return;
+    Scratch& sc = it->second;
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    if (hipSetDevice(device) == hipSuccess) {
+        if (sc.last) (void)hipEventSynchronize(sc.last);
+        if (sc.ptr) (void)hipFree(sc.ptr);
+        if (sc.last) (void)hipEventDestroy(sc.last);
+    }
+    (void)hipSetDevice(cur);
+    const int scenes = sc.scenes;
+    sc = Scratch{};
+    sc.scenes = scenes;
+}
+
+// ---- RCCL, loaded on first use (rtx_render with n_gpus > 1) --------------------------
+struct RcclApi {
+    bool tried = false, ok = false;
+    std::string err;
+    ncclResult_t (*CommInitAll)(ncclComm_t*, int, const int*) = nullptr;
+    ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
+    ncclResult_t (*GroupStart)() = nullptr;
+    ncclResult_t (*GroupEnd)() = nullptr;
+    ncclResult_t (*Gather)(const void*, void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    const char* (*GetErrorString)(ncclResult_t) = nullptr;
+};
+std::mutex g_rccl_mu;
+RcclApi g_rccl;
+std::map<int, std::vector<ncclComm_t>> g_comms;  // devices 0..n-1 -> communicators (ncclCommInitAll)
+
+const RcclApi* rccl_api() {  // g_rccl_mu held
+    if (g_rccl.tried) return g_rccl.ok ? &g_rccl : nullptr;
+    g_rccl.tried = true;
+    void* h = nullptr;
+    for (const char* name : {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"})
+        if ((h = dlopen(name, RTLD_NOW | RTLD_GLOBAL))) break;
+    if (!h) {
+        g_rccl.err = std::string("cannot load librccl: ") + dlerror();
+        return nullptr;
+    }
+    bool ok = true;
+    auto sym = [&](auto& fn, const char* name) {
+        fn = reinterpret_cast<std::remove_reference_t<decltype(fn)>>(dlsym(h, name));
+        ok = ok && fn != nullptr;
+    };
+    sym(g_rccl.CommInitAll, "ncclCommInitAll");
+    sym(g_rccl.CommDestroy, "ncclCommDestroy");
+    sym(g_rccl.GroupStart, "ncclGroupStart");
+    sym(g_rccl.GroupEnd, "ncclGroupEnd");
+    sym(g_rccl.Gather, "ncclGather");
+    sym(g_rccl.GetErrorString, "ncclGetErrorString");
+    if (!ok) g_rccl.err = "librccl lacks ncclGather / ncclCommInitAll";
+    g_rccl.ok = ok;
+    return ok ? &g_rccl : nullptr;
+}
+
+void release_comms_locked() {  // g_rccl_mu held
+    for (auto& kv : g_comms)
+        for (ncclComm_t c : kv.second)
+            if (c && g_rccl.CommDestroy) (void)g_rccl.CommDestroy(c);
+    g_comms.clear();
+}
 
 }  // namespace
 
@@ -183,6 +264,12 @@ int emit(const rtx_scene_desc* d, int32_t root, std::vector<rtx_entry>& out) {
 
 uint32_t env_knob(const char* name, long dflt, long lo, long hi);
 
+void free_copy(DeviceCopy& c);
+
+int upload_copy(rtx_scene* s, DeviceCopy& c);
+
+// The scene's copy on `device`, uploaded on first use; a failed upload frees what it had
+// allocated.  Every copy is counted in the device's Scratch::scenes.
 int ensure_device(rtx_scene* s, int device, DeviceCopy** out) {
     auto it = s->copies.find(device);
     if (it != s->copies.end()) {
@@ -192,6 +279,20 @@ int ensure_device(rtx_scene* s, int device, DeviceCopy** out) {
     DeviceCopy c;
     c.device = device;
     HIP_TRY(hipSetDevice(device));
+    if (int rc = upload_copy(s, c)) {
+        free_copy(c);
+        return rc;
+    }
+    {
+        std::lock_guard<std::mutex> lk(g_scratch_mu);
+        ++g_scratch[device].scenes;
+    }
+    auto res = s->copies.emplace(device, c);
+    *out = &res.first->second;
+    return RTX_OK;
+}
+
+int upload_copy(rtx_scene* s, DeviceCopy& c) {
     HIP_TRY(hipMalloc(&c.entries, (s->entries.size() + 1) * sizeof(rtx_entry) + s->quadtab.size() * sizeof(float)));
     {  // device layout: all 'a' halves, then all 'b' halves (rtxd::SceneRef), each ending
        // with the sentinel entry (rtx_layout.h).  Every entry names its successor (node: next
@@ -288,13 +389,12 @@ int ensure_device(rtx_scene* s, int device, DeviceCopy** out) {
     HIP_TRY(hipMalloc(&c.counters, 16 * sizeof(unsigned long long)));
     HIP_TRY(hipEventCreate(&c.ev0));
     HIP_TRY(hipEventCreate(&c.ev1));
-    auto res = s->copies.emplace(device, c);
-    *out = &res.first->second;
     return RTX_OK;
 }
 
 void free_copy(DeviceCopy& c) {
     if (hipSetDevice(c.device) != hipSuccess) return;
+    (void)hipDeviceSynchronize();  // no render of this copy still running
     (void)hipFree(c.entries);
     (void)hipFree(c.materials);
     (void)hipFree(c.textures);
@@ -302,6 +402,14 @@ void free_copy(DeviceCopy& c) {
     (void)hipFree(c.counters);
     if (c.ev0) (void)hipEventDestroy(c.ev0);
     if (c.ev1) (void)hipEventDestroy(c.ev1);
+}
+
+// Free a scene's copy; the last copy on a device also frees the device's scratch.
+void drop_copy(DeviceCopy& c) {
+    free_copy(c);
+    std::lock_guard<std::mutex> lk(g_scratch_mu);
+    Scratch& sc = g_scratch[c.device];
+    if (sc.scenes > 0 && --sc.scenes == 0) release_scratch_locked(c.device);
 }
 
 int check_camera(const rtx_camera* cam) {
@@ -390,25 +498,28 @@ rtxd::Params make_params(const rtx_scene* s, const DeviceCopy* c, const rtx_came
 }
 
 // Enqueue one region on the current device, bracketed by HIP events on `stream`.
+// *chunks receives the number of sample chunks (render kernel launches).
 int enqueue_on(rtx_scene* s, DeviceCopy* c, const rtx_camera* cam, uint64_t seed, const rtx_region* r, float* d_out,
-               hipStream_t stream, uint32_t flags, bool timed) {
+               hipStream_t stream, uint32_t flags, bool timed, uint32_t* chunks) {
     rtxd::Params p = make_params(s, c, cam, seed, r, d_out);
     const uint32_t th = (flags >> 8) & 0x7Fu;  // RTX_FLAG_SHADE_THRESH(n) override
     if (th) p.shade_thresh = th > 64 ? 64 : th;
-    Scratch* scr = nullptr;
-    std::unique_lock<std::mutex> scr_lock(g_scratch_mu, std::defer_lock);
-    if (rtxd::uses_items(p, flags)) {
-        // v3 scratch: up to RTX_SCRATCH_MB (default 16 GiB of the 288 GB HBM) of sample
-        // colours, 12 B each; the samples are rendered in chunks that fit.
+    *chunks = 0;
+    std::unique_lock<std::mutex> scr_lock(g_scratch_mu);
+    Scratch* scr = &g_scratch[c->device];
+    if (!scr->last) HIP_TRY(hipEventCreateWithFlags(&scr->last, hipEventDisableTiming));
+    // Every render on this device waits for the previous one (the shared scratch, and the
+    // scene's counters / unit queue, are reused).
+    HIP_TRY(hipStreamWaitEvent(stream, scr->last, 0));
+    if (p.width > 0 && p.rows > 0) {
+        // Sample scratch: up to RTX_SCRATCH_MB (default 16 GiB of the 288 GB HBM) of sample
+        // colours, 12 B each; the samples run in chunks that fit.
         const uint64_t per_sample = (uint64_t)p.width * p.rows * 12;
         const uint64_t budget = (uint64_t)env_knob("RTX_SCRATCH_MB", 16384, 1, 1 << 20) << 20;
-        uint64_t chunk = per_sample ? budget / per_sample : 0;
+        uint64_t chunk = budget / per_sample;
         if (chunk > cam->samples_per_pixel) chunk = cam->samples_per_pixel;
         if (chunk < 1) return fail(RTX_ERR_OOM, "RTX_SCRATCH_MB too small for one sample of the region");
         const size_t need = (size_t)(chunk * per_sample);
-        scr_lock.lock();
-        scr = &g_scratch[c->device];
-        if (!scr->last) HIP_TRY(hipEventCreateWithFlags(&scr->last, hipEventDisableTiming));
         if (scr->bytes < need) {
             HIP_TRY(hipEventSynchronize(scr->last));
             if (scr->ptr) HIP_TRY(hipFree(scr->ptr));
@@ -417,25 +528,26 @@ int enqueue_on(rtx_scene* s, DeviceCopy* c, const rtx_camera* cam, uint64_t seed
             HIP_TRY(hipMalloc(&scr->ptr, need));
             scr->bytes = need;
         }
-        HIP_TRY(hipStreamWaitEvent(stream, scr->last, 0));
         p.scratch = scr->ptr;
         p.kn = (uint32_t)chunk;
+        *chunks = (uint32_t)((cam->samples_per_pixel + chunk - 1) / chunk);
         p.sub = env_knob("RTX_ITEM_SUB", 0, 0, 4096);  // 0: chosen per chunk by launch_items
         p.item_waves = env_knob("RTX_ITEM_WAVES", 8, 4, 8) >= 8 ? 8u : 4u;
         p.grid_pct = env_knob("RTX_ITEM_GRID", 100, 1, 100);
         p.debug_launch = env_knob("RTX_DEBUG_LAUNCH", 0, 0, 1);
         p.prim_batch = env_knob("RTX_PRIM_BATCH", 16, 1, 65);  // 65: primitive tests only when no node is left
     }
-    if (flags & RTX_FLAG_COUNTERS) HIP_TRY(hipMemsetAsync(c->counters, 0, 16 * sizeof(unsigned long long), stream));
+    // every stats slot, the unit queue head and the watchdog flag start at 0 for every render
+    HIP_TRY(hipMemsetAsync(c->counters, 0, 16 * sizeof(unsigned long long), stream));
     if (timed) HIP_TRY(hipEventRecord(c->ev0, stream));
     HIP_TRY(rtxd::launch_render(p, flags, stream));
-    if (scr) HIP_TRY(hipEventRecord(scr->last, stream));
     if (timed) HIP_TRY(hipEventRecord(c->ev1, stream));
+    HIP_TRY(hipEventRecord(scr->last, stream));
     return RTX_OK;
 }
 
 // Wait for an enqueue_on(timed=true) and read its time and counters.
-int collect_on(DeviceCopy* c, bool count, uint64_t samples, rtx_stats* st) {
+int collect_on(DeviceCopy* c, bool count, uint64_t samples, uint32_t chunks, rtx_stats* st) {
     HIP_TRY(hipEventSynchronize(c->ev1));
     float ms = 0.0f;
     HIP_TRY(hipEventElapsedTime(&ms, c->ev0, c->ev1));
@@ -458,6 +570,7 @@ int collect_on(DeviceCopy* c, bool count, uint64_t samples, rtx_stats* st) {
     st->shade_cycles = h[13];
     st->idle_lanes = h[14];
     st->cache_hits = h[15];
+    st->sample_chunks = chunks;
     st->kernel_ms = ms;
     return RTX_OK;
 }
@@ -492,9 +605,11 @@ int validate_tables(const rtx_scene_desc* d) {
                     return fail(RTX_ERR_INVALID_ARG, "texture %u: Perlin permutation entry out of range", i);
         }
         if (t.type > RTX_TEX_NOISE) return fail(RTX_ERR_INVALID_ARG, "texture %u: unknown type %u", i, t.type);
-        if (t.type == RTX_TEX_IMAGE && (int32_t)t.height > 0 &&
-            (uint64_t)t.texel_offset + (uint64_t)t.width * t.height > d->n_texels)
-            return fail(RTX_ERR_INVALID_ARG, "texture %u texels out of range", i);
+        if (t.type == RTX_TEX_IMAGE && (int32_t)t.height > 0) {  // RGBA16 raster + border texel (rtx.h)
+            if (t.texel_offset & 1u) return fail(RTX_ERR_INVALID_ARG, "texture %u: texel_offset must be even", i);
+            if ((uint64_t)t.texel_offset + RTX_IMAGE_TEXEL_WORDS * ((uint64_t)t.width * t.height + 1) > d->n_texels)
+                return fail(RTX_ERR_INVALID_ARG, "texture %u texels out of range", i);
+        }
     }
     return RTX_OK;
 }
@@ -526,12 +641,42 @@ int finish_scene(rtx_scene* s, const rtx_scene_desc* d, rtx_scene** out) {
     }
     DeviceCopy* c = nullptr;
     if (int rc = ensure_device(s, cur, &c)) {
-        for (auto& kv : s->copies) free_copy(kv.second);
+        for (auto& kv : s->copies) drop_copy(kv.second);
         delete s;
         return rc;
     }
     *out = s;
     return RTX_OK;
+}
+
+// rtx_render's band assembly on device 0: the RCCL-gathered bands g[d][r][:] (n bands
+// of R rows, row_floats = 3 W floats each; band d holds image rows y = d + r n) -> img[y][:].
+__global__ __launch_bounds__(256) void deinterleave_bands(const float* __restrict__ g, float* __restrict__ img,
+                                                          uint32_t n, uint32_t R, uint32_t H, uint32_t row_floats) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= (uint64_t)H * row_floats) return;
+    const uint32_t y = (uint32_t)(i / row_floats), x = (uint32_t)(i % row_floats);
+    img[i] = g[((uint64_t)(y % n) * R + y / n) * row_floats + x];
+}
+
+void add_stats(rtx_stats* acc, const rtx_stats& s) {
+    acc->samples += s.samples;
+    acc->segments += s.segments;
+    acc->node_visits += s.node_visits;
+    acc->prim_tests += s.prim_tests;
+    acc->hits += s.hits;
+    acc->texel_fetches += s.texel_fetches;
+    acc->rng_draws += s.rng_draws;
+    acc->kernel_ms = std::max(acc->kernel_ms, s.kernel_ms);
+    acc->wave_iters += s.wave_iters;
+    acc->lane_steps += s.lane_steps;
+    acc->shade_phases += s.shade_phases;
+    acc->shade_lanes += s.shade_lanes;
+    acc->trav_cycles += s.trav_cycles;
+    acc->shade_cycles += s.shade_cycles;
+    acc->idle_lanes += s.idle_lanes;
+    acc->cache_hits += s.cache_hits;
+    acc->sample_chunks = std::max(acc->sample_chunks, s.sample_chunks);
 }
 
 }  // namespace
@@ -541,7 +686,8 @@ extern "C" {
 int rtx_version(void) { return RTX_ABI_VERSION; }
 
 const char* rtx_build_info(void) {
-    return "librtx gfx950 megakernel v1 (persistent wave loop, LDS scene, threaded pre-order BVH); built " __DATE__ " " __TIME__;
+    return "librtx gfx950 megakernel (ABI 4: persistent (pixel, sample) item waves, LDS scene, threaded pre-order BVH, "
+           "RGBA16 image texels, RCCL band gather); built " __DATE__ " " __TIME__;
 }
 
 const char* rtx_last_error(void) { return g_last_error.c_str(); }
@@ -615,7 +761,7 @@ void rtx_scene_destroy(rtx_scene* s) {
     if (!s) return;
     int cur = 0;
     (void)hipGetDevice(&cur);
-    for (auto& kv : s->copies) free_copy(kv.second);
+    for (auto& kv : s->copies) drop_copy(kv.second);
     (void)hipSetDevice(cur);
     delete s;
 }
@@ -640,9 +786,11 @@ int rtx_render_region_device(rtx_scene* s, const rtx_camera* cam, uint64_t seed,
     if (int rc = ensure_device(s, cur, &c)) return rc;
     HIP_TRY(hipSetDevice(cur));
     const bool count = (flags & RTX_FLAG_COUNTERS) != 0;
-    if (int rc = enqueue_on(s, c, cam, seed, region, d_out, (hipStream_t)hip_stream, flags, stats != nullptr)) return rc;
+    uint32_t chunks = 0;
+    if (int rc = enqueue_on(s, c, cam, seed, region, d_out, (hipStream_t)hip_stream, flags, stats != nullptr, &chunks))
+        return rc;
     if (!stats) return RTX_OK;
-    return collect_on(c, count, (uint64_t)region_rows(region) * region->width * cam->samples_per_pixel, stats);
+    return collect_on(c, count, (uint64_t)region_rows(region) * region->width * cam->samples_per_pixel, chunks, stats);
 }
 
 int rtx_render(rtx_scene* s, const rtx_camera* cam, uint64_t seed, int n_gpus, float* out_rgb, rtx_stats* stats) {
@@ -654,63 +802,150 @@ int rtx_render(rtx_scene* s, const rtx_camera* cam, uint64_t seed, int n_gpus, f
     if (n_gpus <= 0) n_gpus = 1;
     if (n_gpus > ndev) return fail(RTX_ERR_INVALID_ARG, "n_gpus=%d but %d devices visible", n_gpus, ndev);
     if ((uint32_t)n_gpus > cam->image_height) n_gpus = (int)cam->image_height;
+    // RCCL for more than one device (RTX_FORCE_RCCL=1: also for one, a 1-rank gather)
+    const bool use_rccl = n_gpus > 1 || env_knob("RTX_FORCE_RCCL", 0, 0, 1) == 1;
     std::lock_guard<std::mutex> lk(s->mu);
     int cur = 0;
     HIP_TRY(hipGetDevice(&cur));
+    const int n = n_gpus;
     const uint32_t W = cam->image_width, H = cam->image_height;
-    std::vector<float*> bufs(n_gpus, nullptr);
-    std::vector<hipStream_t> streams(n_gpus, nullptr);
-    std::vector<rtx_region> regs(n_gpus);
-    std::vector<rtx_stats> sts(n_gpus);
+    const uint32_t R = (H + n - 1) / n;  // rows of band 0, the longest: every band is sent padded to R
+    const size_t band_floats = (size_t)R * W * 3;
+    std::vector<float*> bufs(n, nullptr);
+    std::vector<hipStream_t> streams(n, nullptr);
+    std::vector<rtx_region> regs(n);
+    std::vector<uint32_t> chunks(n, 0);
+    float *gathered = nullptr, *img = nullptr;
+    hipEvent_t g0 = nullptr, g1 = nullptr;
+    rtx_stats total;
+    std::memset(&total, 0, sizeof(total));
     int rc = RTX_OK;
-    // Each device renders a row-interleaved band (rows y % n == d) of the full image.
-    for (int d = 0; d < n_gpus && rc == RTX_OK; ++d) {
+    // 1. Each device renders its row-interleaved band (rows y % n == d) concurrently.
+    for (int d = 0; d < n && rc == RTX_OK; ++d) {
         DeviceCopy* c = nullptr;
         if ((rc = ensure_device(s, d, &c))) break;
         if (hipSetDevice(d) != hipSuccess) { rc = fail(RTX_ERR_HIP, "hipSetDevice(%d)", d); break; }
-        regs[d] = rtx_region{0, 0, W, H, (uint32_t)d, (uint32_t)n_gpus};
-        const size_t bytes = (size_t)region_rows(&regs[d]) * W * 3 * sizeof(float);
+        regs[d] = rtx_region{0, 0, W, H, (uint32_t)d, (uint32_t)n};
         if (hipStreamCreateWithFlags(&streams[d], hipStreamNonBlocking) != hipSuccess) { rc = fail(RTX_ERR_HIP, "stream"); break; }
-        if (hipMalloc(&bufs[d], std::max<size_t>(bytes, 4)) != hipSuccess) { rc = fail(RTX_ERR_OOM, "hipMalloc %zu", bytes); break; }
-        rc = enqueue_on(s, c, cam, seed, &regs[d], bufs[d], streams[d], stats ? RTX_FLAG_COUNTERS : 0u, true);
+        if (hipMalloc(&bufs[d], std::max<size_t>(band_floats, 1) * sizeof(float)) != hipSuccess) {
+            rc = fail(RTX_ERR_OOM, "hipMalloc band %zu B", band_floats * sizeof(float));
+            break;
+        }
+        rc = enqueue_on(s, c, cam, seed, &regs[d], bufs[d], streams[d], stats ? RTX_FLAG_COUNTERS : 0u, true, &chunks[d]);
     }
-    // All devices run concurrently; collect after every launch is enqueued.
-    for (int d = 0; d < n_gpus && rc == RTX_OK && stats; ++d) {
+    // 2. Wait for every band (and read its counters), so gather_ms times only the gather.
+    for (int d = 0; d < n && rc == RTX_OK; ++d) {
         if (hipSetDevice(d) != hipSuccess) { rc = fail(RTX_ERR_HIP, "hipSetDevice(%d)", d); break; }
-        rc = collect_on(&s->copies[d], true, 0, &sts[d]);
+        rtx_stats st;
+        uint64_t samples = (uint64_t)region_rows(&regs[d]) * W * cam->samples_per_pixel;
+        if ((rc = collect_on(&s->copies[d], stats != nullptr, samples, chunks[d], &st))) break;
+        add_stats(&total, st);
     }
-    // Bands -> host rows y = d + r * n (strided copy de-interleaves them).
-    for (int d = 0; d < n_gpus && rc == RTX_OK; ++d) {
-        if (hipSetDevice(d) != hipSuccess) { rc = fail(RTX_ERR_HIP, "hipSetDevice(%d)", d); break; }
-        const uint32_t rows = region_rows(&regs[d]);
-        if (rows == 0) continue;
-        hipError_t e = hipMemcpy2DAsync(out_rgb + (size_t)d * W * 3, (size_t)n_gpus * W * 3 * sizeof(float), bufs[d],
-                                        (size_t)W * 3 * sizeof(float), (size_t)W * 3 * sizeof(float), rows,
-                                        hipMemcpyDeviceToHost, streams[d]);
-        if (e == hipSuccess) e = hipStreamSynchronize(streams[d]);
-        if (e != hipSuccess) rc = fail(RTX_ERR_HIP, "copy band %d: %s", d, hipGetErrorString(e));
+    // 3. Assemble: one ncclGather of the padded bands to device 0 over xGMI, the
+    //    de-interleave on device 0, then the copy into the caller's buffer.
+    if (rc == RTX_OK && use_rccl) {
+        std::lock_guard<std::mutex> rl(g_rccl_mu);
+        const RcclApi* api = rccl_api();
+        if (!api) rc = fail(RTX_ERR_RCCL, "%s", g_rccl.err.c_str());
+        std::vector<ncclComm_t>* comms = nullptr;
+        if (rc == RTX_OK) {
+            auto it = g_comms.find(n);
+            if (it == g_comms.end()) {
+                std::vector<ncclComm_t> cs(n, nullptr);
+                std::vector<int> devs(n);
+                for (int d = 0; d < n; ++d) devs[d] = d;
+                const ncclResult_t e = api->CommInitAll(cs.data(), n, devs.data());
+                if (e != ncclSuccess) rc = fail(RTX_ERR_RCCL, "ncclCommInitAll(%d): %s", n, api->GetErrorString(e));
+                else it = g_comms.emplace(n, cs).first;
+            }
+            if (rc == RTX_OK) comms = &it->second;
+        }
+        if (rc == RTX_OK) {
+            if (hipSetDevice(0) != hipSuccess || hipMalloc(&gathered, (size_t)n * band_floats * sizeof(float)) != hipSuccess ||
+                hipMalloc(&img, (size_t)H * W * 3 * sizeof(float)) != hipSuccess ||
+                hipEventCreate(&g0) != hipSuccess || hipEventCreate(&g1) != hipSuccess ||
+                hipEventRecord(g0, streams[0]) != hipSuccess)
+                rc = fail(RTX_ERR_OOM, "device-0 buffers for the gather of %d bands", n);
+        }
+        if (rc == RTX_OK) {
+            ncclResult_t e = api->GroupStart();
+            for (int d = 0; d < n && e == ncclSuccess; ++d)
+                e = api->Gather(bufs[d], d == 0 ? gathered : nullptr, band_floats, ncclFloat, 0, (*comms)[d], streams[d]);
+            const ncclResult_t e2 = api->GroupEnd();
+            if (e == ncclSuccess) e = e2;
+            if (e != ncclSuccess) rc = fail(RTX_ERR_RCCL, "ncclGather: %s", api->GetErrorString(e));
+        }
+        if (rc == RTX_OK) {
+            (void)hipSetDevice(0);
+            const uint64_t total_floats = (uint64_t)H * W * 3;
+            hipLaunchKernelGGL(deinterleave_bands, dim3((uint32_t)((total_floats + 255) / 256)), dim3(256), 0, streams[0],
+                               gathered, img, (uint32_t)n, R, H, W * 3);
+            hipError_t e = hipGetLastError();
+            if (e == hipSuccess) e = hipEventRecord(g1, streams[0]);
+            if (e == hipSuccess) e = hipMemcpyAsync(out_rgb, img, total_floats * sizeof(float), hipMemcpyDeviceToHost, streams[0]);
+            if (e == hipSuccess) e = hipStreamSynchronize(streams[0]);
+            for (int d = 1; d < n && e == hipSuccess; ++d)
+                if ((e = hipSetDevice(d)) == hipSuccess) e = hipStreamSynchronize(streams[d]);
+            float ms = 0.0f;
+            if (e == hipSuccess && hipSetDevice(0) == hipSuccess) e = hipEventElapsedTime(&ms, g0, g1);
+            if (e != hipSuccess) rc = fail(RTX_ERR_HIP, "band assembly: %s", hipGetErrorString(e));
+            total.gather_ms = ms;
+        }
+    } else if (rc == RTX_OK) {  // one device, no RCCL: the band is the image
+        (void)hipSetDevice(0);
+        hipError_t e = hipMemcpyAsync(out_rgb, bufs[0], (size_t)H * W * 3 * sizeof(float), hipMemcpyDeviceToHost, streams[0]);
+        if (e == hipSuccess) e = hipStreamSynchronize(streams[0]);
+        if (e != hipSuccess) rc = fail(RTX_ERR_HIP, "copy image: %s", hipGetErrorString(e));
     }
-    for (int d = 0; d < n_gpus; ++d) {
+    for (int d = 0; d < n; ++d) {
         if (hipSetDevice(d) != hipSuccess) continue;
         if (streams[d]) (void)hipStreamSynchronize(streams[d]);
         if (bufs[d]) (void)hipFree(bufs[d]);
+        if (d == 0) {
+            if (gathered) (void)hipFree(gathered);
+            if (img) (void)hipFree(img);
+            if (g0) (void)hipEventDestroy(g0);
+            if (g1) (void)hipEventDestroy(g1);
+        }
         if (streams[d]) (void)hipStreamDestroy(streams[d]);
     }
     (void)hipSetDevice(cur);
-    if (rc == RTX_OK && stats) {
-        std::memset(stats, 0, sizeof(*stats));
-        for (int d = 0; d < n_gpus; ++d) {
-            stats->samples += sts[d].samples;
-            stats->segments += sts[d].segments;
-            stats->node_visits += sts[d].node_visits;
-            stats->prim_tests += sts[d].prim_tests;
-            stats->hits += sts[d].hits;
-            stats->texel_fetches += sts[d].texel_fetches;
-            stats->rng_draws += sts[d].rng_draws;
-            stats->kernel_ms = std::max(stats->kernel_ms, sts[d].kernel_ms);
-        }
-    }
+    if (rc == RTX_OK && stats) *stats = total;
     return rc;
+}
+
+int rtx_release_device_memory(int device) {
+    g_last_error.clear();
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess) return fail(RTX_ERR_NO_DEVICE, "no HIP device");
+    if (device < -1 || device >= ndev) return fail(RTX_ERR_INVALID_ARG, "device %d of %d", device, ndev);
+    {
+        std::lock_guard<std::mutex> lk(g_scratch_mu);
+        for (auto& kv : g_scratch)
+            if (device < 0 || kv.first == device) release_scratch_locked(kv.first);
+    }
+    {
+        std::lock_guard<std::mutex> lk(g_ppm_mu);
+        int cur = 0;
+        (void)hipGetDevice(&cur);
+        for (auto& kv : g_ppm)
+            if ((device < 0 || kv.first == device) && kv.second.ptr && hipSetDevice(kv.first) == hipSuccess) {
+                (void)hipFree(kv.second.ptr);
+                kv.second = PpmScratch{};
+            }
+        (void)hipSetDevice(cur);
+    }
+    {  // communicators span devices 0..n-1: any release drops them all
+        std::lock_guard<std::mutex> lk(g_rccl_mu);
+        release_comms_locked();
+    }
+    return RTX_OK;
+}
+
+uint64_t rtx_device_scratch_bytes(int device) {
+    std::lock_guard<std::mutex> lk(g_scratch_mu);
+    auto it = g_scratch.find(device);
+    return it == g_scratch.end() ? 0 : (uint64_t)it->second.bytes;
 }
 
 uint64_t rtx_ppm_max_bytes(uint32_t width, uint32_t height) { return rtxd::ppm_max_bytes(width, height); }
@@ -725,26 +960,33 @@ int rtx_encode_ppm_device(const float* d_rgb, uint32_t width, uint32_t height, c
     if (capacity < need) return fail(RTX_ERR_INVALID_ARG, "capacity %llu < rtx_ppm_max_bytes %llu",
                                      (unsigned long long)capacity, (unsigned long long)need);
     hipStream_t st = (hipStream_t)hip_stream;
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev));
     char header[64];
     const uint64_t hl = rtxd::ppm_header(width, height, header);
     HIP_TRY(hipMemcpyAsync(d_text, header, hl, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipStreamSynchronize(st));  // the header's stack buffer must outlive the copy
     uint64_t total = hl;
     if (n) {
         size_t sb = 0;
         HIP_TRY(rtxd::ppm_scratch_bytes(n, &sb));
-        void* scratch = nullptr;
-        HIP_TRY(hipMalloc(&scratch, sb));
-        hipError_t e = rtxd::ppm_encode(d_rgb, width, height, d_text, scratch, sb, hl, st);
+        std::lock_guard<std::mutex> lk(g_ppm_mu);  // held until the encode has finished
+        PpmScratch& ps = g_ppm[dev];
+        if (ps.bytes < sb) {
+            if (ps.ptr) HIP_TRY(hipFree(ps.ptr));
+            ps = PpmScratch{};
+            HIP_TRY(hipMalloc(&ps.ptr, sb));
+            ps.bytes = sb;
+        }
         uint64_t last_off = 0;
         uint32_t last_len = 0;
-        if (e == hipSuccess) e = hipMemcpyAsync(&last_off, rtxd::ppm_last_offset(scratch, n), 8, hipMemcpyDeviceToHost, st);
-        if (e == hipSuccess) e = hipMemcpyAsync(&last_len, rtxd::ppm_last_length(scratch, n), 4, hipMemcpyDeviceToHost, st);
-        if (e == hipSuccess) e = hipStreamSynchronize(st);
-        (void)hipFree(scratch);
+        hipError_t e = rtxd::ppm_encode(d_rgb, width, height, d_text, ps.ptr, ps.bytes, hl, st);
+        if (e == hipSuccess) e = hipMemcpyAsync(&last_off, rtxd::ppm_last_offset(ps.ptr, n), 8, hipMemcpyDeviceToHost, st);
+        if (e == hipSuccess) e = hipMemcpyAsync(&last_len, rtxd::ppm_last_length(ps.ptr, n), 4, hipMemcpyDeviceToHost, st);
+        const hipError_t es = hipStreamSynchronize(st);  // always: the copies target this frame
         HIP_TRY(e);
+        HIP_TRY(es);
         total += last_off + last_len;
-    } else {
-        HIP_TRY(hipStreamSynchronize(st));
     }
     *out_len = total;
     return RTX_OK;

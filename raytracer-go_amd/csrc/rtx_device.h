@@ -396,10 +396,10 @@ struct Params {
     uint32_t x0, y0, width, rows, rank, world;
     float* out;
     unsigned long long* counters;  // rtx_stats order when counting (16 x u64)
-    uint32_t shade_thresh;         // v1/v2: shade once this many lanes of a wave wait (1..64)
-    uint32_t* tile_counter;        // v2: global tile queue head (zeroed before each launch)
-    uint32_t* error_flag;          // v2: set to 1 by a wave that hit the watchdog
-    uint64_t watchdog_ticks;       // v2: per-wave limit in s_memrealtime ticks (100 MHz)
+    uint32_t shade_thresh;         // shade once this many lanes of a wave wait (1..64)
+    uint32_t* tile_counter;        // global unit queue head (zeroed before each chunk's launch)
+    uint32_t* error_flag;          // set to 1 by a wave that hit the watchdog (zeroed per render)
+    uint64_t watchdog_ticks;       // per-wave limit in s_memrealtime ticks (100 MHz)
     uint32_t has_uv;               // scene has an image texture (UV needed at hits)
     uint32_t has_noise;            // scene has a Perlin NoiseTexture (v3 NOISE kernels)
     // v3 (render_items): samples [k0, k0 + kn) of every pixel, one colour per sample
@@ -476,21 +476,24 @@ __device__ __forceinline__ V3 texture_value(const Params& p, uint32_t ti, float 
         const float g = noise_texture(p.texels + t.texel_offset, t.scale, pt.x, pt.y, pt.z);
         return v3(g, g, g);
     }
-    // RTX_TEX_IMAGE
+    // RTX_TEX_IMAGE: Dy() <= 0 -> the debug colour; else At(int(u*Dx), int(v*Dy)).RGBA()
     if ((int32_t)t.height <= 0) return v3(0.0f, 1.0f, 1.0f);
-    const float uu = u < 0.0f ? 0.0f : (u > 1.0f ? 1.0f : u);
+    const float uu = u < 0.0f ? 0.0f : (u > 1.0f ? 1.0f : u);  // Clamp passes NaN through
     const float vc = v < 0.0f ? 0.0f : (v > 1.0f ? 1.0f : v);
     const float vv = 1.0f - vc;
     const float fi = uu * (float)t.width;
     const float fj = vv * (float)t.height;
     if (COUNT) ++cnt.texel_fetches;
-    if (!(fi >= 0.0f) || !(fj >= 0.0f)) return v3(0.0f, 0.0f, 0.0f);  // NaN
-    const int64_t i = (int64_t)fi, j = (int64_t)fj;
-    if (i >= (int64_t)t.width || j >= (int64_t)t.height) return v3(0.0f, 0.0f, 0.0f);
-    const uint32_t px = p.texels[t.texel_offset + (uint64_t)j * t.width + (uint64_t)i];
-    const float cs = 1.0f / 65535.0f;
-    return v3((float)((px & 0xFFu) * 257u) * cs, (float)(((px >> 8) & 0xFFu) * 257u) * cs,
-              (float)(((px >> 16) & 0xFFu) * 257u) * cs);
+    // int(i), int(j) truncate; i == Dx (u == 1), j == Dy (v == 0) and NaN (int(NaN) =
+    // MinInt64) lie outside the bounds: the border texel after the raster (rtx.h)
+    uint64_t idx = (uint64_t)t.width * t.height;
+    if (fi >= 0.0f && fj >= 0.0f) {
+        const uint64_t i = (uint64_t)fi, j = (uint64_t)fj;
+        if (i < t.width && j < t.height) idx = j * t.width + i;
+    }
+    const uint2 px = *reinterpret_cast<const uint2*>(p.texels + t.texel_offset + 2 * idx);  // RGBA16
+    const float cs = 1.0f / 65535.0f;  // colScale = float32(1.0 / 65535.0)
+    return v3((float)(px.x & 0xFFFFu) * cs, (float)(px.x >> 16) * cs, (float)(px.y & 0xFFFFu) * cs);
 }
 
 // Material index of the primitive at entry `hit`.

@@ -7,17 +7,13 @@
 // keyed by global pixel index and k), so a pixel's value does not depend on the tile,
 // the region, the scheduling or the number of GPUs.
 //
-// Four schedules of the same per-sample code (rtx_device.h), identical output:
-//  v3 render_items  (default) persistent waves over (pixel, sample) items; colours go
-//                   to an HBM scratch and reduce_samples sums them in sample order.
-//  v1 render_wave   one 8x8 tile per wave, one pixel per lane, path regeneration
-//                   (RTX_FLAG_KERNEL_V1; RTX_FLAG_WAVE_GEOM variants).
-//  v2 render_pool   persistent waves over a pool of pixels fed by a global tile queue;
-//                   lanes take any idle pixel of the pool (RTX_FLAG_KERNEL_POOL).
-//  v0 render_pixels thread per pixel, samples in a plain loop (the first version).
-// v1-v3 step every traversing lane through BVH entries (three per wave vote) and shade
-// in batches: once `shade_thresh` lanes of the wave wait (or none traverses), all
-// waiting lanes shade together, so shading and its Philox blocks run in lockstep.
+// Schedule (v3): persistent waves over (pixel, sample) items; every item's colour goes to
+// an HBM scratch and reduce_samples sums them in sample order afterwards.  Waves step
+// every traversing lane through BVH entries (six per wave vote) and shade in batches:
+// once `shade_thresh` lanes of the wave wait (or none traverses), all waiting lanes shade
+// together, so shading and its Philox blocks run in lockstep.  (The earlier schedules
+// v0 thread-per-pixel, v1 wave-per-tile and v2 pixel pool were measured slower and
+// removed in ABI 4; DESIGN.md §5 keeps their numbers.)
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -46,49 +42,8 @@ __device__ __forceinline__ void flush_sched(const Params& p, uint64_t wi, uint64
 }
 
 // ------------------------------------------------------------------------------------
-// v0: thread per pixel, samples in a loop, traversal from global memory.
-// ------------------------------------------------------------------------------------
-constexpr int TILE_W = 16;
-constexpr int TILE_H = 16;
-constexpr int BLOCK = TILE_W * TILE_H;
-
-template <bool COUNT, bool QUADS>
-__global__ __launch_bounds__(BLOCK) void render_pixels(Params p) {
-    const uint32_t lx = blockIdx.x * TILE_W + (threadIdx.x % TILE_W);
-    const uint32_t lr = blockIdx.y * TILE_H + (threadIdx.x / TILE_W);
-    if (lx >= p.width || lr >= p.rows) return;
-    const uint32_t x = p.x0 + lx;
-    const uint32_t y = p.y0 + p.rank + lr * p.world;
-    const rtx_camera& c = p.cam;
-    const V3 base = pixel_base(c, x, y);
-    PathRng rng{(uint32_t)p.seed, (uint32_t)(p.seed >> 32), y * c.image_width + x, 0};
-    Counters cnt{0, 0, 0, 0, 0, 0};
-    const SceneRef E = scene_ref(p.entries, p.n_entries, p.materials);
-    V3 sum = v3(0.0f, 0.0f, 0.0f);
-    for (uint32_t k = 0; k < c.samples_per_pixel; ++k) {
-        rng.sample = k;
-        Ray r = camera_ray(c, base, rng, cnt.draws);
-        V3 thr = v3(1.0f, 1.0f, 1.0f), acc = v3(0.0f, 0.0f, 0.0f), col = acc;
-        for (uint32_t seg = 0; seg < c.max_depth; ++seg) {  // ray.go:33 depth limit
-            if (COUNT) ++cnt.segments;
-            Trav t;
-            trav_begin(t, r);
-            while (t.i < 16 * p.n_entries) trav_step<COUNT, QUADS>(t, r, E, cnt);
-            if (shade<COUNT, QUADS>(p, E, t, seg, r, thr, acc, rng, cnt, col)) break;
-        }
-        sum = add(sum, col);  // camera.go:259 (col = 0 when the depth ran out)
-    }
-    const V3 avg = scale(sum, 1.0f / (float)c.samples_per_pixel);  // camera.go:261
-    float* o = p.out + ((size_t)lr * p.width + lx) * 3;
-    o[0] = avg.x;
-    o[1] = avg.y;
-    o[2] = avg.z;
-    if (COUNT) flush_counters(p, c.samples_per_pixel, cnt);
-}
-
-// ------------------------------------------------------------------------------------
-// Traversal phase shared by v1 and v2.  Lane modes: 0 = traversing, 1 and 2 = waiting
-// for the shading phase, 3 = neither.  Runs BVH steps until at least `thresh` lanes
+// Traversal phase.  Lane modes: 0 = traversing, 1 and 2 = waiting for the shading
+// phase, 3 = neither.  Runs BVH steps until at least `thresh` lanes
 // wait or none traverses.  Each traversing lane takes one entry (box or sphere, by its
 // tag) per iteration.  (Separate box and sphere batches, steered by link-type bits in
 // the entries, were measured: the extra decode per step cost more than the reduced
@@ -139,176 +94,7 @@ __device__ __forceinline__ void traverse_phase(uint32_t& mode, Trav& t, const Ra
     }
 }
 
-// ------------------------------------------------------------------------------------
-// v1: wave loop, one pixel per lane, path regeneration, batched shading.
-//
-// PERSIST = false (default): one wave per 8x8 tile; a lane idles once its pixel is finished
-// until the wave's slowest pixel is (measured: 26 % of lane slots at the headline
-// config).  PERSIST = true: the grid is the device's resident capacity; a wave claims
-// 8x8 tiles from a global counter and hands their pixels, in order, to its lanes as
-// they finish, so its lanes stay on one or two neighbouring tiles (per-lane claims from
-// the global counter scattered a wave over the whole claim frontier and lost 24 % per
-// iteration to incoherence).  A pixel is still traced by one lane, samples
-// k = 0..spp-1 in order, so its float32 sum is the reference's whatever the schedule.
-// Measured at 100 spp: PERSIST raises traversal lane use from 0.50 to 0.62 but costs
-// 15 % more cycles per iteration (divergence grows with the active lanes), a net loss.
-// ------------------------------------------------------------------------------------
 enum : uint32_t { M_TRAV = 0, M_SHADE = 1, M_START = 2, M_DONE = 3, M_CLAIM = 4 };
-
-// BLOCK = 64 * WX * WY threads: a WX x WY grid of waves, each an 8x8 pixel tile; one LDS
-// copy of the scene per block.  MINW = minimum waves per SIMD requested from the
-// register allocator (0 = compiler's choice).  STEPS: entries per lane between votes.
-template <bool COUNT, bool USE_LDS, int WX, int WY, int MINW, int STEPS, bool PERSIST, bool QUADS>
-__global__ __launch_bounds__(64 * WX * WY, MINW) void render_wave(Params p) {
-    constexpr uint32_t WAVE_BLOCK = 64 * WX * WY;
-    extern __shared__ float4 lds_entries[];
-    SceneRef E;
-    if constexpr (USE_LDS) {
-        const uint32_t n4 = scene_float4s(p.n_entries, p.n_quads);  // entries, then the quad table
-        for (uint32_t t = threadIdx.x; t < n4; t += WAVE_BLOCK) lds_entries[t] = p.entries[t];
-        __syncthreads();
-        E = scene_ref(lds_entries, p.n_entries, p.materials);
-    } else {
-        E = scene_ref(p.entries, p.n_entries, p.materials);
-    }
-    const uint32_t n_entries = p.n_entries;
-    const uint32_t thresh = p.shade_thresh;
-    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-    const rtx_camera& c = p.cam;
-    const uint32_t spp = c.samples_per_pixel;
-    const uint32_t tiles_x = (p.width + 7u) / 8u;
-    const uint32_t n_tiles = tiles_x * ((p.rows + 7u) / 8u);
-    uint32_t cur_tile = 0, cursor = 64u;  // PERSIST: the wave's tile and its next pixel (uniform)
-    bool exhausted = false;
-
-    uint32_t lx = blockIdx.x * (8u * WX) + (wave % WX) * 8u + (lane & 7u);
-    uint32_t lr = blockIdx.y * (8u * WY) + (wave / WX) * 8u + (lane >> 3);
-    const bool active = !PERSIST && lx < p.width && lr < p.rows;
-    V3 base = pixel_base(c, p.x0 + lx, p.y0 + p.rank + lr * p.world);
-    uint32_t mode = PERSIST ? M_CLAIM : (active ? M_START : M_DONE);
-    uint32_t seg = 0, pixels_done = 0;
-    V3 sum = v3(0.0f, 0.0f, 0.0f);
-    V3 thr = v3(1.0f, 1.0f, 1.0f), acc = v3(0.0f, 0.0f, 0.0f);
-    Ray r{v3(0, 0, 0), v3(0, 0, 0)};
-    PathRng rng{(uint32_t)p.seed, (uint32_t)(p.seed >> 32),
-                (p.y0 + p.rank + lr * p.world) * c.image_width + p.x0 + lx, 0};
-    Trav t{};
-    t.i = 16 * p.n_entries;  // on the sentinel until its first ray
-    Counters cnt{0, 0, 0, 0, 0, 0};
-    uint64_t wave_iters = 0, lane_steps = 0, shade_phases = 0, shade_lanes = 0;
-    uint64_t trav_cycles = 0, shade_cycles = 0, clk = 0, idle_lanes = 0;  // COUNT only
-
-    for (;;) {
-        if (COUNT) clk = __builtin_amdgcn_s_memtime();
-        traverse_phase<COUNT, STEPS, QUADS>(mode, t, r, E, n_entries, thresh, cnt, wave_iters, lane_steps, shade_phases,
-                                     shade_lanes, idle_lanes);
-        if (COUNT) {
-            const uint64_t now = __builtin_amdgcn_s_memtime();
-            trav_cycles += now - clk;
-            clk = now;
-        }
-        if (ballot(mode != M_DONE) == 0) break;
-
-        // ---- shading phase ----------------------------------------------------------
-        // The scatter samples of this phase, drawn by the whole wave together.
-        const Scatter sc = coop_scatter<QUADS>(p, E, rng, seg + 1, mode == M_SHADE ? t.hit : -1);
-        bool ready = false;                // a ray to trace (continued path or new sample)
-        bool fresh = mode == M_START;      // the lane needs its pixel's next sample
-        if (mode == M_SHADE) {
-            V3 color;
-            bool done = shade<COUNT, QUADS>(p, E, t, seg, r, thr, acc, rng, cnt, color, &sc);
-            ++seg;
-            if (!done && seg == c.max_depth) {  // depth exhausted: GetColor(0) = 0 (ray.go:33)
-                done = true;
-                color = acc;
-            }
-            if (done) {
-                sum = add(sum, color);  // camera.go:259
-                ++rng.sample;
-                fresh = true;
-            } else {
-                ready = true;
-            }
-        }
-        // New samples, at one program point for the whole wave (camera_ray's Philox runs
-        // in lockstep).  Loops only for max depth 0 (every sample black) and ragged claims.
-        for (;;) {
-            if (fresh && rng.sample >= spp) {  // pixel finished (camera.go:261)
-                const V3 avg = scale(sum, 1.0f / (float)spp);
-                float* o = p.out + ((size_t)lr * p.width + lx) * 3;
-                o[0] = avg.x;
-                o[1] = avg.y;
-                o[2] = avg.z;
-                ++pixels_done;
-                fresh = false;
-                mode = PERSIST ? M_CLAIM : M_DONE;
-            }
-            if constexpr (PERSIST) {  // lanes without a pixel take the next ones of the wave's tile
-                for (;;) {
-                    const uint64_t wm = ballot(mode == M_CLAIM);
-                    if (wm == 0) break;
-                    if (cursor >= 64u && !exhausted) {  // claim the next 8x8 tile (wave-uniform)
-                        uint32_t tl = 0;
-                        if (lane == 0) tl = atomicAdd(p.tile_counter, 1u);
-                        cur_tile = (uint32_t)__shfl((int)tl, 0);
-                        cursor = 0;
-                        exhausted = cur_tile >= n_tiles;
-                    }
-                    if (exhausted) {
-                        if (mode == M_CLAIM) mode = M_DONE;
-                        break;
-                    }
-                    const uint32_t rank = (uint32_t)__popcll(wm & ((1ull << lane) - 1ull));
-                    if (mode == M_CLAIM && rank < 64u - cursor) {
-                        const uint32_t l = cursor + rank;
-                        lx = (cur_tile % tiles_x) * 8u + (l & 7u);
-                        lr = (cur_tile / tiles_x) * 8u + (l >> 3);
-                        if (lx < p.width && lr < p.rows) {  // else: outside a ragged tile, claim again
-                            const uint32_t x = p.x0 + lx, y = p.y0 + p.rank + lr * p.world;
-                            base = pixel_base(c, x, y);
-                            rng.pixel = y * c.image_width + x;
-                            rng.sample = 0;
-                            sum = v3(0.0f, 0.0f, 0.0f);
-                            fresh = true;
-                            mode = M_START;
-                        }
-                    }
-                    const uint32_t taken = (uint32_t)__popcll(wm);
-                    cursor = cursor + taken > 64u ? 64u : cursor + taken;
-                }
-            }
-            if (fresh && rng.sample < spp) {
-                r = camera_ray(c, base, rng, cnt.draws);  // GetRay, camera.go:257
-                thr = v3(1.0f, 1.0f, 1.0f);
-                acc = v3(0.0f, 0.0f, 0.0f);
-                seg = 0;
-                if (c.max_depth > 0) {
-                    fresh = false;
-                    ready = true;
-                } else {
-                    sum = add(sum, acc);  // max depth 0: GetColor returns black
-                    ++rng.sample;
-                }
-            }
-            if (ballot(fresh) == 0) break;
-        }
-        if (ready) {  // begin a segment: world.Hit (ray.go:36)
-            if (COUNT) ++cnt.segments;
-            trav_begin(t, r);
-            mode = n_entries > 0 ? M_TRAV : M_SHADE;
-        }
-        if (COUNT) shade_cycles += __builtin_amdgcn_s_memtime() - clk;
-    }
-    if (COUNT) {
-        flush_counters(p, (uint64_t)pixels_done * spp, cnt);
-        if (lane == 0) {
-            flush_sched(p, wave_iters, lane_steps / STEPS, shade_phases, shade_lanes);
-            atomicAdd(&p.counters[12], (unsigned long long)trav_cycles);
-            atomicAdd(&p.counters[13], (unsigned long long)shade_cycles);
-            atomicAdd(&p.counters[14], (unsigned long long)idle_lanes);
-        }
-    }
-}
 
 // ------------------------------------------------------------------------------------
 // v3: persistent waves over (pixel, sample) items; the sum is formed afterwards.
@@ -394,7 +180,16 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
         ++items_done;
     };
 
+    const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+    uint32_t iter = 0;
     for (;;) {
+        // Watchdog (RTX_WATCHDOG_S): a wave never outlives p.watchdog_ticks, so a bug cannot
+        // keep the GPU busy forever; the render then fails with RTX_ERR_HIP (collect_on).
+        // The loop is wave-uniform, so is this test.
+        if ((++iter & 255u) == 0 && __builtin_amdgcn_s_memrealtime() - t_start > p.watchdog_ticks) {
+            if (lane == 0) atomicOr(p.error_flag, 1u);
+            break;
+        }
         if (COUNT) clk = __builtin_amdgcn_s_memtime();
         // primitive batching only for a scene in LDS: a lane that waits re-reads its entry, which
         // from HBM cost config 4 +34 %
@@ -528,284 +323,9 @@ __global__ __launch_bounds__(256) void reduce_samples(Params p, uint32_t last) {
 }
 
 // ------------------------------------------------------------------------------------
-// v2: persistent waves over a pool of pixels fed by a global tile queue.
-//
-// v1 keeps one pixel per lane, so a wave lasts as long as its most expensive pixel
-// (a sky pixel needs ~1 segment per sample, a glass one ~8).  v2 decouples lanes from
-// pixels: each wave owns CH chunks of 64 pixels (8x8 tiles of the region, taken from
-// a global atomic queue) = a pool of POOL_SLOTS pixels in LDS, each with its running
-// float32 sum and next sample index.  A free lane claims any idle pixel of the pool
-// and traces its next sample; a pixel has at most ONE sample in flight, so samples
-// still complete — and are summed — in order k = 0..spp-1 (camera.go:256-261).  When
-// all pixels of a chunk are done, the chunk is refilled from the queue.  The grid is
-// sized to the device's resident capacity; every wave exits once the queue is empty
-// and its chunks are finished, or when its watchdog fires.
-// ------------------------------------------------------------------------------------
-constexpr int POOL_BLOCK = 512;  // 8 waves share one LDS copy of the scene
-constexpr int POOL_WAVES = POOL_BLOCK / 64;
-enum : uint32_t { Q_TRAV = 0, Q_SHADE = 1, Q_FREE = 2, Q_IDLE = 3 };
-constexpr uint32_t ST_INFLIGHT = 0x80000000u, ST_INVALID = 0x40000000u, ST_K = 0x00FFFFFFu;
-
-template <int NCH>  // chunks (8x8 tiles) per wave
-struct WavePool {
-    static constexpr int SLOTS = NCH * 64;
-    float sx[SLOTS], sy[SLOTS], sz[SLOTS];
-    uint32_t st[SLOTS];        // next sample index | INFLIGHT | INVALID
-    int32_t tile[NCH];         // tile of the region held by chunk c, -1 = empty
-    uint32_t remaining[NCH];   // pixels of chunk c not finished yet
-    uint32_t origin[NCH];      // region x0 | y0 << 16 of the tile
-    uint32_t pad[NCH];
-};
-static_assert(sizeof(WavePool<2>) % 16 == 0 && sizeof(WavePool<4>) % 16 == 0, "keep the scene copy 16-B aligned");
-
-__device__ __forceinline__ void wave_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-template <bool COUNT, bool USE_LDS, int NCH>
-__global__ __launch_bounds__(POOL_BLOCK) void render_pool(Params p) {
-    using Pool = WavePool<NCH>;
-    constexpr uint32_t CH = NCH, POOL_SLOTS = Pool::SLOTS;
-    extern __shared__ float4 lds_dyn[];
-    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-    Pool* wp = reinterpret_cast<Pool*>(lds_dyn) + wave;
-    SceneRef E;
-    if constexpr (USE_LDS) {
-        float4* scene = lds_dyn + (POOL_WAVES * sizeof(Pool)) / 16;
-        const uint32_t n4 = scene_float4s(p.n_entries, 0);
-        for (uint32_t t = threadIdx.x; t < n4; t += POOL_BLOCK) scene[t] = p.entries[t];
-        E = scene_ref(scene, p.n_entries, p.materials);
-    } else {
-        E = scene_ref(p.entries, p.n_entries, p.materials);
-    }
-    const uint32_t n_entries = p.n_entries;
-    const uint32_t thresh = p.shade_thresh;
-    const rtx_camera& c = p.cam;
-    const uint32_t spp = c.samples_per_pixel;
-    const uint32_t tiles_x = (p.width + 7) / 8;
-    const uint32_t n_tiles = tiles_x * ((p.rows + 7) / 8);
-
-    // Take the next 8x8 tile of the region into chunk ch (wave-uniform call).
-    auto load_chunk = [&](uint32_t ch) {
-        uint32_t tl = 0;
-        if (lane == 0) tl = atomicAdd(p.tile_counter, 1u);
-        tl = __shfl(tl, 0);
-        const bool has = tl < n_tiles;
-        const uint32_t ox = (tl % tiles_x) * 8, oy = (tl / tiles_x) * 8;
-        const uint32_t lx = ox + (lane & 7u), lr = oy + (lane >> 3);
-        const bool valid = has && lx < p.width && lr < p.rows;
-        const uint32_t s = ch * 64 + lane;
-        wp->sx[s] = 0.0f;
-        wp->sy[s] = 0.0f;
-        wp->sz[s] = 0.0f;
-        wp->st[s] = valid ? 0u : ST_INVALID;
-        const uint32_t nvalid = (uint32_t)__popcll(ballot(valid));
-        if (lane == 0) {
-            wp->tile[ch] = has ? (int32_t)tl : -1;
-            wp->remaining[ch] = nvalid;
-            wp->origin[ch] = ox | (oy << 16);
-        }
-    };
-    for (uint32_t ch = 0; ch < CH; ++ch) load_chunk(ch);
-    __syncthreads();  // scene copy + pool init visible
-
-    uint32_t mode = Q_FREE;
-    bool begin = false;  // set up a new segment at the end of this shading phase
-    uint32_t slot = 0, px = 0, py = 0, seg = 0;
-    uint32_t cursor = 0;  // wave-uniform claim cursor over the pool
-    V3 thr = v3(1.0f, 1.0f, 1.0f), acc = v3(0.0f, 0.0f, 0.0f);
-    Ray r{v3(0, 0, 0), v3(0, 0, 0)};
-    PathRng rng{(uint32_t)p.seed, (uint32_t)(p.seed >> 32), 0, 0};
-    Trav t{};
-    t.i = 16 * p.n_entries;  // on the sentinel until its first ray
-    Counters cnt{0, 0, 0, 0, 0, 0};
-    uint64_t samples = 0;
-    uint64_t wave_iters = 0, lane_steps = 0, shade_phases = 0, shade_lanes = 0;
-    uint64_t idle_lanes = 0;  // (v2: Q_IDLE lanes; not reported)
-    const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
-    uint32_t iter = 0;
-
-    for (;;) {
-        // Watchdog: a wave never outlives p.watchdog_ticks (the grid always drains).
-        if ((++iter & 255u) == 0 && __builtin_amdgcn_s_memrealtime() - t_start > p.watchdog_ticks) {
-            if (lane == 0) atomicOr(p.error_flag, 1u);
-            break;
-        }
-        traverse_phase<COUNT, 3>(mode, t, r, E, n_entries, thresh, cnt, wave_iters, lane_steps, shade_phases,
-                                 shade_lanes, idle_lanes);
-
-        // ---- shading phase: finish or continue paths ---------------------------------------
-        if (mode == Q_SHADE) {
-            V3 color = acc;
-            bool done = c.max_depth == 0;  // GetColor(0) returns black (ray.go:33-35)
-            if (!done) {
-                done = shade<COUNT>(p, E, t, seg, r, thr, acc, rng, cnt, color);
-                ++seg;
-                if (!done && seg == c.max_depth) {  // depth exhausted
-                    done = true;
-                    color = acc;
-                }
-            }
-            if (done) {  // sum += sample, in sample order (camera.go:259)
-                wp->sx[slot] = wp->sx[slot] + color.x;
-                wp->sy[slot] = wp->sy[slot] + color.y;
-                wp->sz[slot] = wp->sz[slot] + color.z;
-                const uint32_t kn = (wp->st[slot] & ST_K) + 1;
-                wp->st[slot] = kn;  // clears INFLIGHT
-                if (COUNT) ++samples;
-                if (kn == spp) {  // pixel complete: sum * (1/spp), camera.go:261
-                    const float inv = 1.0f / (float)spp;
-                    float* o = p.out + ((size_t)py * p.width + px) * 3;
-                    o[0] = wp->sx[slot] * inv;
-                    o[1] = wp->sy[slot] * inv;
-                    o[2] = wp->sz[slot] * inv;
-                    atomicSub(&wp->remaining[slot >> 6], 1u);
-                }
-                mode = Q_FREE;
-            } else {
-                mode = Q_TRAV;
-                begin = true;
-            }
-        }
-        wave_sync();
-
-        // ---- refill finished chunks from the global queue (wave-uniform) -------------------
-        bool any_chunk = false;
-        for (uint32_t ch = 0; ch < CH; ++ch) {
-            if (wp->tile[ch] >= 0 && wp->remaining[ch] == 0) {
-                load_chunk(ch);
-                wave_sync();
-            }
-            any_chunk |= wp->tile[ch] >= 0;
-        }
-        if (!any_chunk && ballot(mode == Q_TRAV || mode == Q_SHADE) == 0) break;
-
-        // ---- claim idle pixels for free lanes ------------------------------------------------
-        const uint64_t freem = ballot(mode == Q_FREE || mode == Q_IDLE);
-        if (mode == Q_FREE || mode == Q_IDLE) {
-            const uint32_t rank = (uint32_t)__popcll(freem & ((1ull << lane) - 1ull));
-            const uint32_t cand = (cursor + rank) % POOL_SLOTS;
-            const uint32_t st = wp->st[cand];
-            if ((st & (ST_INFLIGHT | ST_INVALID)) == 0 && (st & ST_K) < spp) {
-                wp->st[cand] = st | ST_INFLIGHT;
-                slot = cand;
-                const uint32_t org = wp->origin[cand >> 6];
-                const uint32_t j = cand & 63u;
-                px = (org & 0xFFFFu) + (j & 7u);
-                py = (org >> 16) + (j >> 3);
-                const uint32_t x = p.x0 + px, y = p.y0 + p.rank + py * p.world;
-                rng.pixel = y * c.image_width + x;
-                rng.sample = st & ST_K;
-                r = camera_ray(c, pixel_base(c, x, y), rng, cnt.draws);
-                thr = v3(1.0f, 1.0f, 1.0f);
-                acc = v3(0.0f, 0.0f, 0.0f);
-                seg = 0;
-                mode = Q_TRAV;
-                begin = true;
-                if (c.max_depth == 0) {
-                    mode = Q_SHADE;  // finishes black at the next shading phase
-                    begin = false;
-                }
-            } else {
-                mode = Q_IDLE;
-            }
-        }
-        cursor = (cursor + (uint32_t)__popcll(freem)) % POOL_SLOTS;
-
-        // ---- begin the next segment (world.Hit, ray.go:36) for lanes that just scattered
-        // or claimed a sample; lanes still mid-traversal keep their state ----------------------
-        if (begin) {
-            begin = false;
-            if (COUNT) ++cnt.segments;
-            trav_begin(t, r);
-            if (n_entries == 0) mode = Q_SHADE;
-        }
-    }
-
-    if (COUNT) {
-        flush_counters(p, samples, cnt);
-        if (lane == 0) flush_sched(p, wave_iters, lane_steps / 3, shade_phases, shade_lanes);
-    }
-}
-
-// ------------------------------------------------------------------------------------
 // launches
 // ------------------------------------------------------------------------------------
 constexpr uint32_t LDS_MAX_BYTES = 64 * 1024;
-
-// LDS bytes of the scene copy: entries and the quad table.
-inline size_t scene_lds_bytes(const Params& p) { return (size_t)scene_float4s(p.n_entries, p.n_quads) * 16; }
-
-template <bool COUNT, int NCH>
-hipError_t launch_pool(const Params& p, bool use_lds, hipStream_t stream) {
-    const size_t shmem = POOL_WAVES * sizeof(WavePool<NCH>) + (use_lds ? scene_lds_bytes(p) : 0);
-    int dev = 0, cus = 0, per_cu = 0;
-    hipError_t e = hipGetDevice(&dev);
-    if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    if (e != hipSuccess) return e;
-    e = use_lds
-            ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, render_pool<COUNT, true, NCH>, POOL_BLOCK, shmem)
-            : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, render_pool<COUNT, false, NCH>, POOL_BLOCK, shmem);
-    if (e != hipSuccess) return e;
-    if (per_cu < 1) per_cu = 1;
-    const uint32_t tiles = ((p.width + 7) / 8) * ((p.rows + 7) / 8);
-    uint32_t blocks = (uint32_t)(per_cu * cus);
-    const uint32_t need = (tiles + POOL_WAVES * NCH - 1) / (POOL_WAVES * NCH);  // no wave starts empty-handed
-    if (blocks > need) blocks = need;
-    if (blocks == 0) blocks = 1;
-    e = hipMemsetAsync(p.tile_counter, 0, 2 * sizeof(uint32_t), stream);  // queue head + watchdog flag
-    if (e != hipSuccess) return e;
-    if (use_lds)
-        hipLaunchKernelGGL((render_pool<COUNT, true, NCH>), dim3(blocks), dim3(POOL_BLOCK), shmem, stream, p);
-    else
-        hipLaunchKernelGGL((render_pool<COUNT, false, NCH>), dim3(blocks), dim3(POOL_BLOCK), shmem, stream, p);
-    return hipGetLastError();
-}
-
-template <bool COUNT, int WX, int WY, int MINW, int STEPS = 1, bool PERSIST = false, bool QUADS = false>
-hipError_t launch_wave_geom(const Params& p, bool use_lds, hipStream_t stream) {
-    const size_t shmem = use_lds ? scene_lds_bytes(p) : 0;
-    const auto kern = use_lds ? render_wave<COUNT, true, WX, WY, MINW, STEPS, PERSIST, QUADS>
-                              : render_wave<COUNT, false, WX, WY, MINW, STEPS, PERSIST, QUADS>;
-    constexpr int block = 64 * WX * WY;
-    if constexpr (PERSIST) {
-        int dev = 0, cus = 0, per_cu = 0;
-        hipError_t e = hipGetDevice(&dev);
-        if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, block, shmem);
-        if (e != hipSuccess) return e;
-        if (per_cu < 1) per_cu = 1;
-        const uint64_t tiles = (uint64_t)((p.width + 7) / 8) * ((p.rows + 7) / 8);
-        uint64_t blocks = (uint64_t)per_cu * cus;
-        if (p.grid_pct > 0 && p.grid_pct < 100) blocks = (blocks * p.grid_pct + 99) / 100;
-        const uint64_t need = (tiles + WX * WY - 1) / (WX * WY);  // no wave starts without a tile
-        if (blocks > need) blocks = need;
-        if (blocks == 0) blocks = 1;
-        e = hipMemsetAsync(p.tile_counter, 0, 2 * sizeof(uint32_t), stream);  // claim counter + flag
-        if (e != hipSuccess) return e;
-        hipLaunchKernelGGL(kern, dim3((uint32_t)blocks), dim3(block), shmem, stream, p);
-    } else {
-        const dim3 grid((p.width + 8 * WX - 1) / (8 * WX), (p.rows + 8 * WY - 1) / (8 * WY));
-        hipLaunchKernelGGL(kern, grid, dim3(block), shmem, stream, p);
-    }
-    return hipGetLastError();
-}
-
-// Block geometry of v1 (RTX_FLAG_WAVE_GEOM): waves per block and the register budget.
-template <bool COUNT>
-hipError_t launch_wave(const Params& p, uint32_t geom, bool use_lds, hipStream_t stream) {
-    switch (geom) {
-    case 1: return launch_wave_geom<COUNT, 2, 2, 0, 3, true>(p, use_lds, stream);   // persistent, claims tiles
-    case 2: return launch_wave_geom<COUNT, 2, 2, 0, 1, true>(p, use_lds, stream);   // 1 step per vote
-    case 3: return launch_wave_geom<COUNT, 2, 2, 0, 4, true>(p, use_lds, stream);   // 4 steps per vote
-    case 4: return launch_wave_geom<COUNT, 4, 2, 0, 3, true>(p, use_lds, stream);   // 8 waves per block
-    case 5: return launch_wave_geom<COUNT, 4, 2, 8, 3, true>(p, use_lds, stream);   // 8 waves, >= 8/SIMD
-    case 6: return launch_wave_geom<COUNT, 1, 1, 0, 3, true>(p, use_lds, stream);   // 1 wave per block
-    default: return launch_wave_geom<COUNT, 2, 2, 0, 3, false>(p, use_lds, stream); // one tile per wave
-    }
-}
 
 // v3: chunks of p.kn samples (the scratch holds one chunk), each rendered by a
 // resident-capacity grid of render_items and summed into p.out by reduce_samples.
@@ -845,7 +365,7 @@ hipError_t launch_items(Params p, bool use_lds, hipStream_t stream) {
         if (p.debug_launch)
             fprintf(stderr, "rtx v3: waves/wg %d, wgs/CU %d, CUs %d, grid %llu, sub %u, units %llu, lds %zu B\n", WAVES,
                     per_cu, cus, (unsigned long long)blocks, p.sub, (unsigned long long)units, shmem);
-        e = hipMemsetAsync(p.tile_counter, 0, 2 * sizeof(uint32_t), stream);
+        e = hipMemsetAsync(p.tile_counter, 0, sizeof(uint32_t), stream);  // (the watchdog flag: once per render)
         if (e != hipSuccess) return e;
         hipLaunchKernelGGL(kern, dim3((uint32_t)blocks), dim3(block), shmem, stream, p);
         hipLaunchKernelGGL(reduce_samples, dim3((uint32_t)((npix + 255) / 256)), dim3(256), 0, stream, p,
@@ -854,14 +374,6 @@ hipError_t launch_items(Params p, bool use_lds, hipStream_t stream) {
         if (e != hipSuccess) return e;
     }
     return hipSuccess;
-}
-
-bool uses_items(const Params& p, uint32_t flags) {
-    const bool work = p.width > 0 && p.rows > 0 && p.cam.samples_per_pixel > 0 && p.cam.max_depth > 0;
-    if (p.has_noise) return work;  // Perlin scenes run v3 only (the NOISE instantiations)
-    if (flags & (RTX_FLAG_KERNEL_V0 | RTX_FLAG_KERNEL_V1 | RTX_FLAG_KERNEL_POOL)) return false;
-    if (((flags >> 24) & 7u) != 0) return false;  // RTX_FLAG_WAVE_GEOM tunes v1
-    return work;
 }
 
 #ifndef RTX_HYB_WAVES  // the same for scenes in HBM with a 64 KB LDS cache of their top levels
@@ -890,37 +402,13 @@ hipError_t launch_items_for(const Params& p, bool use_lds, hipStream_t stream) {
 
 hipError_t launch_render(const Params& p, uint32_t flags, hipStream_t stream) {
     if (p.width == 0 || p.rows == 0) return hipSuccess;
+    if (!p.scratch) return hipErrorInvalidValue;  // the caller sizes the sample scratch
     const bool count = (flags & RTX_FLAG_COUNTERS) != 0;
-    const bool quads = p.n_quads > 0;
-    const bool use_lds = !(flags & RTX_FLAG_NO_LDS) && scene_lds_bytes(p) <= LDS_MAX_BYTES;
-    if (uses_items(p, flags)) {
-        if (!p.scratch) return hipErrorInvalidValue;  // the caller sizes the v3 scratch
-        const bool use_lds = !(flags & RTX_FLAG_NO_LDS) && (p.n_entries + 1) * 16 <= LDS_B &&
-                             lds_fixed_bytes(p.n_entries, p.n_quads, p.n_materials) <= LDS_MAX_BYTES;
-        return count ? launch_items_for<true>(p, use_lds, stream) : launch_items_for<false>(p, use_lds, stream);
-    }
-    if (flags & RTX_FLAG_KERNEL_V0) {
-        const dim3 grid((p.width + TILE_W - 1) / TILE_W, (p.rows + TILE_H - 1) / TILE_H);
-        const auto kern = count ? (quads ? render_pixels<true, true> : render_pixels<true, false>)
-                                : (quads ? render_pixels<false, true> : render_pixels<false, false>);
-        hipLaunchKernelGGL(kern, grid, dim3(BLOCK), 0, stream, p);
-        return hipGetLastError();
-    }
-    // Scenes with quads (hittables.go:138-216) run the default v1 schedule built with the
-    // three-kind step; the scheduling variants below are sphere-only.
-    if (quads)
-        return count ? launch_wave_geom<true, 2, 2, 0, 3, false, true>(p, use_lds, stream)
-                     : launch_wave_geom<false, 2, 2, 0, 3, false, true>(p, use_lds, stream);
-    // v2 keeps tile origins in 16 bits: regions wider or taller than 65535 use v1.
-    if ((flags & RTX_FLAG_KERNEL_POOL) && p.width <= 0xFFFFu && p.rows <= 0xFFFFu) {
-        if (flags & RTX_FLAG_POOL4)
-            return count ? launch_pool<true, 4>(p, use_lds, stream) : launch_pool<false, 4>(p, use_lds, stream);
-        return count ? launch_pool<true, 2>(p, use_lds, stream) : launch_pool<false, 2>(p, use_lds, stream);
-    }
-    uint32_t geom = (flags >> 24) & 7u;
-    // The persistent kernels claim 8x8 tiles by a 32-bit index.
-    if (geom != 0 && (uint64_t)((p.width + 7) / 8) * ((p.rows + 7) / 8) > 0xFFFF0000ull) geom = 0;
-    return count ? launch_wave<true>(p, geom, use_lds, stream) : launch_wave<false>(p, geom, use_lds, stream);
+    // the whole scene in LDS (fixed layout) when its 'a' halves fit below LDS_B and all of it
+    // in 64 KB; else from HBM, with the top levels cached in LDS when stored first (n_hot)
+    const bool use_lds = !(flags & RTX_FLAG_NO_LDS) && (p.n_entries + 1) * 16 <= LDS_B &&
+                         lds_fixed_bytes(p.n_entries, p.n_quads, p.n_materials) <= LDS_MAX_BYTES;
+    return count ? launch_items_for<true>(p, use_lds, stream) : launch_items_for<false>(p, use_lds, stream);
 }
 
 }  // namespace rtxd

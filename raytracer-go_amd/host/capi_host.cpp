@@ -68,6 +68,24 @@ int64_t rtxhost_scene_world_spheres(const rtxhost_scene* s, rtx_sphere* out, uin
 
 const rtx_scene_desc* rtxhost_scene_desc(const rtxhost_scene* s) { return s ? &s->flat.desc : nullptr; }
 
+int rtxhost_synthetic_earth_ycbcr(uint64_t seed, int32_t w, int32_t h, uint8_t* y, uint8_t* cb, uint8_t* cr) {
+    g_err.clear();
+    if (w <= 0 || h <= 0 || !y || !cb || !cr) return set_err(Error{RTX_ERR_INVALID_ARG, "bad arguments"});
+    auto img = std::dynamic_pointer_cast<YCbCrImage>(SyntheticEarth(seed, w, h));
+    std::memcpy(y, img->Y.data(), img->Y.size());
+    std::memcpy(cb, img->Cb.data(), img->Cb.size());
+    std::memcpy(cr, img->Cr.data(), img->Cr.size());
+    return RTX_OK;
+}
+
+void rtxhost_ycbcr_rgba(uint8_t y, uint8_t cb, uint8_t cr, uint32_t out[4]) {
+    const RGBA64 c = YCbCrToRGBA(y, cb, cr);
+    out[0] = c.r;
+    out[1] = c.g;
+    out[2] = c.b;
+    out[3] = c.a;
+}
+
 static CameraPtr make_camera(const SceneSpec& spec, int32_t w, int32_t spp, int32_t depth, uint64_t seed, int gpus) {
     std::vector<CameraOpt> opts = spec.opts;
     if (spp > 0) opts.push_back(WithSamplesPerPixel(spp));

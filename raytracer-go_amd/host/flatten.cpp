@@ -44,14 +44,32 @@ struct Flattener {
             r.even[0] = c->even.X; r.even[1] = c->even.Y; r.even[2] = c->even.Z;
             r.odd[0] = c->odd.X; r.odd[1] = c->odd.Y; r.odd[2] = c->odd.Z;
         } else if (auto im = dynamic_cast<const ImageTexture*>(t.get())) {
+            // At(i, j).RGBA() for the raster, then the border colour (rtx.h RTX_TEX_IMAGE)
             r.type = RTX_TEX_IMAGE;
             const Image* img = im->img.get();
-            r.width = img ? (uint32_t)std::max(img->W, 0) : 0u;
-            r.height = img ? (uint32_t)std::max(img->H, 0) : 0u;
-            r.texel_offset = (uint32_t)fs.texels.size();
-            if (img && img->W > 0 && img->H > 0) {
-                if (img->rgba.size() != (size_t)img->W * img->H) return fail(RTX_ERR_INVALID_ARG, "image size mismatch");
-                fs.texels.insert(fs.texels.end(), img->rgba.begin(), img->rgba.end());
+            if (!img) return fail(RTX_ERR_INVALID_ARG, "ImageTexture with a nil image");
+            const Rectangle b = img->Bounds();
+            if (b.Dy() > 0) {
+                // GetTexture indexes At(int(u*Dx), int(v*Dy)) from 0, so the table is exact when
+                // the bounds start at the origin (jpeg.Decode, image.New*); others stay on the CPU.
+                if (b.MinX != 0 || b.MinY != 0)
+                    return fail(RTX_ERR_UNSUPPORTED, "ImageTexture whose Bounds().Min is not (0, 0)");
+                if (b.Dx() > 0xFFFFFFF || b.Dy() > 0xFFFFFFF) return fail(RTX_ERR_INVALID_ARG, "image too large");
+                r.width = (uint32_t)b.Dx();
+                r.height = (uint32_t)b.Dy();
+                if (fs.texels.size() & 1u) fs.texels.push_back(0);  // texel_offset even (8-B texels)
+                r.texel_offset = (uint32_t)fs.texels.size();
+                fs.texels.reserve(fs.texels.size() + 2 * ((size_t)r.width * r.height + 1));
+                auto put = [&](const RGBA64& c) {
+                    fs.texels.push_back((c.r & 0xFFFFu) | (c.g & 0xFFFFu) << 16);
+                    fs.texels.push_back((c.b & 0xFFFFu) | (c.a & 0xFFFFu) << 16);
+                };
+                for (int64_t j = 0; j < b.Dy(); ++j)
+                    for (int64_t i = 0; i < b.Dx(); ++i) put(img->At(i, j));
+                put(img->At(b.MaxX, b.MinY));  // outside the bounds
+            } else {
+                r.width = (uint32_t)std::max<int64_t>(b.Dx(), 0);
+                r.height = 0;  // Dy() <= 0: GetTexture's debug colour, no texels
             }
         } else if (auto nt = dynamic_cast<const NoiseTexture*>(t.get())) {  // RTX_NOISE_TEXELS layout
             const Perlin& per = nt->perlin;

@@ -128,12 +128,54 @@ public:
     float scale;
     Color even, odd;
 };
-// image.Image stand-in: an RGBA8 raster (image.RGBA), rows top to bottom.
-struct Image {
-    int W = 0, H = 0;
-    std::vector<uint32_t> rgba;  // r | g<<8 | b<<16 | a<<24
+// ---- Go's image package: what ImageTexture.GetTexture uses of an image.Image --------
+// (Bounds() and At(x, y).RGBA(); materials.go:175-193).  Go's `int` is 64-bit.
+struct Rectangle {  // image.Rectangle (image/geom.go)
+    int64_t MinX = 0, MinY = 0, MaxX = 0, MaxY = 0;
+    int64_t Dx() const { return MaxX - MinX; }
+    int64_t Dy() const { return MaxY - MinY; }
+    bool In(int64_t x, int64_t y) const { return MinX <= x && x < MaxX && MinY <= y && y < MaxY; }  // Point.In
+};
+Rectangle Rect(int64_t x0, int64_t y0, int64_t x1, int64_t y1);  // image.Rect (canonicalised)
+struct RGBA64 {  // color.Color.RGBA(): alpha-premultiplied 16-bit channels in uint32
+    uint32_t r = 0, g = 0, b = 0, a = 0;
+};
+class Image {  // image.Image
+public:
+    virtual ~Image() = default;
+    virtual Rectangle Bounds() const = 0;
+    virtual RGBA64 At(int64_t x, int64_t y) const = 0;  // At(x, y).RGBA()
 };
 using ImagePtr = std::shared_ptr<Image>;
+// *image.RGBA (image/image.go): 4 bytes per pixel, Pix[(y-Min.Y)*Stride + (x-Min.X)*4].
+// At outside Bounds is color.RGBA{} (0, 0, 0, 0); color.RGBA.RGBA() widens r to r | r<<8.
+class RGBAImage : public Image {
+public:
+    Rectangle Rect;
+    int64_t Stride = 0;
+    std::vector<uint8_t> Pix;
+    Rectangle Bounds() const override { return Rect; }
+    RGBA64 At(int64_t x, int64_t y) const override;
+};
+std::shared_ptr<RGBAImage> NewRGBA(Rectangle r);  // image.NewRGBA
+// *image.YCbCr (image/ycbcr.go), what jpeg.Decode returns for a colour JPEG: a Y plane and
+// Cb/Cr planes subsampled by SubsampleRatio.  At outside Bounds is color.YCbCr{} (Y = Cb =
+// Cr = 0), whose RGBA() is (0, 34678, 0, 65535) — a green, not black.
+enum class YCbCrSubsampleRatio { R444 = 0, R422, R420, R440, R411, R410 };
+class YCbCrImage : public Image {
+public:
+    std::vector<uint8_t> Y, Cb, Cr;
+    int64_t YStride = 0, CStride = 0;
+    YCbCrSubsampleRatio SubsampleRatio = YCbCrSubsampleRatio::R444;
+    Rectangle Rect;
+    Rectangle Bounds() const override { return Rect; }
+    RGBA64 At(int64_t x, int64_t y) const override;  // YCbCrAt(x, y).RGBA()
+    int64_t YOffset(int64_t x, int64_t y) const;
+    int64_t COffset(int64_t x, int64_t y) const;
+};
+std::shared_ptr<YCbCrImage> NewYCbCr(Rectangle r, YCbCrSubsampleRatio ratio);  // image.NewYCbCr
+// color.YCbCr{y, cb, cr}.RGBA() (image/color/ycbcr.go): 16-bit JFIF conversion.
+RGBA64 YCbCrToRGBA(uint8_t y, uint8_t cb, uint8_t cr);
 class ImageTexture : public Texture {
 public:
     explicit ImageTexture(ImagePtr im) : img(std::move(im)) {}

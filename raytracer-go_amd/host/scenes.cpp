@@ -97,35 +97,65 @@ SceneSpec StressSpheres(uint64_t seed, int n) {
     return s;
 }
 
-ImagePtr SyntheticEarth(uint64_t seed, int w, int h) {
-    auto img = std::make_shared<Image>();
-    img->W = w;
-    img->H = h;
-    img->rgba.resize((size_t)w * h);
+// The seeded earth-like colour of texel (x, y) of a w x h map, 8-bit RGB.
+static void earth_rgb(const float ph[6], uint32_t grain, int x, int y, int w, int h, uint32_t rgb[3]) {
+    const float lat = ((float)y + 0.5f) / (float)h;  // 0 top .. 1 bottom
+    const float lon = ((float)x + 0.5f) / (float)w;
+    const float a = std::sin(6.2831853f * 2.0f * lon + ph[0]) * std::sin(3.1415927f * 3.0f * lat + ph[1]);
+    const float b = 0.5f * std::sin(6.2831853f * 5.0f * lon + ph[2]) * std::cos(3.1415927f * 4.0f * lat + ph[3]);
+    const float c = 0.25f * std::sin(6.2831853f * 11.0f * lon + ph[4] + 3.0f * lat + ph[5]);
+    const float land = a + b + c;
+    if (lat < 0.07f || lat > 0.93f) {  // ice caps
+        rgb[0] = 225 + (grain & 15); rgb[1] = 230 + (grain & 15); rgb[2] = 240 + (grain & 15);
+    } else if (land > 0.35f) {         // land
+        rgb[0] = 70 + grain * 2; rgb[1] = 110 + grain; rgb[2] = 40 + grain;
+    } else {                           // ocean
+        rgb[0] = 10 + grain / 2; rgb[1] = 40 + grain; rgb[2] = 120 + grain * 2;
+    }
+}
+
+ImagePtr SyntheticEarthRGBA(uint64_t seed, int w, int h) {
+    auto img = NewRGBA(Rect(0, 0, w, h));
     Rand r(seed, kStreamTexture);
     // A few seeded low-frequency waves decide land vs ocean; a per-texel draw adds grain.
     float ph[6];
     for (float& v : ph) v = 6.2831853f * r.Float32();
-    for (int y = 0; y < h; ++y) {
-        const float lat = ((float)y + 0.5f) / (float)h;  // 0 top .. 1 bottom
+    for (int y = 0; y < h; ++y)
         for (int x = 0; x < w; ++x) {
-            const float lon = ((float)x + 0.5f) / (float)w;
-            const float a = std::sin(6.2831853f * 2.0f * lon + ph[0]) * std::sin(3.1415927f * 3.0f * lat + ph[1]);
-            const float b = 0.5f * std::sin(6.2831853f * 5.0f * lon + ph[2]) * std::cos(3.1415927f * 4.0f * lat + ph[3]);
-            const float c = 0.25f * std::sin(6.2831853f * 11.0f * lon + ph[4] + 3.0f * lat + ph[5]);
-            const float land = a + b + c;
-            const uint32_t grain = r.Uint32() & 31u;
-            uint32_t R, G, B;
-            if (lat < 0.07f || lat > 0.93f) {  // ice caps
-                R = 225 + (grain & 15); G = 230 + (grain & 15); B = 240 + (grain & 15);
-            } else if (land > 0.35f) {         // land
-                R = 70 + grain * 2; G = 110 + grain; B = 40 + grain;
-            } else {                           // ocean
-                R = 10 + grain / 2; G = 40 + grain; B = 120 + grain * 2;
-            }
-            img->rgba[(size_t)y * w + x] = R | (G << 8) | (B << 16) | (255u << 24);
+            uint32_t rgb[3];
+            earth_rgb(ph, r.Uint32() & 31u, x, y, w, h, rgb);
+            uint8_t* p = &img->Pix[(size_t)(y * img->Stride + 4 * x)];
+            p[0] = (uint8_t)rgb[0]; p[1] = (uint8_t)rgb[1]; p[2] = (uint8_t)rgb[2]; p[3] = 255;
         }
-    }
+    return img;
+}
+
+// The planes a baseline JFIF encoder + jpeg.Decode would give for the same map: 4:2:0,
+// Y per texel and Cb/Cr per 2x2 block (from the block's top-left texel), with
+// integer JFIF forward transforms and a seeded +-1 grain on Y.  Only the decoder side
+// (YCbCr.At / RGBA) has to match Go; this is just a deterministic source of planes.
+ImagePtr SyntheticEarth(uint64_t seed, int w, int h) {
+    auto img = NewYCbCr(Rect(0, 0, w, h), YCbCrSubsampleRatio::R420);
+    Rand r(seed, kStreamTexture);
+    float ph[6];
+    for (float& v : ph) v = 6.2831853f * r.Float32();
+    auto clamp8 = [](int v) { return (uint8_t)(v < 0 ? 0 : (v > 255 ? 255 : v)); };
+    for (int y = 0; y < h; ++y)
+        for (int x = 0; x < w; ++x) {
+            const uint32_t word = r.Uint32();
+            uint32_t c[3];
+            earth_rgb(ph, word & 31u, x, y, w, h, c);
+            const int R = (int)c[0], G = (int)c[1], B = (int)c[2];
+            const int yy = (19595 * R + 38470 * G + 7471 * B + (1 << 15)) >> 16;
+            img->Y[(size_t)img->YOffset(x, y)] = clamp8(yy + (int)((word >> 5) % 3u) - 1);
+            if ((x & 1) == 0 && (y & 1) == 0) {
+                const int cb = ((-11056 * R - 21712 * G + 32768 * B + (1 << 15)) >> 16) + 128;
+                const int cr = ((32768 * R - 27440 * G - 5328 * B + (1 << 15)) >> 16) + 128;
+                const size_t ci = (size_t)img->COffset(x, y);
+                img->Cb[ci] = clamp8(cb);
+                img->Cr[ci] = clamp8(cr);
+            }
+        }
     return img;
 }
 
@@ -150,19 +180,19 @@ SceneSpec EarthDielectric(uint64_t seed, int tex_w, int tex_h) {
     return s;
 }
 
-SceneSpec Earth(uint64_t seed, int tex_w, int tex_h) {  // main.go:80-104
+SceneSpec Earth(uint64_t seed, int tex_w, int tex_h, ImagePtr img, float look_z) {  // main.go:80-104
     SceneSpec s;
     s.name = "earth";
     s.opts = {WithSamplesPerPixel(100),
               WithMaxRayDepth(50),
-              WithLookFrom(NewVec3(0, 0, 12)),
+              WithLookFrom(NewVec3(0, 0, look_z)),
               WithLookAt(NewVec3(0, 0, 0)),
               WithFOVDegrees(20),
               WithDefocusAngleDegrees(0),
               WithBackgroundColor(NewVec3(0.7f, 0.8f, 1))};
     Seed(seed);
     auto world = NewWorld();
-    auto mat = NewLambertian(NewImageTexture(SyntheticEarth(seed, tex_w, tex_h)));
+    auto mat = NewLambertian(NewImageTexture(img ? img : SyntheticEarth(seed, tex_w, tex_h)));
     world->Add(NewSphere(NewVec3(0, 0, 0), 2, mat));
     s.list = world;
     s.bvh_draw0 = GlobalRand().Drawn();
@@ -291,6 +321,11 @@ bool BuildScene(const std::string& name, uint64_t seed, SceneSpec& out) {
     else if (name == "stress_100k") out = StressSpheres(seed, 100000);
     else if (name == "earth_dielectric") out = EarthDielectric(seed, 2048, 1024);
     else if (name == "earth") out = Earth(seed, 2048, 1024);
+    // main.go's earth with the map as an *image.RGBA instead of jpeg.Decode's *image.YCbCr
+    else if (name == "earth_rgba") out = Earth(seed, 2048, 1024, SyntheticEarthRGBA(seed, 2048, 1024));
+    // main.go's earth seen from -z: the far side, where u = (phi + 5 pi/12) / 2 pi reaches 1
+    // (hittables.go:125) and GetTexture reads At(Dx, j), outside the image
+    else if (name == "earth_far_side") out = Earth(seed, 2048, 1024, nullptr, -12.0f);
     else if (name == "quad_demo") out = QuadDemo(seed);
     else if (name == "cornell_box") out = CornellBox(seed);
     else if (name == "perlin_demo") out = PerlinDemo(seed);

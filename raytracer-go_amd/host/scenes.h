@@ -32,9 +32,14 @@ SceneSpec StressSpheres(uint64_t seed, int n);
 SceneSpec EarthDielectric(uint64_t seed, int tex_w, int tex_h);
 // earth, main.go:80-104, with a synthetic texture standing in for the missing
 // textures/earthmap.jpg (.MISSING_LARGE_BLOBS:2).
-SceneSpec Earth(uint64_t seed, int tex_w, int tex_h);
-// A seeded RGBA8 "earth-like" raster (oceans, continents, ice caps).
+// img: the texture (default SyntheticEarth); look_z: the camera's z (main.go: 12).
+SceneSpec Earth(uint64_t seed, int tex_w, int tex_h, ImagePtr img = nullptr, float look_z = 12.0f);
+// A seeded "earth-like" map (oceans, continents, ice caps) as the *image.YCbCr 4:2:0 a
+// colour JPEG decodes to (jpeg.Decode, file.go:20-28): what main.go's earth scene and
+// config 5 texture with, standing in for the missing textures/earthmap.jpg.
 ImagePtr SyntheticEarth(uint64_t seed, int w, int h);
+// The same map as an *image.RGBA (8-bit channels, black outside the bounds).
+ImagePtr SyntheticEarthRGBA(uint64_t seed, int w, int h);
 
 // quadDemo, main.go:132-160: five Lambertian quads.
 SceneSpec QuadDemo(uint64_t seed);
@@ -47,8 +52,8 @@ SceneSpec CornellBox(uint64_t seed);
 SceneSpec PerlinDemo(uint64_t seed);
 SceneSpec SimpleLightDemo(uint64_t seed);
 
-// By name: "random_spheres", "stress_100k", "earth_dielectric", "earth", "quad_demo",
-// "cornell_box", "perlin_demo", "simple_light_demo".
+// By name: "random_spheres", "stress_100k", "earth_dielectric", "earth", "earth_rgba",
+// "earth_far_side", "quad_demo", "cornell_box", "perlin_demo", "simple_light_demo".
 bool BuildScene(const std::string& name, uint64_t seed, SceneSpec& out);
 
 }  // namespace internal

@@ -26,20 +26,12 @@ RTX_PRIM_QUAD = 1
 RTX_MAT_LAMBERTIAN, RTX_MAT_METAL, RTX_MAT_DIELECTRIC, RTX_MAT_DIFFUSE_LIGHT = 0, 1, 2, 3
 RTX_TEX_SOLID, RTX_TEX_CHECKERED, RTX_TEX_IMAGE, RTX_TEX_NOISE = 0, 1, 2, 3
 RTX_FLAG_COUNTERS = 1
-RTX_FLAG_KERNEL_V0 = 2
 RTX_FLAG_NO_LDS = 4
-RTX_FLAG_KERNEL_POOL = 8
-RTX_FLAG_POOL4 = 16
-RTX_FLAG_KERNEL_ITEMS = 32
-RTX_FLAG_KERNEL_V1 = 64
+RTX_IMAGE_TEXEL_WORDS = 2  # RGBA16 image texels: two uint32 words each (rtx.h)
 
 
 def RTX_FLAG_SHADE_THRESH(n: int) -> int:
     return (n & 0x7F) << 8
-
-
-def RTX_FLAG_WAVE_GEOM(n: int) -> int:
-    return (n & 7) << 24
 
 
 def ref_prim(ptype: int, index: int) -> int:
@@ -99,7 +91,7 @@ class Stats(ctypes.Structure):
                 ("rng_draws", c_uint64), ("kernel_ms", c_double), ("gather_ms", c_double),
                 ("wave_iters", c_uint64), ("lane_steps", c_uint64), ("shade_phases", c_uint64),
                 ("shade_lanes", c_uint64), ("trav_cycles", c_uint64), ("shade_cycles", c_uint64),
-                ("idle_lanes", c_uint64), ("cache_hits", c_uint64)]
+                ("idle_lanes", c_uint64), ("cache_hits", c_uint64), ("sample_chunks", c_uint64)]
 
     def as_dict(self) -> dict:
         return {name: getattr(self, name) for name, _ in self._fields_}
@@ -109,10 +101,12 @@ RTX_SYMBOLS = [
     "rtx_version", "rtx_build_info", "rtx_last_error", "rtx_device_count", "rtx_scene_create",
     "rtx_scene_destroy", "rtx_scene_device_bytes", "rtx_render", "rtx_render_region_device", "rtx_region_rows",
     "rtx_ppm_max_bytes", "rtx_encode_ppm_device", "rtx_render_ppm", "rtx_scene_create_spheres", "rtx_scene_export",
+    "rtx_release_device_memory", "rtx_device_scratch_bytes",
 ]
 RTXHOST_SYMBOLS = [
     "rtxhost_build_scene", "rtxhost_scene_free", "rtxhost_scene_desc", "rtxhost_scene_camera",
     "rtxhost_render_ppm", "rtxhost_ppm_encode", "rtxhost_last_error", "rtxhost_scene_world_spheres",
+    "rtxhost_synthetic_earth_ycbcr", "rtxhost_ycbcr_rgba",
 ]
 
 _lib = None
@@ -162,6 +156,10 @@ def load() -> ctypes.CDLL:
     L.rtx_scene_create_spheres.restype = c_int
     L.rtx_scene_export.argtypes = [c_void_p, c_void_p, c_uint64]
     L.rtx_scene_export.restype = c_uint64
+    L.rtx_release_device_memory.argtypes = [c_int]
+    L.rtx_release_device_memory.restype = c_int
+    L.rtx_device_scratch_bytes.argtypes = [c_int]
+    L.rtx_device_scratch_bytes.restype = c_uint64
     _lib = L
     return L
 
@@ -190,6 +188,10 @@ def load_host() -> ctypes.CDLL:
     H.rtxhost_last_error.restype = c_char_p
     H.rtxhost_scene_world_spheres.argtypes = [c_void_p, POINTER(Sphere), c_uint64, POINTER(c_uint64), POINTER(c_uint64)]
     H.rtxhost_scene_world_spheres.restype = ctypes.c_int64
+    H.rtxhost_synthetic_earth_ycbcr.argtypes = [c_uint64, c_int32, c_int32, c_void_p, c_void_p, c_void_p]
+    H.rtxhost_synthetic_earth_ycbcr.restype = c_int
+    H.rtxhost_ycbcr_rgba.argtypes = [ctypes.c_uint8, ctypes.c_uint8, ctypes.c_uint8, POINTER(c_uint32)]
+    H.rtxhost_ycbcr_rgba.restype = None
     _host = H
     return H
 
@@ -221,7 +223,9 @@ class HostScene:
 
     @property
     def desc(self):
-        return load_host().rtxhost_scene_desc(self._h)
+        d = load_host().rtxhost_scene_desc(self._h)
+        d._owner = self  # the tables live in this scene: keep it alive as long as the pointer
+        return d
 
     def camera(self, width: int = 0, spp: int = 0, depth: int = 0) -> Camera:
         cam = Camera()
@@ -336,6 +340,35 @@ class DeviceScene:
             self.close()
         except Exception:
             pass
+
+
+def release_device_memory(device: int = -1) -> None:
+    """rtx_release_device_memory: free the per-device scratch (and RCCL communicators)."""
+    check(load().rtx_release_device_memory(device), "rtx_release_device_memory")
+
+
+def device_scratch_bytes(device: int = 0) -> int:
+    return int(load().rtx_device_scratch_bytes(device))
+
+
+def synthetic_earth_ycbcr(seed: int, w: int = 2048, h: int = 1024):
+    """(Y [h, w], Cb, Cr [(h+1)//2, (w+1)//2]) uint8 planes of the earth scenes' *image.YCbCr map."""
+    import numpy as np
+    cw, ch = (w + 1) // 2, (h + 1) // 2
+    Y = np.empty((h, w), dtype=np.uint8)
+    Cb = np.empty((ch, cw), dtype=np.uint8)
+    Cr = np.empty((ch, cw), dtype=np.uint8)
+    rc = load_host().rtxhost_synthetic_earth_ycbcr(seed, w, h, Y.ctypes.data_as(c_void_p), Cb.ctypes.data_as(c_void_p),
+                                                   Cr.ctypes.data_as(c_void_p))
+    if rc != RTX_OK:
+        raise RtxError(rc, load_host().rtxhost_last_error().decode())
+    return Y, Cb, Cr
+
+
+def host_ycbcr_rgba(y: int, cb: int, cr: int):
+    o = (c_uint32 * 4)()
+    load_host().rtxhost_ycbcr_rgba(y, cb, cr, o)
+    return tuple(o)
 
 
 def region_rows(region: Region) -> int:

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """A/B kernel variants on one device, interleaved rounds in one process (guide §5.4 rule 24).
 
-  python scripts/ab.py [--width 1920] [--spp 100] [--rounds 3] [--variants v1,v0,nolds]
+  python scripts/ab.py [--width 1920] [--spp 100] [--rounds 3] [--variants v3,nolds,t40]
+  (RTX_LIB=path selects another build of librtx.so: scripts/gpu_ab_libs.sh)
 Checks that every variant's image is bit-identical to the first one."""
 import argparse
 import os
@@ -14,15 +15,9 @@ import torch  # noqa: E402
 
 import rtx  # noqa: E402
 
-POOL = 8  # RTX_FLAG_KERNEL_POOL
-V1 = rtx.RTX_FLAG_KERNEL_V1
-VARIANTS = {"v3": 0, "v1": V1, "v2": POOL, "v0": rtx.RTX_FLAG_KERNEL_V0, "nolds": rtx.RTX_FLAG_NO_LDS,
-            "v1nolds": V1 | rtx.RTX_FLAG_NO_LDS, "p4": POOL | 16}
-for _g in range(8):
-    VARIANTS[f"g{_g}"] = V1 | rtx.RTX_FLAG_WAVE_GEOM(_g)
+VARIANTS = {"v3": 0, "nolds": rtx.RTX_FLAG_NO_LDS}
 for _t in range(1, 65):
-    VARIANTS[f"t{_t}"] = _t << 8  # RTX_FLAG_SHADE_THRESH (default schedule)
-    VARIANTS[f"v2t{_t}"] = (_t << 8) | POOL
+    VARIANTS[f"t{_t}"] = rtx.RTX_FLAG_SHADE_THRESH(_t)
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--scene", default="random_spheres")
@@ -30,7 +25,7 @@ ap.add_argument("--width", type=int, default=1920)
 ap.add_argument("--spp", type=int, default=100)
 ap.add_argument("--rounds", type=int, default=3)
 ap.add_argument("--depth", type=int, default=0, help="max depth (0: the scene's)")
-ap.add_argument("--variants", default="v1,v0")
+ap.add_argument("--variants", default="v3,nolds")
 args = ap.parse_args()
 
 torch.cuda.set_device(0)

@@ -25,7 +25,7 @@ ORDER_ITERATIVE = 1
 class Counters(ctypes.Structure):
     _fields_ = [("samples", c_uint64), ("segments", c_uint64), ("node_visits", c_uint64),
                 ("prim_tests_ref", c_uint64), ("prim_tests", c_uint64), ("hits", c_uint64),
-                ("texel_fetches", c_uint64), ("rng_draws", c_uint64)]
+                ("texel_fetches", c_uint64), ("rng_draws", c_uint64), ("texel_border", c_uint64)]
 
     def as_dict(self) -> dict:
         return {name: int(getattr(self, name)) for name, _ in self._fields_}
@@ -80,6 +80,13 @@ def load():
     L.oracle_go_sin.restype = ctypes.c_double
     L.oracle_noise_texture.argtypes = [POINTER(c_uint32), c_float, POINTER(c_float)]
     L.oracle_noise_texture.restype = c_float
+    L.oracle_ycbcr_rgba.argtypes = [ctypes.c_uint8, ctypes.c_uint8, ctypes.c_uint8, POINTER(c_uint32)]
+    L.oracle_ycbcr_rgba.restype = None
+    L.oracle_ycbcr_rgba_all.argtypes = [c_void_p]
+    L.oracle_ycbcr_rgba_all.restype = None
+    L.oracle_ycbcr_texels.argtypes = [c_void_p, c_void_p, c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
+                                      ctypes.c_int64, c_int, c_void_p]
+    L.oracle_ycbcr_texels.restype = c_int
     _lib = L
     return L
 
@@ -91,6 +98,32 @@ def philox(ctr, key):
     O = (c_uint32 * 4)()
     L.oracle_philox4x32_10(C, K, O)
     return list(O)
+
+
+def ycbcr_rgba(y: int, cb: int, cr: int):
+    """color.YCbCr{y, cb, cr}.RGBA() (r, g, b) as the oracle restates it."""
+    o = (c_uint32 * 3)()
+    load().oracle_ycbcr_rgba(y, cb, cr, o)
+    return tuple(o)
+
+
+def ycbcr_rgba_all():
+    """[2^24, 3] uint32: RGBA() of every (y, cb, cr), index y << 16 | cb << 8 | cr."""
+    out = np.empty((1 << 24, 3), dtype=np.uint32)
+    load().oracle_ycbcr_rgba_all(out.ctypes.data_as(c_void_p))
+    return out
+
+
+def ycbcr_texels(Y, Cb, Cr, w: int, h: int, ratio: int = 2):
+    """The RTX_TEX_IMAGE words (RGBA16 raster + border) of an *image.YCbCr (0,0)-(w,h)."""
+    cw = {0: w, 1: (w + 1) // 2, 2: (w + 1) // 2, 3: w, 4: (w + 3) // 4, 5: (w + 3) // 4}[ratio]
+    Y, Cb, Cr = (np.ascontiguousarray(a, dtype=np.uint8) for a in (Y, Cb, Cr))
+    out = np.empty(2 * (w * h + 1), dtype=np.uint32)
+    rc = load().oracle_ycbcr_texels(Y.ctypes.data_as(c_void_p), Cb.ctypes.data_as(c_void_p),
+                                    Cr.ctypes.data_as(c_void_p), w, h, w, cw, ratio, out.ctypes.data_as(c_void_p))
+    if rc != 0:
+        raise RuntimeError("oracle_ycbcr_texels rejected its arguments")
+    return out
 
 
 def region_rows(reg: rtx.Region) -> int:

@@ -1,0 +1,47 @@
+"""bench.py's own rank launcher on the CPU: `python bench.py --gpus N` without torchrun starts
+N rank processes (RANK / WORLD_SIZE / MASTER_* as torch.distributed.run sets them), and the
+ranks run the multi-GPU plumbing of the bench — process group, row-interleaved shards, the
+gather to rank 0, de-interleave, rank 0's single JSON line with the framebuffer hash — over
+gloo, with each shard filled with its global pixel index instead of a render (the GPU path
+swaps in "nccl" = RCCL and the megakernel)."""
+import hashlib
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def expected_hash(W):
+    H = W * 9 // 16
+    img = np.repeat((np.arange(H * W, dtype=np.float32).reshape(H, W))[..., None], 3, axis=2)
+    return hashlib.sha256(np.ascontiguousarray(img).tobytes()).hexdigest()[:16]
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 8])
+def test_plain_launch_spawns_ranks(n):
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
+    res = subprocess.run([sys.executable, "bench.py", "--gpus", str(n), "--selftest-gloo", "--width", "64"],
+                         cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert res.returncode == 0, res.stderr[-3000:]
+    lines = [ln for ln in res.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, res.stdout  # only rank 0 prints
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == n and out["world_size"] == n
+    assert out["backend"] == ("gloo" if n > 1 else None)
+    assert out["framebuffer_sha256_16"] == expected_hash(64)
+
+
+def test_failed_rank_fails_the_launch():
+    env = dict(os.environ)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
+        env.pop(k, None)
+    # rank 1 exits before joining the process group, leaving rank 0 waiting in the rendezvous:
+    # the launcher must stop it and return non-zero, not hang.
+    res = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--selftest-gloo", "--selftest-fail-rank", "1"],
+                         cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert res.returncode != 0

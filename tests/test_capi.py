@@ -34,7 +34,7 @@ def test_binding_lists_match_headers(built):
 
 def test_version_and_build_info(built):
     L = rtx.load()
-    assert L.rtx_version() == 3
+    assert L.rtx_version() == 4
     assert b"gfx950" in L.rtx_build_info()
 
 
@@ -181,3 +181,20 @@ def test_ref_prim_encoding():
     assert rtx.ref_prim(0, 0) == -1
     assert rtx.ref_prim(0, 5) == ~5
     assert rtx.ref_prim(1, 3) == ~((1 << 28) | 3)
+
+
+def test_image_texture_validation(built):
+    """RTX_TEX_IMAGE holds width*height RGBA16 texels (2 words each) plus the border texel,
+    at an even word offset (include/rtx.h)."""
+    t = texture(rtx.RTX_TEX_IMAGE)
+    t.width, t.height = 2, 2
+    words = (ctypes.c_uint32 * 10)()
+    d = make_desc([sphere()], [lambertian()], [t])
+    d.texels, d.n_texels = words, 8  # the raster without its border texel
+    rc, msg = create(d)
+    assert rc == rtx.RTX_ERR_INVALID_ARG and "texels out of range" in msg
+    t.texel_offset = 1
+    d = make_desc([sphere()], [lambertian()], [t])
+    d.texels, d.n_texels = words, 10
+    rc, msg = create(d)
+    assert rc == rtx.RTX_ERR_INVALID_ARG and "even" in msg

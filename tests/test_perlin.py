@@ -124,7 +124,8 @@ def test_oracle_noise_texture_matches_numpy(built):
 
 
 def test_scene_shapes(built):
-    a = rtx.HostScene("perlin_demo", 1).desc.contents
+    ha = rtx.HostScene("perlin_demo", 1)
+    a = ha.desc.contents
     assert a.n_spheres == 2 and a.n_quads == 0
     b = rtx.HostScene("simple_light_demo", 1)
     d = b.desc.contents
@@ -174,9 +175,9 @@ def gpu_check(torch, scene, cam, seed, reg, flags=0):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("flags", [0, rtx.RTX_FLAG_KERNEL_V1, rtx.RTX_FLAG_NO_LDS], ids=["v3", "v1-flag", "global"])
+@pytest.mark.parametrize("flags", [0, 64, rtx.RTX_FLAG_NO_LDS], ids=["v3", "removed-v1-flag", "global"])
 def test_gpu_perlin_demo_full(torch_cuda, built, flags):
-    """perlinDemo at 400x225x4 spp (the V1 flag still runs v3: Perlin scenes are v3-only)."""
+    """perlinDemo at 400x225x4 spp (the flag bit of the removed v1 schedule is ignored)."""
     s = rtx.HostScene("perlin_demo", 1)
     cam = s.camera(spp=4)
     gpu_check(torch_cuda, s, cam, 2, rtx.Region(0, 0, cam.image_width, cam.image_height, 0, 1), flags)

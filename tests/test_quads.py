@@ -203,8 +203,7 @@ def test_gpu_light_panel(torch_cuda, built):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("flags", [0, rtx.RTX_FLAG_KERNEL_V1, rtx.RTX_FLAG_KERNEL_V0, rtx.RTX_FLAG_NO_LDS],
-                         ids=["v3", "v1", "v0", "v3-global"])
+@pytest.mark.parametrize("flags", [0, rtx.RTX_FLAG_NO_LDS], ids=["v3", "v3-global"])
 def test_gpu_quad_demo_full(torch_cuda, built, flags):
     s = rtx.HostScene("quad_demo", 1)
     cam = s.camera(spp=8)
