@@ -165,6 +165,8 @@ def schedule(st: dict) -> dict:
         it = 64.0 * st["wave_iters"]
         out["trav_lane_util"] = round(st["lane_steps"] / it, 4)
         out["idle_lane_frac"] = round(st["idle_lanes"] / it, 4)
+        out["parked_lane_frac"] = round(st.get("parked_lanes", 0) / it, 4)  # waiting to shade
+        out["deferred_lane_frac"] = round(st.get("deferred_lanes", 0) / it, 4)  # other entry kind
         cyc = st["trav_cycles"] + st["shade_cycles"]
         out["shade_cycle_share"] = round(st["shade_cycles"] / cyc, 4) if cyc else None
     reads = st.get("node_visits", 0) + st.get("prim_tests", 0)

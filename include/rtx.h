@@ -220,6 +220,10 @@ typedef struct rtx_stats {
                               levels */
     uint64_t sample_chunks; /* launches of the render kernel: the samples of every pixel run in
                                chunks that fit the per-device colour scratch (always filled) */
+    uint64_t parked_lanes;   /* lanes parked on the end sentinel (waiting to shade, or without
+                                an item) per walk step, summed over steps / steps per vote   */
+    uint64_t deferred_lanes; /* lanes whose entry kind (node / primitive) a batched walk step
+                                did not run, likewise                                        */
 } rtx_stats;
 
 #define RTX_FLAG_COUNTERS 1u /* count work units (separate kernel instantiation) */

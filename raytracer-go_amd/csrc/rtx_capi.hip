@@ -386,7 +386,7 @@ int upload_copy(rtx_scene* s, DeviceCopy& c) {
     HIP_TRY(hipMalloc(&c.texels, std::max<size_t>(1, s->texels.size()) * sizeof(uint32_t)));
     if (!s->texels.empty())
         HIP_TRY(hipMemcpy(c.texels, s->texels.data(), s->texels.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
-    HIP_TRY(hipMalloc(&c.counters, 16 * sizeof(unsigned long long)));
+    HIP_TRY(hipMalloc(&c.counters, rtxd::COUNTER_SLOTS * sizeof(unsigned long long)));
     HIP_TRY(hipEventCreate(&c.ev0));
     HIP_TRY(hipEventCreate(&c.ev1));
     return RTX_OK;
@@ -487,7 +487,7 @@ rtxd::Params make_params(const rtx_scene* s, const DeviceCopy* c, const rtx_came
     p.world = r->world;
     p.out = d_out;
     p.counters = c->counters;
-    p.tile_counter = reinterpret_cast<uint32_t*>(c->counters + 7);  // slot 7 low: v2 tile queue head
+    p.tile_counter = reinterpret_cast<uint32_t*>(c->counters + 7);  // slot 7 low: unit queue head
     p.error_flag = reinterpret_cast<uint32_t*>(c->counters + 7) + 1;  // slot 7 high: watchdog flag
     p.watchdog_ticks = watchdog_ticks();
     p.shade_thresh = shade_thresh();
@@ -538,7 +538,7 @@ int enqueue_on(rtx_scene* s, DeviceCopy* c, const rtx_camera* cam, uint64_t seed
         p.prim_batch = env_knob("RTX_PRIM_BATCH", 16, 1, 65);  // 65: primitive tests only when no node is left
     }
     // every stats slot, the unit queue head and the watchdog flag start at 0 for every render
-    HIP_TRY(hipMemsetAsync(c->counters, 0, 16 * sizeof(unsigned long long), stream));
+    HIP_TRY(hipMemsetAsync(c->counters, 0, rtxd::COUNTER_SLOTS * sizeof(unsigned long long), stream));
     if (timed) HIP_TRY(hipEventRecord(c->ev0, stream));
     HIP_TRY(rtxd::launch_render(p, flags, stream));
     if (timed) HIP_TRY(hipEventRecord(c->ev1, stream));
@@ -551,8 +551,8 @@ int collect_on(DeviceCopy* c, bool count, uint64_t samples, uint32_t chunks, rtx
     HIP_TRY(hipEventSynchronize(c->ev1));
     float ms = 0.0f;
     HIP_TRY(hipEventElapsedTime(&ms, c->ev0, c->ev1));
-    unsigned long long h[16] = {0};
-    HIP_TRY(hipMemcpy(h, c->counters, 16 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    unsigned long long h[rtxd::COUNTER_SLOTS] = {0};
+    HIP_TRY(hipMemcpy(h, c->counters, rtxd::COUNTER_SLOTS * sizeof(unsigned long long), hipMemcpyDeviceToHost));
     if ((h[7] >> 32) != 0) return fail(RTX_ERR_HIP, "render kernel watchdog fired (RTX_WATCHDOG_S): output incomplete");
     std::memset(st, 0, sizeof(*st));
     st->samples = count ? h[0] : samples;
@@ -570,6 +570,8 @@ int collect_on(DeviceCopy* c, bool count, uint64_t samples, uint32_t chunks, rtx
     st->shade_cycles = h[13];
     st->idle_lanes = h[14];
     st->cache_hits = h[15];
+    st->parked_lanes = h[16];
+    st->deferred_lanes = h[17];
     st->sample_chunks = chunks;
     st->kernel_ms = ms;
     return RTX_OK;
@@ -676,6 +678,8 @@ void add_stats(rtx_stats* acc, const rtx_stats& s) {
     acc->shade_cycles += s.shade_cycles;
     acc->idle_lanes += s.idle_lanes;
     acc->cache_hits += s.cache_hits;
+    acc->parked_lanes += s.parked_lanes;
+    acc->deferred_lanes += s.deferred_lanes;
     acc->sample_chunks = std::max(acc->sample_chunks, s.sample_chunks);
 }
 

@@ -383,6 +383,8 @@ constexpr uint32_t RTX_DEV_TEX_INLINE = 0xFFFFFFFFu;
 // ---------------------------------------------------------------------------------
 // Kernel parameters
 // ---------------------------------------------------------------------------------
+constexpr uint32_t COUNTER_SLOTS = 24;  // device stats slots (rtx_capi.hip collect_on)
+
 struct Params {
     const float4* entries;   // n_entries + 1 'a' halves, as many 'b', 4 * n_quads (SceneRef)
     uint32_t n_entries;
@@ -395,7 +397,7 @@ struct Params {
     uint64_t seed;
     uint32_t x0, y0, width, rows, rank, world;
     float* out;
-    unsigned long long* counters;  // rtx_stats order when counting (16 x u64)
+    unsigned long long* counters;  // rtx_stats order when counting (COUNTER_SLOTS x u64)
     uint32_t shade_thresh;         // shade once this many lanes of a wave wait (1..64)
     uint32_t* tile_counter;        // global unit queue head (zeroed before each chunk's launch)
     uint32_t* error_flag;          // set to 1 by a wave that hit the watchdog (zeroed per render)
@@ -581,6 +583,7 @@ struct Trav {
     int32_t hit;
     float closest, ix, iy, iz, a;
     bool nx, ny, nz;
+    bool safe;  // 1/dir and the origin are finite: box_step<.., MED3 = true> is exact for this ray
 };
 
 __device__ __forceinline__ void trav_begin(Trav& t, const Ray& r) {
@@ -591,6 +594,8 @@ __device__ __forceinline__ void trav_begin(Trav& t, const Ray& r) {
     t.nx = t.ix < 0.0f;
     t.ny = t.iy < 0.0f;
     t.nz = t.iz < 0.0f;
+    t.safe = __builtin_isfinite(t.ix) && __builtin_isfinite(t.iy) && __builtin_isfinite(t.iz) &&
+             __builtin_isfinite(r.o.x) && __builtin_isfinite(r.o.y) && __builtin_isfinite(r.o.z);
     t.a = lensq(r.d);  // hittables.go:98, loop-invariant
     t.closest = __builtin_inff();
     t.hit = -1;
@@ -681,13 +686,41 @@ __device__ __forceinline__ void sphere_test(Trav& t, const Ray& r, const float4 
     }
 }
 
+// v_med3_f32 (no canonicalisation of the operands: they are products, tmin or the running bound).
+__device__ __forceinline__ float med3(float a, float b, float c) {
+    float d;
+    asm("v_med3_f32 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+    return d;
+}
+
 // Aabb.Hit (bvh.go:52-61, 84-102) of the node entry (ea, eb) with next position `tag`:
 // the walk moves to the next entry on a hit, else to the escape.
-template <bool COUNT>
+//
+// MED3 (rays with t.safe): per axis ta = (min - o) * invD and tb = (max - o) * invD
+// without the sign selects, and both bounds clamped into [min(ta, tb), max(ta, tb)] by one
+// v_med3_f32 each: lo = clamp(lo, n, f), hi = clamp(hi, n, f).  While [lo, hi] and the axis
+// slab overlap, the clamps leave lo = max(lo, n) and hi = min(hi, f) — the reference's swap and
+// bound updates; once they are disjoint, lo and hi collapse onto the same slab end and stay
+// ordered lo >= hi (clamping is monotone), so `lo < hi` after three axes is exactly the
+// reference's per-axis early-exit result.  It needs NaN-free slab distances: finite 1/dir and
+// origin (a zero direction component gives 1/dir = inf and 0 * inf = NaN when the origin lies
+// on a slab plane, which the reference ignores (`t0 > min` is false for NaN) — those rays take
+// the select path).  20 VALU per box instead of 24.
+template <bool COUNT, bool MED3 = false>
 __device__ __forceinline__ void box_step(Trav& t, const Ray& r, const float4 ea, const float4 eb, int32_t tag,
                                          Counters& cnt) {
     const float tmin = 0.001f;  // ray.go:37
     if (COUNT && __float_as_int(ea.w) != tag) ++cnt.node_visits;  // (not the sentinel: escape == next)
+    if constexpr (MED3) {
+        const float tax = (ea.x - r.o.x) * t.ix, tbx = (eb.x - r.o.x) * t.ix;
+        const float tay = (ea.y - r.o.y) * t.iy, tby = (eb.y - r.o.y) * t.iy;
+        const float taz = (ea.z - r.o.z) * t.iz, tbz = (eb.z - r.o.z) * t.iz;
+        const float lo = med3(med3(med3(tmin, tax, tbx), tay, tby), taz, tbz);
+        const float hi = med3(med3(med3(t.closest, tax, tbx), tay, tby), taz, tbz);
+        const uint32_t take = 0u - (uint32_t)(lo < hi);
+        t.i = ((uint32_t)tag & take) | ((uint32_t)__float_as_int(ea.w) & ~take);
+        return;
+    }
     // Per axis: t0 = (min - o) * invD, t1 = (max - o) * invD, swapped if invD < 0.
     // (Scalar FP32 throughout: a v_pk_mul_f32 / v_pk_add_f32 issues at a quarter of
     // v_mul_f32's rate on gfx950, scripts/micro/pk_rate.hip, so packing loses 2x.)
@@ -718,7 +751,7 @@ __device__ __forceinline__ void box_step(Trav& t, const Ray& r, const float4 ea,
 // running bound `closest` = the closest hit so far (bvh.go:227-232).
 // QUADS: the scene holds quads (a third entry kind); false compiles the sphere-only step.
 // FIXED: E is v3's LDS layout at LDS address 0 (scene_ref_fixed).
-template <bool COUNT, bool QUADS = false, bool FIXED = false, bool HYB = false>
+template <bool COUNT, bool QUADS = false, bool FIXED = false, bool HYB = false, bool MED3 = false>
 __device__ __forceinline__ void trav_step(Trav& t, const Ray& r, const SceneRef E, Counters& cnt) {
     float4 ea, eb;
     load_entry<FIXED, HYB>(E, t.i, ea, eb);
@@ -726,7 +759,7 @@ __device__ __forceinline__ void trav_step(Trav& t, const Ray& r, const SceneRef 
     const int32_t tag = __float_as_int(eb.w);  // device recoding, rtx_layout.h
     // (tag > -2, not tag >= 0: a sign test became a 64-bit compare of eb.z:eb.w)
     if (tag > -2) {  // a node (or the sentinel)
-        box_step<COUNT>(t, r, ea, eb, tag, cnt);
+        box_step<COUNT, MED3>(t, r, ea, eb, tag, cnt);
     } else {
         if (QUADS && tag == RTX_E_QUAD) quad_test<COUNT>(t, r, E, ea, eb, t.i, cnt);
         else sphere_test<COUNT>(t, r, ea, eb, t.i, cnt);
@@ -741,10 +774,12 @@ __device__ __forceinline__ void trav_step(Trav& t, const Ray& r, const SceneRef 
 // again next step.  Each lane still takes the reference's steps in the reference's order with
 // the current bound, so every result is unchanged; the wave no longer pays both paths in the
 // ~75 % of steps where a few lanes sit on primitives.
-// Returns (COUNT only) the lanes whose entry the step processed, wave-uniform.
-template <bool COUNT, bool QUADS, bool FIXED, bool HYB>
+// Returns (COUNT only) the lanes whose entry the step processed, wave-uniform; `idle` gets the
+// lanes parked on the sentinel (low 16 bits) and the lanes whose entry kind the step did not
+// run (high 16 bits).
+template <bool COUNT, bool QUADS, bool FIXED, bool HYB, bool MED3>
 __device__ __forceinline__ uint32_t trav_step_batched(Trav& t, const Ray& r, const SceneRef E, Counters& cnt,
-                                                      uint32_t end, uint32_t kmin) {
+                                                      uint32_t end, uint32_t kmin, uint32_t& idle) {
     float4 ea, eb;
     load_entry<FIXED, HYB>(E, t.i, ea, eb);
     const int32_t tag = __float_as_int(eb.w);
@@ -763,7 +798,11 @@ __device__ __forceinline__ uint32_t trav_step_batched(Trav& t, const Ray& r, con
         }
     } else if (__builtin_amdgcn_inverse_ballot_w64(bm)) {  // lanes on a node (the sentinel's step is a no-op)
         if (COUNT && HYB && t.i < E.hot) ++cnt.cache_hits;
-        box_step<COUNT>(t, r, ea, eb, tag, cnt);
+        box_step<COUNT, MED3>(t, r, ea, eb, tag, cnt);
+    }
+    if (COUNT) {
+        const uint32_t walking = (uint32_t)__popcll(pm | bm);
+        idle += (64u - walking) | ((uint32_t)__popcll(prims ? bm : pm) << 16);
     }
     return COUNT ? (uint32_t)__popcll(prims ? pm : bm) : 0u;
 }

@@ -52,25 +52,32 @@ __device__ __forceinline__ void flush_sched(const Params& p, uint64_t wi, uint64
 // STEPS > 1 takes up to STEPS entries per lane between two wave votes.  (A branch-free
 // step that evaluates the box and the sphere test on every lane measured 8 % slower:
 // most waves hold only box entries at a step, and the branch skips the sphere test.)
-template <bool COUNT, int STEPS = 1, bool QUADS = false, bool FIXED = false, bool HYB = false, bool BATCH = false>
-__device__ __forceinline__ void traverse_phase(uint32_t& mode, Trav& t, const Ray& r, const SceneRef E,
-                                               uint32_t n_entries, uint32_t thresh, Counters& cnt,
-                                               uint64_t& wave_iters, uint64_t& lane_steps, uint64_t& shade_phases,
-                                               uint64_t& shade_lanes, uint64_t& idle_lanes, uint32_t prim_batch = 0) {
+template <bool COUNT, int STEPS, bool QUADS, bool FIXED, bool HYB, bool BATCH, bool MED3>
+__device__ __forceinline__ void traverse_loop(uint32_t& mode, Trav& t, const Ray& r, const SceneRef E,
+                                              uint32_t n_entries, uint32_t thresh, Counters& cnt,
+                                              uint64_t& wave_iters, uint64_t& lane_steps, uint64_t& shade_phases,
+                                              uint64_t& shade_lanes, uint64_t& idle_lanes, uint64_t& parked,
+                                              uint64_t& deferred, uint32_t prim_batch) {
     for (;;) {
         // Every lane steps: one that is not traversing (or finishes early) waits on the
         // sentinel, t.i = 16 * n_entries, where a step changes nothing — cheaper than masking
         // the wave per step.
         uint32_t done = 0;  // COUNT: lane-steps that tested an entry (a lane on the sentinel idles)
+        uint32_t idle = 0;  // COUNT: parked (low 16 bits) and deferred (high 16 bits) lane-steps
         if constexpr (BATCH) {
 #pragma unroll
             for (int s = 0; s < STEPS; ++s)
-                done += trav_step_batched<COUNT, QUADS, FIXED, HYB>(t, r, E, cnt, 16 * n_entries, prim_batch);
+                done += trav_step_batched<COUNT, QUADS, FIXED, HYB, MED3>(t, r, E, cnt, 16 * n_entries, prim_batch,
+                                                                         idle);
         } else {
 #pragma unroll
             for (int s = 0; s < STEPS; ++s) {
-                if (COUNT) done += (uint32_t)__popcll(ballot(t.i < 16 * n_entries));
-                trav_step<COUNT, QUADS, FIXED, HYB>(t, r, E, cnt);
+                if (COUNT) {
+                    const uint32_t w = (uint32_t)__popcll(ballot(t.i < 16 * n_entries));
+                    done += w;
+                    idle += 64u - w;
+                }
+                trav_step<COUNT, QUADS, FIXED, HYB, MED3>(t, r, E, cnt);
             }
         }
         // votes on single compares, combined with SALU (a vote on a combined condition was
@@ -82,6 +89,8 @@ __device__ __forceinline__ void traverse_phase(uint32_t& mode, Trav& t, const Ra
         if (COUNT) {
             ++wave_iters;
             lane_steps += done;
+            parked += idle & 0xFFFFu;
+            deferred += idle >> 16;
             idle_lanes += (uint64_t)__popcll(ballot(mode == 3));
         }
         if (trav == 0 || (uint32_t)__popcll(pend) >= thresh) {
@@ -92,6 +101,26 @@ __device__ __forceinline__ void traverse_phase(uint32_t& mode, Trav& t, const Ra
             return;
         }
     }
+}
+
+// The traversal phase: the med3 box test (box_step) when every walking lane's ray has finite
+// 1/dir and origin — all but a handful of rays per frame —, else the select form for the whole
+// phase.  (A lane's ray is fixed for the phase; lanes parked on the sentinel do not matter: a
+// step there changes nothing either way.)
+template <bool COUNT, int STEPS = 1, bool QUADS = false, bool FIXED = false, bool HYB = false, bool BATCH = false>
+__device__ __forceinline__ void traverse_phase(uint32_t& mode, Trav& t, const Ray& r, const SceneRef E,
+                                               uint32_t n_entries, uint32_t thresh, Counters& cnt,
+                                               uint64_t& wave_iters, uint64_t& lane_steps, uint64_t& shade_phases,
+                                               uint64_t& shade_lanes, uint64_t& idle_lanes, uint64_t& parked,
+                                               uint64_t& deferred, uint32_t prim_batch = 0) {
+    if (ballot(!t.safe && t.i < 16 * n_entries) == 0)
+        traverse_loop<COUNT, STEPS, QUADS, FIXED, HYB, BATCH, true>(mode, t, r, E, n_entries, thresh, cnt, wave_iters,
+                                                                  lane_steps, shade_phases, shade_lanes, idle_lanes,
+                                                                  parked, deferred, prim_batch);
+    else
+        traverse_loop<COUNT, STEPS, QUADS, FIXED, HYB, BATCH, false>(mode, t, r, E, n_entries, thresh, cnt,
+                                                                   wave_iters, lane_steps, shade_phases, shade_lanes,
+                                                                   idle_lanes, parked, deferred, prim_batch);
 }
 
 enum : uint32_t { M_TRAV = 0, M_SHADE = 1, M_START = 2, M_DONE = 3, M_CLAIM = 4 };
@@ -170,7 +199,7 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
     t.i = 16 * p.n_entries;  // on the sentinel until its first ray
     Counters cnt{0, 0, 0, 0, 0, 0};
     uint64_t wave_iters = 0, lane_steps = 0, shade_phases = 0, shade_lanes = 0;
-    uint64_t trav_cycles = 0, shade_cycles = 0, clk = 0, idle_lanes = 0;  // COUNT only
+    uint64_t trav_cycles = 0, shade_cycles = 0, clk = 0, idle_lanes = 0, parked = 0, deferred = 0;  // COUNT only
 
     auto store = [&](V3 col) {  // the item's colour, GetColor's result for sample k
         float* o = p.scratch + ((size_t)(rng.sample - p.k0) * npix + pix) * 3;
@@ -195,7 +224,7 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
         // from HBM cost config 4 +34 %
         traverse_phase<COUNT, STEPS, QUADS, USE_LDS, HYB, USE_LDS>(mode, t, r, E, n_entries, thresh, cnt, wave_iters,
                                                               lane_steps, shade_phases, shade_lanes, idle_lanes,
-                                                              p.prim_batch);
+                                                              parked, deferred, p.prim_batch);
         if (COUNT) {
             const uint64_t now = __builtin_amdgcn_s_memtime();
             trav_cycles += now - clk;
@@ -287,6 +316,8 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
             atomicAdd(&p.counters[12], (unsigned long long)trav_cycles);
             atomicAdd(&p.counters[13], (unsigned long long)shade_cycles);
             atomicAdd(&p.counters[14], (unsigned long long)idle_lanes);
+            atomicAdd(&p.counters[16], (unsigned long long)(parked / STEPS));
+            atomicAdd(&p.counters[17], (unsigned long long)(deferred / STEPS));
         }
     }
 }
