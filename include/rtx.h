@@ -224,6 +224,8 @@ typedef struct rtx_stats {
                                 an item) per walk step, summed over steps / steps per vote   */
     uint64_t deferred_lanes; /* lanes whose entry kind (node / primitive) a batched walk step
                                 did not run, likewise                                        */
+    uint64_t shade_split_cycles[4]; /* shade_cycles split: scatter sampling, shading, item claims +
+                                       camera rays, segment starts (1/dir)                    */
 } rtx_stats;
 
 #define RTX_FLAG_COUNTERS 1u /* count work units (separate kernel instantiation) */

@@ -572,6 +572,7 @@ int collect_on(DeviceCopy* c, bool count, uint64_t samples, uint32_t chunks, rtx
     st->cache_hits = h[15];
     st->parked_lanes = h[16];
     st->deferred_lanes = h[17];
+    for (int q = 0; q < 4; ++q) st->shade_split_cycles[q] = h[18 + q];
     st->sample_chunks = chunks;
     st->kernel_ms = ms;
     return RTX_OK;
@@ -680,6 +681,7 @@ void add_stats(rtx_stats* acc, const rtx_stats& s) {
     acc->cache_hits += s.cache_hits;
     acc->parked_lanes += s.parked_lanes;
     acc->deferred_lanes += s.deferred_lanes;
+    for (int q = 0; q < 4; ++q) acc->shade_split_cycles[q] += s.shade_split_cycles[q];
     acc->sample_chunks = std::max(acc->sample_chunks, s.sample_chunks);
 }
 

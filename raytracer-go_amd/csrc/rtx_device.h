@@ -582,8 +582,9 @@ struct Trav {
     uint32_t i;  // walk position: the byte offset of the current entry's half, 16 * index
     int32_t hit;
     float closest, ix, iy, iz, a;
+    float ra;   // RN(1 / a): the sphere test's divisions as div_by (SAFE rays)
     bool nx, ny, nz;
-    bool safe;  // 1/dir and the origin are finite: box_step<.., MED3 = true> is exact for this ray
+    bool safe;  // 1/dir and the origin finite, a in [2^-60, 2^60]: the SAFE step forms are exact
 };
 
 __device__ __forceinline__ void trav_begin(Trav& t, const Ray& r) {
@@ -594,9 +595,11 @@ __device__ __forceinline__ void trav_begin(Trav& t, const Ray& r) {
     t.nx = t.ix < 0.0f;
     t.ny = t.iy < 0.0f;
     t.nz = t.iz < 0.0f;
-    t.safe = __builtin_isfinite(t.ix) && __builtin_isfinite(t.iy) && __builtin_isfinite(t.iz) &&
-             __builtin_isfinite(r.o.x) && __builtin_isfinite(r.o.y) && __builtin_isfinite(r.o.z);
     t.a = lensq(r.d);  // hittables.go:98, loop-invariant
+    t.ra = 1.0f / t.a;
+    t.safe = __builtin_isfinite(t.ix) && __builtin_isfinite(t.iy) && __builtin_isfinite(t.iz) &&
+             __builtin_isfinite(r.o.x) && __builtin_isfinite(r.o.y) && __builtin_isfinite(r.o.z) &&
+             t.a >= 0x1p-60f && t.a <= 0x1p60f;
     t.closest = __builtin_inff();
     t.hit = -1;
     t.i = 0;
@@ -659,8 +662,21 @@ __device__ __forceinline__ void quad_test(Trav& t, const Ray& r, const SceneRef 
     }
 }
 
+// n / a correctly rounded, given y = RN(1 / a) (Markstein: q0 = RN(n y) is within 1 ulp of n / a,
+// the residual e = n - a q0 is exact by fma, and RN(q0 + e y) = RN(n / a) when y is the
+// correctly rounded reciprocal), for a in [2^-60, 2^60] (Trav::safe): every quotient that can
+// pass `tmin < t < closest` is then a normal number and so exactly the division's.  Quotients
+// that overflow may come out NaN instead of inf, which fails the same tests.  3 VALU instead
+// of the 11 of a division (scripts/micro/fastdiv_check.hip checks it against v_div_* on the GPU).
+__device__ __forceinline__ float div_by(float n, float a, float y) {
+    const float q0 = n * y;
+    const float e = __builtin_fmaf(-a, q0, n);
+    return __builtin_fmaf(e, y, q0);
+}
+
 // (*Sphere).Hit, hittables.go:96-116, of the sphere entry (ea, eb) at `pos` against (tmin, closest).
-template <bool COUNT>
+// SAFE: the two divisions by a as div_by.
+template <bool COUNT, bool SAFE = false>
 __device__ __forceinline__ void sphere_test(Trav& t, const Ray& r, const float4 ea, const float4 eb, uint32_t pos,
                                             Counters& cnt) {
     const float tmin = 0.001f;  // ray.go:37
@@ -671,12 +687,12 @@ __device__ __forceinline__ void sphere_test(Trav& t, const Ray& r, const float4 
     const float disc = hb * hb - t.a * c;                                  // :102
     if (disc >= 0.0f) {                                                    // :104 (NaN: miss either way)
         const float sq = __builtin_sqrtf(disc);                            // :108
-        float tt = (-hb - sq) / t.a;                                       // :110
+        float tt = SAFE ? div_by(-hb - sq, t.a, t.ra) : (-hb - sq) / t.a;  // :110
         bool ok = tmin < tt && tt < t.closest;
         // The second root (:112) only when the first is not beyond tmin (or NaN): a
         // first root at or past closest makes the second, (-hb + sq) / a >= it, fail too.
         if (!(tmin < tt)) {
-            tt = (-hb + sq) / t.a;                                         // :112
+            tt = SAFE ? div_by(-hb + sq, t.a, t.ra) : (-hb + sq) / t.a;    // :112
             ok = tmin < tt && tt < t.closest;
         }
         if (ok) {
@@ -762,7 +778,7 @@ __device__ __forceinline__ void trav_step(Trav& t, const Ray& r, const SceneRef 
         box_step<COUNT, MED3>(t, r, ea, eb, tag, cnt);
     } else {
         if (QUADS && tag == RTX_E_QUAD) quad_test<COUNT>(t, r, E, ea, eb, t.i, cnt);
-        else sphere_test<COUNT>(t, r, ea, eb, t.i, cnt);
+        else sphere_test<COUNT, MED3>(t, r, ea, eb, t.i, cnt);
         t.i = (uint32_t)__float_as_int(eb.z);  // the primitive's successor
     }
 }
@@ -793,7 +809,7 @@ __device__ __forceinline__ uint32_t trav_step_batched(Trav& t, const Ray& r, con
         if (__builtin_amdgcn_inverse_ballot_w64(pm)) {  // = prim, as the vote's mask (no second compare)
             if (COUNT && HYB && t.i < E.hot) ++cnt.cache_hits;
             if (QUADS && tag == RTX_E_QUAD) quad_test<COUNT>(t, r, E, ea, eb, t.i, cnt);
-            else sphere_test<COUNT>(t, r, ea, eb, t.i, cnt);
+            else sphere_test<COUNT, MED3>(t, r, ea, eb, t.i, cnt);
             t.i = (uint32_t)__float_as_int(eb.z);
         }
     } else if (__builtin_amdgcn_inverse_ballot_w64(bm)) {  // lanes on a node (the sentinel's step is a no-op)

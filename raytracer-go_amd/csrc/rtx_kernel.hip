@@ -125,6 +125,13 @@ __device__ __forceinline__ void traverse_phase(uint32_t& mode, Trav& t, const Ra
 
 enum : uint32_t { M_TRAV = 0, M_SHADE = 1, M_START = 2, M_DONE = 3, M_CLAIM = 4 };
 
+// COUNT: add the shader cycles since `clk` to `acc` and restart the clock.
+__device__ __forceinline__ void split_clk(uint64_t& acc, uint64_t& clk) {
+    const uint64_t now = __builtin_amdgcn_s_memtime();
+    acc += now - clk;
+    clk = now;
+}
+
 // ------------------------------------------------------------------------------------
 // v3: persistent waves over (pixel, sample) items; the sum is formed afterwards.
 //
@@ -200,6 +207,7 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
     Counters cnt{0, 0, 0, 0, 0, 0};
     uint64_t wave_iters = 0, lane_steps = 0, shade_phases = 0, shade_lanes = 0;
     uint64_t trav_cycles = 0, shade_cycles = 0, clk = 0, idle_lanes = 0, parked = 0, deferred = 0;  // COUNT only
+    uint64_t split[4] = {0, 0, 0, 0};  // COUNT: shading-phase cycles: scatter, shade, claims + camera rays, trav_begin
 
     auto store = [&](V3 col) {  // the item's colour, GetColor's result for sample k
         float* o = p.scratch + ((size_t)(rng.sample - p.k0) * npix + pix) * 3;
@@ -234,6 +242,7 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
 
         // ---- shading phase ----------------------------------------------------------
         const Scatter sc = coop_scatter<QUADS>(p, E, rng, seg + 1, mode == M_SHADE ? t.hit : -1);
+        if (COUNT) split_clk(split[0], clk);
         bool ready = false;
         if (mode == M_SHADE) {
             V3 color;
@@ -250,6 +259,7 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
                 ready = true;
             }
         }
+        if (COUNT) split_clk(split[1], clk);
         // Lanes without an item take the next ones of the wave's unit; new camera rays
         // at one program point.  Loops only for max depth 0 and ragged tiles.
         for (;;) {
@@ -302,20 +312,25 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
                 }
             }
         }
+        if (COUNT) split_clk(split[2], clk);
         if (ready) {  // begin a segment: world.Hit (ray.go:36)
             if (COUNT) ++cnt.segments;
             trav_begin(t, r);
             mode = n_entries > 0 ? M_TRAV : M_SHADE;
         }
-        if (COUNT) shade_cycles += __builtin_amdgcn_s_memtime() - clk;
+        if (COUNT) split_clk(split[3], clk);
     }
     if (COUNT) {
         flush_counters(p, items_done, cnt);
         if (lane == 0) {
             flush_sched(p, wave_iters, lane_steps / STEPS, shade_phases, shade_lanes);
             atomicAdd(&p.counters[12], (unsigned long long)trav_cycles);
-            atomicAdd(&p.counters[13], (unsigned long long)shade_cycles);
             atomicAdd(&p.counters[14], (unsigned long long)idle_lanes);
+            for (int q = 0; q < 4; ++q) {
+                shade_cycles += split[q];
+                atomicAdd(&p.counters[18 + q], (unsigned long long)split[q]);
+            }
+            atomicAdd(&p.counters[13], (unsigned long long)shade_cycles);
             atomicAdd(&p.counters[16], (unsigned long long)(parked / STEPS));
             atomicAdd(&p.counters[17], (unsigned long long)(deferred / STEPS));
         }

@@ -92,10 +92,11 @@ class Stats(ctypes.Structure):
                 ("wave_iters", c_uint64), ("lane_steps", c_uint64), ("shade_phases", c_uint64),
                 ("shade_lanes", c_uint64), ("trav_cycles", c_uint64), ("shade_cycles", c_uint64),
                 ("idle_lanes", c_uint64), ("cache_hits", c_uint64), ("sample_chunks", c_uint64),
-                ("parked_lanes", c_uint64), ("deferred_lanes", c_uint64)]
+                ("parked_lanes", c_uint64), ("deferred_lanes", c_uint64), ("shade_split_cycles", c_uint64 * 4)]
 
     def as_dict(self) -> dict:
-        return {name: getattr(self, name) for name, _ in self._fields_}
+        return {name: (list(v) if not isinstance(v := getattr(self, name), (int, float)) else v)
+                for name, _ in self._fields_}
 
 
 RTX_SYMBOLS = [

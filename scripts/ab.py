@@ -84,5 +84,7 @@ for n in names:
               f"{c.shade_phases / c.wave_iters:.3f}  shade share {c.shade_cycles / max(c.trav_cycles + c.shade_cycles, 1):.3f}"
               f"  cyc/iter {c.trav_cycles / c.wave_iters:.0f}  cyc/shade {c.shade_cycles / max(c.shade_phases, 1):.0f}"
               f"  idle-lane frac {c.idle_lanes / (64 * c.wave_iters):.3f}"
-              f"  parked {c.parked_lanes / (64 * c.wave_iters):.3f}  deferred {c.deferred_lanes / (64 * c.wave_iters):.3f}",
+              f"  parked {c.parked_lanes / (64 * c.wave_iters):.3f}  deferred {c.deferred_lanes / (64 * c.wave_iters):.3f}"
+              f"  shade split (scatter/shade/claim/begin) "
+              + "/".join(f"{x / max(c.shade_cycles, 1):.3f}" for x in c.shade_split_cycles),
               flush=True)
