@@ -169,6 +169,9 @@ def schedule(st: dict) -> dict:
         out["deferred_lane_frac"] = round(st.get("deferred_lanes", 0) / it, 4)  # other entry kind
         cyc = st["trav_cycles"] + st["shade_cycles"]
         out["shade_cycle_share"] = round(st["shade_cycles"] / cyc, 4) if cyc else None
+        sp = st.get("shade_split_cycles")
+        if cyc and sp:  # shares of all wave cycles: scatter sampling, shading, claims + camera rays, trav_begin
+            out["shade_split"] = {k: round(v / cyc, 4) for k, v in zip(("scatter", "shade", "claim_camera", "begin"), sp)}
     reads = st.get("node_visits", 0) + st.get("prim_tests", 0)
     if st.get("cache_hits") and reads:
         out["lds_cache_hit_frac"] = round(st["cache_hits"] / reads, 4)

@@ -21,6 +21,10 @@
 #include "rtx_device.h"
 #include "rtx_kernel.h"
 
+#ifndef RTX_ASM_STEP  // 1: the timed kernel's walk step in assembly (trav_step_asm); 0 for A/B
+#define RTX_ASM_STEP 1
+#endif
+
 namespace rtxd {
 
 __device__ __forceinline__ void flush_counters(const Params& p, uint64_t samples, const Counters& cnt) {
@@ -66,9 +70,13 @@ __device__ __forceinline__ void traverse_loop(uint32_t& mode, Trav& t, const Ray
         uint32_t idle = 0;  // COUNT: parked (low 16 bits) and deferred (high 16 bits) lane-steps
         if constexpr (BATCH) {
 #pragma unroll
-            for (int s = 0; s < STEPS; ++s)
-                done += trav_step_batched<COUNT, QUADS, FIXED, HYB, MED3>(t, r, E, cnt, 16 * n_entries, prim_batch,
-                                                                         idle);
+            for (int s = 0; s < STEPS; ++s) {
+                if constexpr (RTX_ASM_STEP && !COUNT && !QUADS && FIXED && !HYB && MED3)
+                    trav_step_asm(t, r, 16 * n_entries, prim_batch, 0.001f, 0x260u);  // +-0, +inf classes
+                else
+                    done += trav_step_batched<COUNT, QUADS, FIXED, HYB, MED3>(t, r, E, cnt, 16 * n_entries,
+                                                                             prim_batch, idle);
+            }
         } else {
 #pragma unroll
             for (int s = 0; s < STEPS; ++s) {
