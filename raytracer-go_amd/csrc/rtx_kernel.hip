@@ -21,6 +21,9 @@
 #include "rtx_device.h"
 #include "rtx_kernel.h"
 
+#ifndef RTX_WALK_STEPS  // walk steps per lane between two wave votes
+#define RTX_WALK_STEPS 6
+#endif
 #ifndef RTX_ASM_STEP  // 1: the timed kernel's walk step in assembly (trav_step_asm); 0 for A/B
 #define RTX_ASM_STEP 1
 #endif
@@ -62,6 +65,11 @@ __device__ __forceinline__ void traverse_loop(uint32_t& mode, Trav& t, const Ray
                                               uint64_t& wave_iters, uint64_t& lane_steps, uint64_t& shade_phases,
                                               uint64_t& shade_lanes, uint64_t& idle_lanes, uint64_t& parked,
                                               uint64_t& deferred, uint32_t prim_batch) {
+    // The lane modes are fixed during the phase except walking -> waiting (mode 0 -> 1) on
+    // reaching the sentinel, so the votes are SALU on masks taken once: walking lanes W, waiting
+    // lanes P0, lanes without an item D; per iteration only `at_end` is voted.
+    const uint64_t W = ballot(mode == 0), P0 = ballot(mode - 1u < 2u);
+    const uint64_t D = COUNT ? ballot(mode == 3) : 0ull;
     for (;;) {
         // Every lane steps: one that is not traversing (or finishes early) waits on the
         // sentinel, t.i = 16 * n_entries, where a step changes nothing — cheaper than masking
@@ -88,24 +96,22 @@ __device__ __forceinline__ void traverse_loop(uint32_t& mode, Trav& t, const Ray
                 trav_step<COUNT, QUADS, FIXED, HYB, MED3>(t, r, E, cnt);
             }
         }
-        // votes on single compares, combined with SALU (a vote on a combined condition was
-        // materialised with two extra VALU)
-        const uint64_t walking = ballot(mode == 0), at_end = ballot(t.i >= 16 * n_entries);
-        if (mode == 0 && t.i >= 16 * n_entries) mode = 1;
-        const uint64_t trav = walking & ~at_end;
-        const uint64_t pend = ballot(mode - 1u < 2u);  // mode 1 or 2
+        const uint64_t at_end = ballot(t.i >= 16 * n_entries);
+        const uint64_t trav = W & ~at_end;
+        const uint64_t pend = P0 | (W & at_end);  // mode 1 or 2 after this iteration
         if (COUNT) {
             ++wave_iters;
             lane_steps += done;
             parked += idle & 0xFFFFu;
             deferred += idle >> 16;
-            idle_lanes += (uint64_t)__popcll(ballot(mode == 3));
+            idle_lanes += (uint64_t)__popcll(D);
         }
         if (trav == 0 || (uint32_t)__popcll(pend) >= thresh) {
             if (COUNT) {
                 ++shade_phases;
                 shade_lanes += (uint64_t)__popcll(pend);
             }
+            if (__builtin_amdgcn_inverse_ballot_w64(W & at_end)) mode = 1;  // walked to the end
             return;
         }
     }
@@ -158,7 +164,8 @@ __device__ __forceinline__ void split_clk(uint64_t& acc, uint64_t& clk) {
 // ------------------------------------------------------------------------------------
 template <bool COUNT, bool USE_LDS, bool QUADS, bool NOISE, int WAVES = 8, int MINW = 0, bool HYB = false>
 __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
-    constexpr uint32_t WAVE_BLOCK = 64 * WAVES, STEPS = 6;  // walk steps between two wave votes (A/B with primitive batching: 4 +0.7 %, 8 +0.8 %, 12 +1.3 %)
+    // walk steps between two wave votes (A/B with primitive batching: 4 +0.7 %, 8 +0.8 %, 12 +1.3 %)
+    constexpr uint32_t WAVE_BLOCK = 64 * WAVES, STEPS = RTX_WALK_STEPS;
     extern __shared__ float4 lds_entries[];
     SceneRef E;
     if constexpr (USE_LDS) {
