@@ -823,145 +823,163 @@ __device__ __forceinline__ uint32_t trav_step_batched(Trav& t, const Ray& r, con
     return COUNT ? (uint32_t)__popcll(prims ? pm : bm) : 0u;
 }
 
-// trav_step_batched<false, false, true, false, true> — the timed kernel's walk step for a
-// sphere scene in LDS whose walking lanes all have t.safe rays — written out in GCN assembly.
-// Same decisions, same IEEE operations in the same order, same results (tests/test_gpu_parity.py
-// compares it with the counting kernel, which keeps the C++ step, and with the oracle).  What
-// the compiler could not be talked out of: the uniform choice box/primitive went through
-// s_cselect + s_and vcc, exec + vccz branches, the box test through saveexec + execz + exec
-// restore + phi copies of the position, and the sphere test through three nested divergent
-// ifs: 45 issued instructions per box step, 34 here; the sphere test runs branch-free on the
-// primitive lanes (both roots, then one select).
+// trav_step_batched<false, false, true, false, true> x 6 — the timed kernel's walk between two
+// wave votes, for a sphere scene in LDS whose walking lanes all have t.safe rays — written out in
+// GCN assembly.  Same decisions, same IEEE operations in the same order, same results
+// (tests/test_gpu_parity.py compares it with the counting kernel, which keeps the C++ step, and
+// with the oracle).  What the compiler could not be talked out of: the uniform choice box /
+// primitive went through s_cselect + s_and vcc, exec + vccz branches, the box test through
+// saveexec + execz + exec restore + phi copies of the position, and the sphere test through
+// three nested divergent ifs: 45 issued instructions per box step, 31 here; the sphere test runs
+// branch-free on the primitive lanes (both roots, then one select).  One asm statement for all
+// six steps: the compiler puts an s_nop at every asm boundary, and a read into a register tuple
+// cannot hand its components to another asm statement without copies, so the entry lives in the
+// clobbered v0-v7 (halves a, b) with v8-v9 as scratch.
 //   - kind: primitive = tag < -1; walking = pos < end; node lanes = walking & ~primitive
 //   - the primitive tests run when >= kmin lanes wait on one or no node lane is left
 //   - box (MED3, box_step): per axis (min - o) * inv, (max - o) * inv; lo/hi clamped by v_med3
 //   - sphere (sphere_test<false, true>): hb, c, disc as hittables.go:97-102; sqrt correctly
-//     rounded (the compiler's own f32 sqrt expansion: 2^32 scaling below 2^-96, v_sqrt, the
-//     two neighbour residuals by fma, +-0 / +inf passed through); both roots by div_by; the
-//     first root when tmin < t1, else the second (hittables.go:110-114); disc >= 0 required.
+//     rounded as the compiler expands an f32 sqrt — v_sqrt, then the neighbour whose fma
+//     residual changes sign; inputs below 2^-96 scaled by 2^32 first and the root by 2^-16
+//     after, a path taken only when some lane has 0 <= disc < 2^-96.  (The expansion's last
+//     step, passing +-0 and +inf through, is left out: v_sqrt returns them exactly and both
+//     neighbour residuals are then NaN or a zero, which keeps them.)  Both roots by div_by;
+//     the first root when tmin < t1, else the second (hittables.go:110-114); disc >= 0.
 // gfx950 hazards: a VALU-written SGPR/VCC read as a v_cndmask mask by the next VALU needs
 // s_nop 1; a v_sqrt result read by the next VALU needs s_nop 0 (as the compiler emits them).
-__device__ __forceinline__ void trav_step_asm(Trav& t, const Ray& r, uint32_t end, uint32_t kmin, float tmin,
-                                              uint32_t class_mask) {
-    float4 ea, eb;
-    asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %2 offset:%3\n\ts_waitcnt lgkmcnt(0)"
-                 : "=&v"(ea), "=&v"(eb)
-                 : "v"(t.i), "i"(LDS_B));
-    float ax = ea.x, ay = ea.y, az = ea.z, aw = ea.w, bx = eb.x, by = eb.y, bz = eb.z, bw = eb.w;
-    float u0, u1;
+#define RTX_WALK_STEP_ASM(K)                                                 \
+        "ds_read_b128 v[0:3], %[pos]\n\t"                                    \
+        "ds_read_b128 v[4:7], %[pos] offset:32768\n\t" /* LDS_B */          \
+        "s_waitcnt lgkmcnt(0)\n\t"                                           \
+        "v_cmp_gt_i32_e64 %[pm], -1, v7\n\t"                                 \
+        "v_cmp_lt_u32_e64 %[wm], %[pos], %[end]\n\t"                         \
+        "s_andn2_b64 %[wm], %[wm], %[pm]\n\t"                                \
+        "s_bcnt1_i32_b64 %[cnt], %[pm]\n\t"                                  \
+        "s_cmp_ge_u32 %[cnt], %[kmin]\n\t"                                   \
+        "s_cbranch_scc1 LP%=_" #K "\n\t"                                     \
+        "s_cmp_eq_u64 %[wm], 0\n\t"                                          \
+        "s_cbranch_scc1 LP%=_" #K "\n\t"                                     \
+        /* ---- box tests on the node lanes */                               \
+        "s_and_saveexec_b64 %[save], %[wm]\n\t"                              \
+        "v_sub_f32 v0, v0, %[ox]\n\t"                                        \
+        "v_sub_f32 v4, v4, %[ox]\n\t"                                        \
+        "v_sub_f32 v1, v1, %[oy]\n\t"                                        \
+        "v_sub_f32 v5, v5, %[oy]\n\t"                                        \
+        "v_mul_f32 v0, v0, %[ix]\n\t"                                        \
+        "v_mul_f32 v4, v4, %[ix]\n\t"                                        \
+        "v_sub_f32 v2, v2, %[oz]\n\t"                                        \
+        "v_sub_f32 v6, v6, %[oz]\n\t"                                        \
+        "v_mul_f32 v1, v1, %[iy]\n\t"                                        \
+        "v_mul_f32 v5, v5, %[iy]\n\t"                                        \
+        "v_med3_f32 v8, %[tmin], v0, v4\n\t"                                 \
+        "v_med3_f32 v9, %[cl], v0, v4\n\t"                                   \
+        "v_mul_f32 v2, v2, %[iz]\n\t"                                        \
+        "v_mul_f32 v6, v6, %[iz]\n\t"                                        \
+        "v_med3_f32 v8, v8, v1, v5\n\t"                                      \
+        "v_med3_f32 v9, v9, v1, v5\n\t"                                      \
+        "v_med3_f32 v8, v8, v2, v6\n\t"                                      \
+        "v_med3_f32 v9, v9, v2, v6\n\t"                                      \
+        "v_cmp_lt_f32_e32 vcc, v8, v9\n\t"                                   \
+        "s_nop 1\n\t"                                                        \
+        "v_cndmask_b32_e32 %[pos], v3, v7, vcc\n\t"                          \
+        "s_mov_b64 exec, %[save]\n\t"                                        \
+        "s_branch LE%=_" #K "\n"                                             \
+        /* ---- sphere tests on the primitive lanes */                       \
+        "LP%=_" #K ":\n\t"                                                   \
+        "s_and_saveexec_b64 %[save], %[pm]\n\t"                              \
+        "s_cbranch_execz LR%=_" #K "\n\t"                                    \
+        "v_sub_f32 v0, %[ox], v0\n\t" /* oc = o - center */                  \
+        "v_sub_f32 v1, %[oy], v1\n\t"                                        \
+        "v_sub_f32 v2, %[oz], v2\n\t"                                        \
+        "v_mul_f32 v8, %[dx], v0\n\t" /* hb = d.oc */                        \
+        "v_mul_f32 v9, %[dy], v1\n\t"                                        \
+        "v_add_f32 v8, v8, v9\n\t"                                           \
+        "v_mul_f32 v9, %[dz], v2\n\t"                                        \
+        "v_add_f32 v8, v8, v9\n\t"                                           \
+        "v_mul_f32 v0, v0, v0\n\t" /* c = |oc|^2 - r^2 */                    \
+        "v_mul_f32 v1, v1, v1\n\t"                                           \
+        "v_add_f32 v0, v0, v1\n\t"                                           \
+        "v_mul_f32 v2, v2, v2\n\t"                                           \
+        "v_add_f32 v0, v0, v2\n\t"                                           \
+        "v_sub_f32 v0, v0, v4\n\t"                                           \
+        "v_mul_f32 v0, %[a], v0\n\t" /* disc = hb*hb - a*c */                \
+        "v_mul_f32 v9, v8, v8\n\t"                                           \
+        "v_sub_f32 v0, v9, v0\n\t"                                           \
+        "v_cmp_le_f32_e64 %[dok], 0, v0\n\t"                                 \
+        "v_cmp_gt_f32_e32 vcc, 0xf800000, v0\n\t" /* x < 2^-96 */            \
+        "s_and_b64 %[g1], vcc, %[dok]\n\t"                                   \
+        "s_cbranch_scc1 LS%=_" #K "\n\t"                                     \
+        "v_sqrt_f32_e32 v2, v0\n\t" /* every lane: x >= 2^-96 or x < 0 */    \
+        "s_nop 0\n\t"                                                        \
+        "v_add_u32_e32 v9, -1, v2\n\t"                                       \
+        "v_add_u32_e32 v3, 1, v2\n\t"                                        \
+        "v_fma_f32 v5, -v9, v2, v0\n\t"                                      \
+        "v_fma_f32 v7, -v3, v2, v0\n\t"                                      \
+        "v_cmp_ge_f32_e64 %[g1], 0, v5\n\t"                                  \
+        "s_nop 1\n\t"                                                        \
+        "v_cndmask_b32_e64 v2, v2, v9, %[g1]\n\t"                            \
+        "v_cmp_lt_f32_e64 %[g1], 0, v7\n\t"                                  \
+        "s_nop 1\n\t"                                                        \
+        "v_cndmask_b32_e64 v2, v2, v3, %[g1]\n\t"                            \
+        "s_branch LQ%=_" #K "\n"                                             \
+        "LS%=_" #K ":\n\t" /* some lane: 0 <= x < 2^-96, scaled by 2^32 */   \
+        "v_mul_f32 v1, 0x4f800000, v0\n\t"                                   \
+        "v_cndmask_b32_e32 v1, v0, v1, vcc\n\t"                              \
+        "v_sqrt_f32_e32 v2, v1\n\t"                                          \
+        "s_nop 0\n\t"                                                        \
+        "v_add_u32_e32 v9, -1, v2\n\t"                                       \
+        "v_add_u32_e32 v3, 1, v2\n\t"                                        \
+        "v_fma_f32 v5, -v9, v2, v1\n\t"                                      \
+        "v_fma_f32 v7, -v3, v2, v1\n\t"                                      \
+        "v_cmp_ge_f32_e64 %[g1], 0, v5\n\t"                                  \
+        "s_nop 1\n\t"                                                        \
+        "v_cndmask_b32_e64 v2, v2, v9, %[g1]\n\t"                            \
+        "v_cmp_lt_f32_e64 %[g1], 0, v7\n\t"                                  \
+        "s_nop 1\n\t"                                                        \
+        "v_cndmask_b32_e64 v2, v2, v3, %[g1]\n\t"                            \
+        "v_mul_f32 v9, 0x37800000, v2\n\t" /* x 2^-16 when scaled */         \
+        "v_cndmask_b32_e32 v2, v2, v9, vcc\n"                                \
+        "LQ%=_" #K ":\n\t" /* v2 = sqrt(disc) */                             \
+        "v_sub_f32_e64 v1, -v8, v2\n\t" /* -hb - sq */                       \
+        "v_add_f32_e64 v3, -v8, v2\n\t" /* -hb + sq */                       \
+        "v_mul_f32 v5, v1, %[ra]\n\t"   /* div_by: q0 = n y */               \
+        "v_mul_f32 v7, v3, %[ra]\n\t"                                        \
+        "v_fma_f32 v1, -%[a], v5, v1\n\t" /* e = n - a q0 */                 \
+        "v_fma_f32 v3, -%[a], v7, v3\n\t"                                    \
+        "v_fmac_f32 v5, v1, %[ra]\n\t" /* t1 = q0 + e y */                   \
+        "v_fmac_f32 v7, v3, %[ra]\n\t" /* t2 */                              \
+        "v_cmp_lt_f32_e64 %[g1], %[tmin], v5\n\t"                            \
+        "v_cmp_lt_f32_e64 %[l1], v5, %[cl]\n\t"                              \
+        "v_cmp_lt_f32_e64 %[l2], %[tmin], v7\n\t"                            \
+        "s_and_b64 %[l1], %[l1], %[g1]\n\t"                                  \
+        "s_andn2_b64 %[l2], %[l2], %[g1]\n\t"                                \
+        "v_cmp_lt_f32_e64 %[wm], v7, %[cl]\n\t"                              \
+        "s_and_b64 %[l2], %[l2], %[wm]\n\t"                                  \
+        "s_or_b64 %[l1], %[l1], %[l2]\n\t"                                   \
+        "s_and_b64 %[l1], %[l1], %[dok]\n\t"                                 \
+        "v_cndmask_b32_e64 v7, v7, v5, %[g1]\n\t"                            \
+        "v_lshrrev_b32_e32 v1, 4, %[pos]\n\t"                                \
+        "v_cndmask_b32_e64 %[cl], %[cl], v7, %[l1]\n\t"                      \
+        "v_cndmask_b32_e64 %[hit], %[hit], v1, %[l1]\n\t"                    \
+        "v_mov_b32_e32 %[pos], v6\n"                                         \
+        "LR%=_" #K ":\n\t"                                                   \
+        "s_mov_b64 exec, %[save]\n"                                          \
+        "LE%=_" #K ":\n\t"
+__device__ __forceinline__ void walk6_asm(Trav& t, const Ray& r, uint32_t end, uint32_t kmin, float tmin) {
+    static_assert(LDS_B == 32768, "the asm reads the 'b' halves at offset:32768");
     uint64_t pm, wm, save, g1, l1, l2, dok;
     uint32_t cnt;
-    asm volatile(
-        "v_cmp_gt_i32_e64 %[pm], -1, %[bw]\n\t"
-        "v_cmp_lt_u32_e64 %[wm], %[pos], %[end]\n\t"
-        "s_andn2_b64 %[wm], %[wm], %[pm]\n\t"
-        "s_bcnt1_i32_b64 %[cnt], %[pm]\n\t"
-        "s_cmp_ge_u32 %[cnt], %[kmin]\n\t"
-        "s_cbranch_scc1 LP%=\n\t"
-        "s_cmp_eq_u64 %[wm], 0\n\t"
-        "s_cbranch_scc1 LP%=\n\t"
-        // ---- box tests on the node lanes
-        "s_and_saveexec_b64 %[save], %[wm]\n\t"
-        "v_sub_f32 %[ax], %[ax], %[ox]\n\t"
-        "v_sub_f32 %[bx], %[bx], %[ox]\n\t"
-        "v_sub_f32 %[ay], %[ay], %[oy]\n\t"
-        "v_sub_f32 %[by], %[by], %[oy]\n\t"
-        "v_mul_f32 %[ax], %[ax], %[ix]\n\t"
-        "v_mul_f32 %[bx], %[bx], %[ix]\n\t"
-        "v_sub_f32 %[az], %[az], %[oz]\n\t"
-        "v_sub_f32 %[bz], %[bz], %[oz]\n\t"
-        "v_mul_f32 %[ay], %[ay], %[iy]\n\t"
-        "v_mul_f32 %[by], %[by], %[iy]\n\t"
-        "v_med3_f32 %[u0], %[tmin], %[ax], %[bx]\n\t"
-        "v_med3_f32 %[u1], %[cl], %[ax], %[bx]\n\t"
-        "v_mul_f32 %[az], %[az], %[iz]\n\t"
-        "v_mul_f32 %[bz], %[bz], %[iz]\n\t"
-        "v_med3_f32 %[u0], %[u0], %[ay], %[by]\n\t"
-        "v_med3_f32 %[u1], %[u1], %[ay], %[by]\n\t"
-        "v_med3_f32 %[u0], %[u0], %[az], %[bz]\n\t"
-        "v_med3_f32 %[u1], %[u1], %[az], %[bz]\n\t"
-        "v_cmp_lt_f32_e32 vcc, %[u0], %[u1]\n\t"
-        "s_nop 1\n\t"
-        "v_cndmask_b32_e32 %[pos], %[aw], %[bw], vcc\n\t"
-        "s_mov_b64 exec, %[save]\n\t"
-        "s_branch LE%=\n"
-        // ---- sphere tests on the primitive lanes
-        "LP%=:\n\t"
-        "s_and_saveexec_b64 %[save], %[pm]\n\t"
-        "s_cbranch_execz LR%=\n\t"
-        "v_sub_f32 %[ax], %[ox], %[ax]\n\t"          // oc = o - center
-        "v_sub_f32 %[ay], %[oy], %[ay]\n\t"
-        "v_sub_f32 %[az], %[oz], %[az]\n\t"
-        "v_mul_f32 %[u0], %[dx], %[ax]\n\t"          // hb = d.oc
-        "v_mul_f32 %[u1], %[dy], %[ay]\n\t"
-        "v_add_f32 %[u0], %[u0], %[u1]\n\t"
-        "v_mul_f32 %[u1], %[dz], %[az]\n\t"
-        "v_add_f32 %[u0], %[u0], %[u1]\n\t"
-        "v_mul_f32 %[ax], %[ax], %[ax]\n\t"          // c = |oc|^2 - r^2
-        "v_mul_f32 %[ay], %[ay], %[ay]\n\t"
-        "v_add_f32 %[ax], %[ax], %[ay]\n\t"
-        "v_mul_f32 %[az], %[az], %[az]\n\t"
-        "v_add_f32 %[ax], %[ax], %[az]\n\t"
-        "v_sub_f32 %[ax], %[ax], %[bx]\n\t"
-        "v_mul_f32 %[ax], %[a], %[ax]\n\t"           // disc = hb*hb - a*c
-        "v_mul_f32 %[u1], %[u0], %[u0]\n\t"
-        "v_sub_f32 %[ax], %[u1], %[ax]\n\t"
-        "v_cmp_le_f32_e64 %[dok], 0, %[ax]\n\t"
-        "v_mul_f32 %[ay], 0x4f800000, %[ax]\n\t"     // sqrt: x < 2^-96 -> x * 2^32
-        "v_cmp_gt_f32_e32 vcc, 0xf800000, %[ax]\n\t"
-        "s_nop 1\n\t"
-        "v_cndmask_b32_e32 %[ay], %[ax], %[ay], vcc\n\t"
-        "v_sqrt_f32_e32 %[az], %[ay]\n\t"
-        "s_nop 0\n\t"
-        "v_add_u32_e32 %[u1], -1, %[az]\n\t"
-        "v_add_u32_e32 %[aw], 1, %[az]\n\t"
-        "v_fma_f32 %[by], -%[u1], %[az], %[ay]\n\t"
-        "v_fma_f32 %[bw], -%[aw], %[az], %[ay]\n\t"
-        "v_cmp_ge_f32_e64 %[g1], 0, %[by]\n\t"
-        "s_nop 1\n\t"
-        "v_cndmask_b32_e64 %[az], %[az], %[u1], %[g1]\n\t"
-        "v_cmp_lt_f32_e64 %[g1], 0, %[bw]\n\t"
-        "s_nop 1\n\t"
-        "v_cndmask_b32_e64 %[az], %[az], %[aw], %[g1]\n\t"
-        "v_mul_f32 %[u1], 0x37800000, %[az]\n\t"     // x 2^-16 when scaled
-        "v_cndmask_b32_e32 %[az], %[az], %[u1], vcc\n\t"
-        "v_cmp_class_f32_e64 %[g1], %[ay], %[cmask]\n\t"
-        "s_nop 1\n\t"
-        "v_cndmask_b32_e64 %[az], %[az], %[ay], %[g1]\n\t"  // sq
-        "v_sub_f32_e64 %[ay], -%[u0], %[az]\n\t"     // -hb - sq
-        "v_add_f32_e64 %[aw], -%[u0], %[az]\n\t"     // -hb + sq
-        "v_mul_f32 %[by], %[ay], %[ra]\n\t"          // div_by: q0 = n y
-        "v_mul_f32 %[bw], %[aw], %[ra]\n\t"
-        "v_fma_f32 %[ay], -%[a], %[by], %[ay]\n\t"   // e = n - a q0
-        "v_fma_f32 %[aw], -%[a], %[bw], %[aw]\n\t"
-        "v_fmac_f32 %[by], %[ay], %[ra]\n\t"         // t1 = q0 + e y
-        "v_fmac_f32 %[bw], %[aw], %[ra]\n\t"         // t2
-        "v_cmp_lt_f32_e64 %[g1], %[tmin], %[by]\n\t"
-        "v_cmp_lt_f32_e64 %[l1], %[by], %[cl]\n\t"
-        "v_cmp_lt_f32_e64 %[l2], %[tmin], %[bw]\n\t"
-        "s_and_b64 %[l1], %[l1], %[g1]\n\t"
-        "s_andn2_b64 %[l2], %[l2], %[g1]\n\t"
-        "v_cmp_lt_f32_e64 %[wm], %[bw], %[cl]\n\t"
-        "s_and_b64 %[l2], %[l2], %[wm]\n\t"
-        "s_or_b64 %[l1], %[l1], %[l2]\n\t"
-        "s_and_b64 %[l1], %[l1], %[dok]\n\t"
-        "v_cndmask_b32_e64 %[bw], %[bw], %[by], %[g1]\n\t"
-        "v_lshrrev_b32_e32 %[ay], 4, %[pos]\n\t"
-        "v_cndmask_b32_e64 %[cl], %[cl], %[bw], %[l1]\n\t"
-        "v_cndmask_b32_e64 %[hit], %[hit], %[ay], %[l1]\n\t"
-        "v_mov_b32_e32 %[pos], %[bz]\n"
-        "LR%=:\n\t"
-        "s_mov_b64 exec, %[save]\n"
-        "LE%=:"
-        : [pos] "+v"(t.i), [cl] "+v"(t.closest), [hit] "+v"(t.hit), [ax] "+v"(ax), [ay] "+v"(ay), [az] "+v"(az),
-          [aw] "+v"(aw), [bx] "+v"(bx), [by] "+v"(by), [bz] "+v"(bz), [bw] "+v"(bw), [u0] "=&v"(u0),
-          [u1] "=&v"(u1), [pm] "=&s"(pm), [wm] "=&s"(wm), [save] "=&s"(save), [g1] "=&s"(g1), [l1] "=&s"(l1),
-          [l2] "=&s"(l2), [dok] "=&s"(dok), [cnt] "=&s"(cnt)
-        : [ox] "v"(r.o.x), [oy] "v"(r.o.y), [oz] "v"(r.o.z), [dx] "v"(r.d.x), [dy] "v"(r.d.y), [dz] "v"(r.d.z),
-          [ix] "v"(t.ix), [iy] "v"(t.iy), [iz] "v"(t.iz), [a] "v"(t.a), [ra] "v"(t.ra), [end] "s"(end),
-          [kmin] "s"(kmin), [tmin] "s"(tmin), [cmask] "s"(class_mask)
-        : "vcc", "scc");
+    asm volatile(RTX_WALK_STEP_ASM(0) RTX_WALK_STEP_ASM(1) RTX_WALK_STEP_ASM(2) RTX_WALK_STEP_ASM(3)
+                     RTX_WALK_STEP_ASM(4) RTX_WALK_STEP_ASM(5)
+                 : [pos] "+v"(t.i), [cl] "+v"(t.closest), [hit] "+v"(t.hit), [pm] "=&s"(pm), [wm] "=&s"(wm),
+                   [save] "=&s"(save), [g1] "=&s"(g1), [l1] "=&s"(l1), [l2] "=&s"(l2), [dok] "=&s"(dok),
+                   [cnt] "=&s"(cnt)
+                 : [ox] "v"(r.o.x), [oy] "v"(r.o.y), [oz] "v"(r.o.z), [dx] "v"(r.d.x), [dy] "v"(r.d.y),
+                   [dz] "v"(r.d.z), [ix] "v"(t.ix), [iy] "v"(t.iy), [iz] "v"(t.iz), [a] "v"(t.a), [ra] "v"(t.ra),
+                   [end] "s"(end), [kmin] "s"(kmin), [tmin] "s"(tmin)
+                 : "v0", "v1", "v2", "v3", "v4", "v5", "v6", "v7", "v8", "v9", "vcc", "scc");
 }
+#undef RTX_WALK_STEP_ASM
 
 // Shade the result of segment `seg` (ray.go:36-53, materials.go:33-113).  Returns true
 // when the path ends, with its colour in `color`; otherwise r / thr hold the next

@@ -76,15 +76,14 @@ __device__ __forceinline__ void traverse_loop(uint32_t& mode, Trav& t, const Ray
         // the wave per step.
         uint32_t done = 0;  // COUNT: lane-steps that tested an entry (a lane on the sentinel idles)
         uint32_t idle = 0;  // COUNT: parked (low 16 bits) and deferred (high 16 bits) lane-steps
-        if constexpr (BATCH) {
+        if constexpr (RTX_ASM_STEP && BATCH && !COUNT && !QUADS && FIXED && !HYB && MED3) {
+            static_assert(STEPS == 6, "walk6_asm takes six steps");
+            walk6_asm(t, r, 16 * n_entries, prim_batch, 0.001f);
+        } else if constexpr (BATCH) {
 #pragma unroll
-            for (int s = 0; s < STEPS; ++s) {
-                if constexpr (RTX_ASM_STEP && !COUNT && !QUADS && FIXED && !HYB && MED3)
-                    trav_step_asm(t, r, 16 * n_entries, prim_batch, 0.001f, 0x260u);  // +-0, +inf classes
-                else
-                    done += trav_step_batched<COUNT, QUADS, FIXED, HYB, MED3>(t, r, E, cnt, 16 * n_entries,
-                                                                             prim_batch, idle);
-            }
+            for (int s = 0; s < STEPS; ++s)
+                done += trav_step_batched<COUNT, QUADS, FIXED, HYB, MED3>(t, r, E, cnt, 16 * n_entries, prim_batch,
+                                                                         idle);
         } else {
 #pragma unroll
             for (int s = 0; s < STEPS; ++s) {
