@@ -965,19 +965,37 @@ __device__ __forceinline__ uint32_t trav_step_batched(Trav& t, const Ray& r, con
         "LR%=_" #K ":\n\t"                                                   \
         "s_mov_b64 exec, %[save]\n"                                          \
         "LE%=_" #K ":\n\t"
-__device__ __forceinline__ void walk6_asm(Trav& t, const Ray& r, uint32_t end, uint32_t kmin, float tmin) {
+// The whole traversal phase (traverse_loop's !COUNT body for this case): six asm steps, then the
+// vote — at_end = pos >= end, walking lanes W, waiting lanes P0 — until no lane walks or at
+// least `thresh` wait; returns the final at_end mask.  Positions only increase along a walk, so
+// every lane reaches the sentinel and the loop ends.
+__device__ __forceinline__ uint64_t walk_phase_asm(Trav& t, const Ray& r, uint32_t end, uint32_t kmin, float tmin,
+                                                   uint64_t W, uint64_t P0, uint32_t thresh) {
     static_assert(LDS_B == 32768, "the asm reads the 'b' halves at offset:32768");
-    uint64_t pm, wm, save, g1, l1, l2, dok;
+    uint64_t pm, wm, save, g1, l1, l2, dok, at;
     uint32_t cnt;
-    asm volatile(RTX_WALK_STEP_ASM(0) RTX_WALK_STEP_ASM(1) RTX_WALK_STEP_ASM(2) RTX_WALK_STEP_ASM(3)
-                     RTX_WALK_STEP_ASM(4) RTX_WALK_STEP_ASM(5)
+    asm volatile("LW%=:\n\t"
+                 RTX_WALK_STEP_ASM(0) RTX_WALK_STEP_ASM(1) RTX_WALK_STEP_ASM(2) RTX_WALK_STEP_ASM(3)
+                 RTX_WALK_STEP_ASM(4) RTX_WALK_STEP_ASM(5)
+                 "v_cmp_ge_u32_e64 %[at], %[pos], %[end]\n\t"
+                 "s_andn2_b64 %[l1], %[W], %[at]\n\t"  // still walking
+                 "s_cmp_eq_u64 %[l1], 0\n\t"
+                 "s_cbranch_scc1 LX%=\n\t"
+                 "s_and_b64 %[l1], %[W], %[at]\n\t"
+                 "s_or_b64 %[l1], %[l1], %[P0]\n\t"  // waiting to shade
+                 "s_bcnt1_i32_b64 %[cnt], %[l1]\n\t"
+                 "s_cmp_lt_u32 %[cnt], %[thresh]\n\t"
+                 "s_cbranch_scc1 LW%=\n"
+                 "LX%=:"
                  : [pos] "+v"(t.i), [cl] "+v"(t.closest), [hit] "+v"(t.hit), [pm] "=&s"(pm), [wm] "=&s"(wm),
                    [save] "=&s"(save), [g1] "=&s"(g1), [l1] "=&s"(l1), [l2] "=&s"(l2), [dok] "=&s"(dok),
-                   [cnt] "=&s"(cnt)
+                   [cnt] "=&s"(cnt), [at] "=&s"(at)
                  : [ox] "v"(r.o.x), [oy] "v"(r.o.y), [oz] "v"(r.o.z), [dx] "v"(r.d.x), [dy] "v"(r.d.y),
                    [dz] "v"(r.d.z), [ix] "v"(t.ix), [iy] "v"(t.iy), [iz] "v"(t.iz), [a] "v"(t.a), [ra] "v"(t.ra),
-                   [end] "s"(end), [kmin] "s"(kmin), [tmin] "s"(tmin)
+                   [end] "s"(end), [kmin] "s"(kmin), [tmin] "s"(tmin), [W] "s"(W), [P0] "s"(P0),
+                   [thresh] "s"(thresh)
                  : "v0", "v1", "v2", "v3", "v4", "v5", "v6", "v7", "v8", "v9", "vcc", "scc");
+    return at;
 }
 #undef RTX_WALK_STEP_ASM
 

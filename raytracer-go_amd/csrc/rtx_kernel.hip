@@ -70,16 +70,19 @@ __device__ __forceinline__ void traverse_loop(uint32_t& mode, Trav& t, const Ray
     // lanes P0, lanes without an item D; per iteration only `at_end` is voted.
     const uint64_t W = ballot(mode == 0), P0 = ballot(mode - 1u < 2u);
     const uint64_t D = COUNT ? ballot(mode == 3) : 0ull;
+    if constexpr (RTX_ASM_STEP && BATCH && !COUNT && !QUADS && FIXED && !HYB && MED3) {
+        static_assert(STEPS == 6, "walk_phase_asm takes six steps per vote");
+        const uint64_t at_end = walk_phase_asm(t, r, 16 * n_entries, prim_batch, 0.001f, W, P0, thresh);
+        if (__builtin_amdgcn_inverse_ballot_w64(W & at_end)) mode = 1;  // walked to the end
+        return;
+    }
     for (;;) {
         // Every lane steps: one that is not traversing (or finishes early) waits on the
         // sentinel, t.i = 16 * n_entries, where a step changes nothing — cheaper than masking
         // the wave per step.
         uint32_t done = 0;  // COUNT: lane-steps that tested an entry (a lane on the sentinel idles)
         uint32_t idle = 0;  // COUNT: parked (low 16 bits) and deferred (high 16 bits) lane-steps
-        if constexpr (RTX_ASM_STEP && BATCH && !COUNT && !QUADS && FIXED && !HYB && MED3) {
-            static_assert(STEPS == 6, "walk6_asm takes six steps");
-            walk6_asm(t, r, 16 * n_entries, prim_batch, 0.001f);
-        } else if constexpr (BATCH) {
+        if constexpr (BATCH) {
 #pragma unroll
             for (int s = 0; s < STEPS; ++s)
                 done += trav_step_batched<COUNT, QUADS, FIXED, HYB, MED3>(t, r, E, cnt, 16 * n_entries, prim_batch,
