@@ -209,8 +209,9 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
     const uint64_t n_units = (uint64_t)n_tiles * nsub;
     const size_t npix = (size_t)p.width * p.rows;
 
-    // the wave's unit (uniform): tile, first sample, items, next item
-    uint32_t u_tile = 0, u_k0 = 0, u_items = 0, cursor = 0;
+    // the wave's unit (uniform, kept in SGPRs: every value below is derived from readfirstlane):
+    // tile origin (u_x8, u_r8), first sample, items, next item
+    uint32_t u_x8 = 0, u_r8 = 0, u_k0 = 0, u_items = 0, cursor = 0;
     bool exhausted = false;
 
     uint32_t mode = M_CLAIM, seg = 0, items_done = 0;
@@ -285,11 +286,13 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
             if (cursor >= u_items && !exhausted) {  // claim the next unit (wave-uniform)
                 uint32_t un = 0;
                 if (lane == 0) un = atomicAdd(p.tile_counter, 1u);
-                const uint64_t uu = (uint32_t)__shfl((int)un, 0);
+                const uint32_t uu = __builtin_amdgcn_readfirstlane(un);  // the whole wave is here: lane 0's
                 exhausted = uu >= n_units;
                 if (!exhausted) {
-                    u_tile = (uint32_t)(uu / nsub);
-                    u_k0 = p.k0 + (uint32_t)(uu % nsub) * p.sub;
+                    const uint32_t u_tile = uu / nsub;
+                    u_x8 = (u_tile % tiles_x) * 8u;
+                    u_r8 = (u_tile / tiles_x) * 8u;
+                    u_k0 = p.k0 + (uu - u_tile * nsub) * p.sub;
                     const uint32_t cnt_k = min(p.sub, p.k0 + p.kn - u_k0);
                     u_items = 64u * cnt_k;
                     cursor = 0;
@@ -303,8 +306,8 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
             bool got = false;
             if (mode == M_CLAIM && rank < u_items - cursor) {
                 const uint32_t j = cursor + rank, l = j & 63u;  // sample-major within the unit
-                const uint32_t lx = (u_tile % tiles_x) * 8u + (l & 7u);
-                const uint32_t lr = (u_tile / tiles_x) * 8u + (l >> 3);
+                const uint32_t lx = u_x8 + (l & 7u);
+                const uint32_t lr = u_r8 + (l >> 3);
                 if (lx < p.width && lr < p.rows) {  // else: outside a ragged tile, claim again
                     const uint32_t x = p.x0 + lx, y = p.y0 + p.rank + lr * p.world;
                     base = pixel_base(c, x, y);
