@@ -33,9 +33,22 @@ __device__ __forceinline__ float dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y 
 __device__ __forceinline__ V3 cross(V3 l, V3 r) {                                                 // vec3.go:129-135
     return v3(l.y * r.z - l.z * r.y, l.z * r.x - l.x * r.z, l.x * r.y - l.y * r.x);
 }
+// 1 / x, correctly rounded.  When every active lane's |x| lies in [2^-125, 2^125] (exponent
+// field 2..252): one Newton step with fma on v_rcp_f32 (3 VALU), which equals the IEEE quotient
+// on all 4.2e9 such inputs (scripts/micro/fastrcp_check.hip, exhaustive on the GPU); else the
+// compiler's division (~10 VALU).  The vote is wave-uniform, so the branch does not diverge.
+__device__ __forceinline__ bool rcp_fast_ok(float x) { return ((__float_as_uint(x) >> 23) & 0xFFu) - 2u <= 250u; }
+__device__ __forceinline__ float rcp_newton(float x) {
+    const float y0 = __builtin_amdgcn_rcpf(x);
+    return __builtin_fmaf(__builtin_fmaf(-x, y0, 1.0f), y0, y0);
+}
+__device__ __forceinline__ float rcp_ieee(float x) {
+    if (__builtin_amdgcn_ballot_w64(!rcp_fast_ok(x)) == 0) return rcp_newton(x);
+    return 1.0f / x;
+}
 __device__ __forceinline__ V3 unit(V3 v) {                                                         // vec3.go:103-113
     float l = __builtin_sqrtf(lensq(v));
-    return scale(v, 1.0f / l);
+    return scale(v, rcp_ieee(l));
 }
 __device__ __forceinline__ bool near_zero(V3 v) {                                                  // vec3.go:170-172
     return __builtin_fabsf(v.x) < 1e-8f && __builtin_fabsf(v.y) < 1e-8f && __builtin_fabsf(v.z) < 1e-8f;
@@ -428,9 +441,10 @@ struct Counters {
 // SKIP_DISK: without defocus the unit-disk sample is drawn but never used (camera.go:279-281)
 // and no later draw depends on it (every event has its own Philox blocks), so a kernel that
 // does not count draws may leave its rejection loop out (Cornell box -1.7 %).
+// b = block (0, 0) of the sample, drawn by the caller (the shading phase draws it together with
+// the other lanes' scatter blocks: one Philox evaluation for both).
 template <bool SKIP_DISK = false>
-__device__ __forceinline__ Ray camera_ray(const rtx_camera& c, V3 base, const PathRng& rng, uint32_t& draws) {
-    U4 b = rng.block(0, 0);
+__device__ __forceinline__ Ray camera_ray(const rtx_camera& c, V3 base, const PathRng& rng, U4 b, uint32_t& draws) {
     const V3 du = v3(c.pixel_du[0], c.pixel_du[1], c.pixel_du[2]);
     const V3 dv = v3(c.pixel_dv[0], c.pixel_dv[1], c.pixel_dv[2]);
     const float dx = -0.5f + unit_f32(b.x);                       // :290
@@ -515,14 +529,14 @@ __device__ __forceinline__ uint32_t hit_material(const SceneRef E, uint32_t hit)
 // lanes), the n lanes still rejecting get 64/n consecutive lanes each, which evaluate
 // attempts base .. base+64/n-1 of that owner in one round; the owner takes the first
 // accepted one.  Same attempt, same bits, about 3 Philox rounds per phase.
+// b0 = block (e, 0) of a lane with hit >= 0, drawn by the caller.
 template <bool QUADS>
 __device__ __forceinline__ Scatter coop_scatter(const Params& p, const SceneRef E, const PathRng& rng,
-                                                uint32_t e, int32_t hit) {
+                                                uint32_t e, int32_t hit, const U4 b0) {
     Scatter out{v3(0.0f, 0.0f, 0.0f), 0u, 0u};
     bool need = false;
     float x = 0.0f, y = 0.0f, z = 0.0f;
     if (hit >= 0) {
-        const U4 b0 = rng.block(e, 0);
         const uint32_t mi = hit_material<QUADS>(E, (uint32_t)hit);
         const uint32_t ty = E.m[mi].type;
         need = ty == RTX_MAT_LAMBERTIAN || ty == RTX_MAT_METAL;
@@ -589,14 +603,20 @@ struct Trav {
 
 __device__ __forceinline__ void trav_begin(Trav& t, const Ray& r) {
     // InBoundary computes 1/dir per node; hoisting it is bit-identical.
-    t.ix = 1.0f / r.d.x;
-    t.iy = 1.0f / r.d.y;
-    t.iz = 1.0f / r.d.z;
+    if (__builtin_amdgcn_ballot_w64(!(rcp_fast_ok(r.d.x) && rcp_fast_ok(r.d.y) && rcp_fast_ok(r.d.z))) == 0) {
+        t.ix = rcp_newton(r.d.x);
+        t.iy = rcp_newton(r.d.y);
+        t.iz = rcp_newton(r.d.z);
+    } else {
+        t.ix = 1.0f / r.d.x;
+        t.iy = 1.0f / r.d.y;
+        t.iz = 1.0f / r.d.z;
+    }
     t.nx = t.ix < 0.0f;
     t.ny = t.iy < 0.0f;
     t.nz = t.iz < 0.0f;
     t.a = lensq(r.d);  // hittables.go:98, loop-invariant
-    t.ra = 1.0f / t.a;
+    t.ra = rcp_ieee(t.a);
     t.safe = __builtin_isfinite(t.ix) && __builtin_isfinite(t.iy) && __builtin_isfinite(t.iz) &&
              __builtin_isfinite(r.o.x) && __builtin_isfinite(r.o.y) && __builtin_isfinite(r.o.z) &&
              t.a >= 0x1p-60f && t.a <= 0x1p60f;
@@ -905,9 +925,9 @@ __device__ __forceinline__ uint32_t trav_step_batched(Trav& t, const Ray& r, con
         "v_mul_f32 v0, %[a], v0\n\t" /* disc = hb*hb - a*c */                \
         "v_mul_f32 v9, v8, v8\n\t"                                           \
         "v_sub_f32 v0, v9, v0\n\t"                                           \
-        "v_cmp_le_f32_e64 %[dok], 0, v0\n\t"                                 \
+        "v_cmp_le_f32_e64 %[pm], 0, v0\n\t"                                 \
         "v_cmp_gt_f32_e32 vcc, 0xf800000, v0\n\t" /* x < 2^-96 */            \
-        "s_and_b64 %[g1], vcc, %[dok]\n\t"                                   \
+        "s_and_b64 %[g1], vcc, %[pm]\n\t"                                   \
         "s_cbranch_scc1 LS%=_" #K "\n\t"                                     \
         "v_sqrt_f32_e32 v2, v0\n\t" /* every lane: x >= 2^-96 or x < 0 */    \
         "s_nop 0\n\t"                                                        \
@@ -956,7 +976,7 @@ __device__ __forceinline__ uint32_t trav_step_batched(Trav& t, const Ray& r, con
         "v_cmp_lt_f32_e64 %[wm], v7, %[cl]\n\t"                              \
         "s_and_b64 %[l2], %[l2], %[wm]\n\t"                                  \
         "s_or_b64 %[l1], %[l1], %[l2]\n\t"                                   \
-        "s_and_b64 %[l1], %[l1], %[dok]\n\t"                                 \
+        "s_and_b64 %[l1], %[l1], %[pm]\n\t"                                 \
         "v_cndmask_b32_e64 v7, v7, v5, %[g1]\n\t"                            \
         "v_lshrrev_b32_e32 v1, 4, %[pos]\n\t"                                \
         "v_cndmask_b32_e64 %[cl], %[cl], v7, %[l1]\n\t"                      \
@@ -972,30 +992,29 @@ __device__ __forceinline__ uint32_t trav_step_batched(Trav& t, const Ray& r, con
 __device__ __forceinline__ uint64_t walk_phase_asm(Trav& t, const Ray& r, uint32_t end, uint32_t kmin, float tmin,
                                                    uint64_t W, uint64_t P0, uint32_t thresh) {
     static_assert(LDS_B == 32768, "the asm reads the 'b' halves at offset:32768");
-    uint64_t pm, wm, save, g1, l1, l2, dok, at;
+    uint64_t pm, wm, save, g1, l1, l2;
     uint32_t cnt;
     asm volatile("LW%=:\n\t"
                  RTX_WALK_STEP_ASM(0) RTX_WALK_STEP_ASM(1) RTX_WALK_STEP_ASM(2) RTX_WALK_STEP_ASM(3)
                  RTX_WALK_STEP_ASM(4) RTX_WALK_STEP_ASM(5)
-                 "v_cmp_ge_u32_e64 %[at], %[pos], %[end]\n\t"
-                 "s_andn2_b64 %[l1], %[W], %[at]\n\t"  // still walking
+                 "v_cmp_ge_u32_e64 %[pm], %[pos], %[end]\n\t"
+                 "s_andn2_b64 %[l1], %[W], %[pm]\n\t"  // still walking
                  "s_cmp_eq_u64 %[l1], 0\n\t"
                  "s_cbranch_scc1 LX%=\n\t"
-                 "s_and_b64 %[l1], %[W], %[at]\n\t"
+                 "s_and_b64 %[l1], %[W], %[pm]\n\t"
                  "s_or_b64 %[l1], %[l1], %[P0]\n\t"  // waiting to shade
                  "s_bcnt1_i32_b64 %[cnt], %[l1]\n\t"
                  "s_cmp_lt_u32 %[cnt], %[thresh]\n\t"
                  "s_cbranch_scc1 LW%=\n"
                  "LX%=:"
                  : [pos] "+v"(t.i), [cl] "+v"(t.closest), [hit] "+v"(t.hit), [pm] "=&s"(pm), [wm] "=&s"(wm),
-                   [save] "=&s"(save), [g1] "=&s"(g1), [l1] "=&s"(l1), [l2] "=&s"(l2), [dok] "=&s"(dok),
-                   [cnt] "=&s"(cnt), [at] "=&s"(at)
+                   [save] "=&s"(save), [g1] "=&s"(g1), [l1] "=&s"(l1), [l2] "=&s"(l2), [cnt] "=&s"(cnt)
                  : [ox] "v"(r.o.x), [oy] "v"(r.o.y), [oz] "v"(r.o.z), [dx] "v"(r.d.x), [dy] "v"(r.d.y),
                    [dz] "v"(r.d.z), [ix] "v"(t.ix), [iy] "v"(t.iy), [iz] "v"(t.iz), [a] "v"(t.a), [ra] "v"(t.ra),
                    [end] "s"(end), [kmin] "s"(kmin), [tmin] "s"(tmin), [W] "s"(W), [P0] "s"(P0),
                    [thresh] "s"(thresh)
                  : "v0", "v1", "v2", "v3", "v4", "v5", "v6", "v7", "v8", "v9", "vcc", "scc");
-    return at;
+    return pm;  // at_end
 }
 #undef RTX_WALK_STEP_ASM
 

@@ -259,7 +259,9 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
         if (ballot(mode != M_DONE) == 0) break;
 
         // ---- shading phase ----------------------------------------------------------
-        const Scatter sc = coop_scatter<QUADS>(p, E, rng, seg + 1, mode == M_SHADE ? t.hit : -1);
+        U4 b0{0u, 0u, 0u, 0u};
+        if (mode == M_SHADE && t.hit >= 0) b0 = rng.block(seg + 1, 0u);
+        const Scatter sc = coop_scatter<QUADS>(p, E, rng, seg + 1, mode == M_SHADE ? t.hit : -1, b0);
         if (COUNT) split_clk(split[0], clk);
         bool ready = false;
         if (mode == M_SHADE) {
@@ -320,7 +322,7 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
             const uint32_t taken = (uint32_t)__popcll(wm);
             cursor = cursor + taken > u_items ? u_items : cursor + taken;
             if (got) {
-                r = camera_ray<!COUNT>(c, base, rng, cnt.draws);  // GetRay, camera.go:257
+                r = camera_ray<!COUNT>(c, base, rng, rng.block(0u, 0u), cnt.draws);  // GetRay, camera.go:257
                 thr = v3(1.0f, 1.0f, 1.0f);
                 acc = v3(0.0f, 0.0f, 0.0f);
                 seg = 0;

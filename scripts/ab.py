@@ -65,6 +65,9 @@ for rnd in range(args.rounds + 1):
         if rnd > 0:
             times[n].append(s.kernel_ms)
 ref = outs[names[0]].cpu().numpy()
+import hashlib  # noqa: E402
+print(f"image sha256 {hashlib.sha256(np.ascontiguousarray(ref).tobytes()).hexdigest()[:16]} (compare across builds)",
+      flush=True)
 for n in names:
     same = np.array_equal(ref, outs[n].cpu().numpy())
     med = float(np.median(times[n]))
