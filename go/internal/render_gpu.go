@@ -25,6 +25,7 @@ import (
 	"fmt"
 	"io"
 	"math"
+	"runtime"
 	"strconv"
 	"strings"
 	"unsafe"
@@ -40,6 +41,8 @@ type gpuTables struct {
 	materials []C.rtx_material
 	textures  []C.rtx_texture
 	texels    []C.uint32_t
+	lists     []C.rtx_list  // Worlds nested in the tree (ABI 5)
+	listRefs  []C.int32_t
 	matIdx    map[Material]C.uint32_t
 	texIdx    map[Texture]C.uint32_t
 }
@@ -194,7 +197,23 @@ func (t *gpuTables) ref(h Hittable) (C.int32_t, error) {
 			q: vec(q.Q), material: mi, u: vec(q.u), d: C.float(q.D), v: vec(q.v), w: vec(q.w), normal: vec(q.normal),
 		})
 		return primRef(C.RTX_PRIM_QUAD, len(t.quads)-1), nil
-	default: // a World nested inside a BVH (hittables.go:55-72 as a child): the CPU path
+	case *World: // a World nested in the tree (hittables.go:55-72 as a BVH child): a list ref
+		if len(v.hittables) == 0 {
+			return 0, errUnsupported
+		}
+		refs := make([]C.int32_t, len(v.hittables))
+		for i, h := range v.hittables {
+			r, err := t.ref(h)
+			if err != nil {
+				return 0, err
+			}
+			refs[i] = r
+		}
+		first := len(t.listRefs)
+		t.listRefs = append(t.listRefs, refs...)
+		t.lists = append(t.lists, C.rtx_list{first: C.uint32_t(first), count: C.uint32_t(len(refs))})
+		return primRef(C.RTX_PRIM_LIST, len(t.lists)-1), nil
+	default:
 		return 0, errUnsupported
 	}
 }
@@ -236,23 +255,40 @@ func (c *Camera) RenderGPU(world Hittable, writer io.Writer, seed uint64, gpus i
 	if err != nil {
 		return err
 	}
+	// desc holds pointers into Go slices: pinned for the call (cgo: Go memory passed to C may
+	// not contain unpinned Go pointers; runtime.Pinner, Go 1.21).
+	var pin runtime.Pinner
+	defer pin.Unpin()
 	var desc C.rtx_scene_desc
 	if len(t.nodes) > 0 {
+		pin.Pin(&t.nodes[0])
 		desc.nodes, desc.n_nodes = &t.nodes[0], C.uint32_t(len(t.nodes))
 	}
+	pin.Pin(&t.roots[0])
 	desc.roots, desc.n_roots = &t.roots[0], C.uint32_t(len(t.roots))
 	if len(t.spheres) > 0 {
+		pin.Pin(&t.spheres[0])
 		desc.spheres, desc.n_spheres = &t.spheres[0], C.uint32_t(len(t.spheres))
 	}
 	if len(t.quads) > 0 {
+		pin.Pin(&t.quads[0])
 		desc.quads, desc.n_quads = &t.quads[0], C.uint32_t(len(t.quads))
 	}
+	pin.Pin(&t.materials[0])
 	desc.materials, desc.n_materials = &t.materials[0], C.uint32_t(len(t.materials))
 	if len(t.textures) > 0 {
+		pin.Pin(&t.textures[0])
 		desc.textures, desc.n_textures = &t.textures[0], C.uint32_t(len(t.textures))
 	}
 	if len(t.texels) > 0 {
+		pin.Pin(&t.texels[0])
 		desc.texels, desc.n_texels = &t.texels[0], C.uint64_t(len(t.texels))
+	}
+	if len(t.lists) > 0 {
+		pin.Pin(&t.lists[0])
+		pin.Pin(&t.listRefs[0])
+		desc.lists, desc.n_lists = &t.lists[0], C.uint32_t(len(t.lists))
+		desc.list_refs, desc.n_list_refs = &t.listRefs[0], C.uint32_t(len(t.listRefs))
 	}
 	var scene *C.rtx_scene
 	if rc := C.rtx_scene_create(&desc, &scene); rc != 0 {

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define RTX_ABI_VERSION 4
+#define RTX_ABI_VERSION 5
 
 /* ---- status codes ------------------------------------------------------------ */
 enum {
@@ -50,9 +50,13 @@ enum {
 /* ---- scene tables ------------------------------------------------------------ */
 
 /* Child / root reference.  ref >= 0: index into rtx_scene_desc.nodes.
- * ref < 0: a primitive, p = ~ref, type = p >> 28 (RTX_PRIM_*), index = p & 0x0FFFFFFF. */
+ * ref < 0: a primitive, p = ~ref, type = p >> 28 (RTX_PRIM_*), index = p & 0x0FFFFFFF.
+ * RTX_PRIM_LIST (ABI 5): a World nested in the tree (a World handed to NewBVH as a child,
+ * hittables.go:39-76): index into rtx_scene_desc.lists; its items are hit in order with a
+ * running closest bound, (*World).Hit hittables.go:55-72. */
 #define RTX_PRIM_SPHERE 0u
 #define RTX_PRIM_QUAD 1u
+#define RTX_PRIM_LIST 2u
 #define RTX_REF_PRIM(type, index) ((int32_t) ~((int32_t)(((uint32_t)(type) << 28) | ((uint32_t)(index)&0x0FFFFFFFu))))
 
 /* A BVH interior node exactly as internal/bvh.go:132-185 builds it: an AABB
@@ -138,6 +142,12 @@ typedef struct rtx_texture { /* 48 B */
     float pad;
 } rtx_texture;
 
+/* A World nested in the tree: the refs list_refs[first .. first + count), in Add order.  8 B */
+typedef struct rtx_list {
+    uint32_t first;
+    uint32_t count;
+} rtx_list;
+
 typedef struct rtx_scene_desc {
     const rtx_bvh_node* nodes;
     uint32_t n_nodes;
@@ -155,6 +165,11 @@ typedef struct rtx_scene_desc {
     const rtx_texture* textures;
     const uint32_t* texels; /* image RGBA16 texels and Perlin tables (uint32 words) */
     uint64_t n_texels;
+    /* ABI 5: Worlds nested in the tree (RTX_PRIM_LIST refs); zero / NULL when there are none. */
+    const rtx_list* lists;
+    uint32_t n_lists;
+    uint32_t n_list_refs;
+    const int32_t* list_refs;
 } rtx_scene_desc;
 
 /* ---- camera ------------------------------------------------------------------ */

@@ -459,14 +459,42 @@ static int bvh_hit(const ctx_t* cx, const rtx_bvh_node* n, const ray_t* r, float
     return 0;
 }
 
+static int list_hit(const ctx_t* cx, const rtx_list* l, const ray_t* r, float tmin, float tmax, hit_t* out);
+
 static int hit_ref(const ctx_t* cx, int32_t ref, const ray_t* r, float tmin, float tmax, hit_t* out, int dup) {
-    if (ref >= 0) return bvh_hit(cx, &cx->s->nodes[ref], r, tmin, tmax, out);
+    if (ref >= 0 || ((uint32_t)(~ref)) >> 28 == RTX_PRIM_LIST) {
+        /* A node or a nested World.  As the right child of a one-element split (dup,
+         * bvh.go:162-165) its second call runs with the bound clipped to the first one's hit
+         * and finds nothing new (every test is monotone in the bound); the device emits it
+         * once, so its work is not counted here either. */
+        oracle_counters saved;
+        if (dup) saved = *cx->c;
+        int h = ref >= 0 ? bvh_hit(cx, &cx->s->nodes[ref], r, tmin, tmax, out)
+                         : list_hit(cx, &cx->s->lists[((uint32_t)(~ref)) & 0x0FFFFFFFu], r, tmin, tmax, out);
+        if (dup) *cx->c = saved;
+        return h;
+    }
     uint32_t p = (uint32_t)(~ref);
     uint32_t type = p >> 28, idx = p & 0x0FFFFFFFu;
     cx->c->prim_tests_ref++;
     if (!dup) cx->c->prim_tests++;
     if (type == RTX_PRIM_QUAD) return quad_hit(&cx->s->quads[idx], r, tmin, tmax, out);
     return sphere_hit(cx, &cx->s->spheres[idx], r, tmin, tmax, out);
+}
+
+/* (*World).Hit, hittables.go:55-72, of a World nested in the tree (RTX_PRIM_LIST). */
+static int list_hit(const ctx_t* cx, const rtx_list* l, const ray_t* r, float tmin, float tmax, hit_t* out) {
+    int hit_any = 0;
+    float closest = tmax;
+    for (uint32_t i = 0; i < l->count; ++i) {
+        hit_t h;
+        if (hit_ref(cx, cx->s->list_refs[l->first + i], r, tmin, closest, &h, 0)) {
+            hit_any = 1;
+            *out = h;
+            closest = h.t;
+        }
+    }
+    return hit_any;
 }
 
 /* The world passed to Render: a BVH (one root) or a World list, hittables.go:55-72. */
@@ -868,6 +896,9 @@ static int scene_supported(const rtx_scene_desc* s) {
             return 0; /* RGBA16 raster + border texel (rtx.h) */
     }
     if (s->n_quads && !s->quads) return 0;
+    if (s->n_lists && (!s->lists || !s->list_refs)) return 0;
+    for (uint32_t i = 0; i < s->n_lists; ++i)
+        if ((uint64_t)s->lists[i].first + s->lists[i].count > s->n_list_refs) return 0;
     return 1;
 }
 

@@ -181,27 +181,52 @@ int check_ref(const rtx_scene_desc* d, int32_t ref) {
         if (idx >= d->n_quads) return fail(RTX_ERR_INVALID_ARG, "quad ref %u out of range (%u quads)", idx, d->n_quads);
         return RTX_OK;
     }
+    if (type == RTX_PRIM_LIST) {  // a nested World (ABI 5)
+        if (idx >= d->n_lists || !d->lists) return fail(RTX_ERR_INVALID_ARG, "list ref %u out of range (%u lists)", idx, d->n_lists);
+        const rtx_list& l = d->lists[idx];
+        if (l.count == 0) return fail(RTX_ERR_INVALID_ARG, "list %u is empty (a World with nothing added)", idx);
+        if (!d->list_refs || (uint64_t)l.first + l.count > d->n_list_refs)
+            return fail(RTX_ERR_INVALID_ARG, "list %u items out of range (%u list refs)", idx, d->n_list_refs);
+        return RTX_OK;
+    }
     return fail(RTX_ERR_INVALID_ARG, "unknown primitive type %u", type);
 }
 
-// Reject a node graph with a cycle (a Go BVH cannot have one, a hand-built table can).
+// Graph vertex of a ref for check_acyclic: nodes 0..n_nodes-1, lists after them; -1 for a leaf.
+int64_t vertex_of(const rtx_scene_desc* d, int32_t ref) {
+    if (ref >= 0) return ref;
+    const uint32_t p = (uint32_t)(~ref);
+    return (p >> 28) == RTX_PRIM_LIST ? (int64_t)d->n_nodes + (p & 0x0FFFFFFFu) : -1;
+}
+
+// Reject a node / list graph with a cycle (a Go BVH cannot have one, a hand-built table can).
 int check_acyclic(const rtx_scene_desc* d) {
-    std::vector<uint8_t> state(d->n_nodes, 0);  // 0 new, 1 on path, 2 done
-    struct F { int32_t node; int child; };
+    std::vector<uint8_t> state((size_t)d->n_nodes + d->n_lists, 0);  // 0 new, 1 on path, 2 done
+    struct F { int64_t v; uint32_t child; };
+    auto n_children = [&](int64_t v) -> uint32_t {
+        return v < (int64_t)d->n_nodes ? 2u : d->lists[v - d->n_nodes].count;
+    };
+    auto child = [&](int64_t v, uint32_t k) -> int32_t {
+        if (v < (int64_t)d->n_nodes) return k == 0 ? d->nodes[v].left : d->nodes[v].right;
+        const rtx_list& l = d->lists[v - d->n_nodes];
+        return d->list_refs[l.first + k];
+    };
     for (uint32_t r = 0; r < d->n_roots; ++r) {
         if (int rc = check_ref(d, d->roots[r])) return rc;
-        if (d->roots[r] < 0 || state[d->roots[r]] == 2) continue;
-        std::vector<F> st{{d->roots[r], 0}};
-        state[d->roots[r]] = 1;
+        const int64_t v0 = vertex_of(d, d->roots[r]);
+        if (v0 < 0 || state[v0] == 2) continue;
+        std::vector<F> st{{v0, 0}};
+        state[v0] = 1;
         while (!st.empty()) {
             F& f = st.back();
-            if (f.child == 2) { state[f.node] = 2; st.pop_back(); continue; }
-            const int32_t ref = f.child++ == 0 ? d->nodes[f.node].left : d->nodes[f.node].right;
+            if (f.child == n_children(f.v)) { state[f.v] = 2; st.pop_back(); continue; }
+            const int32_t ref = child(f.v, f.child++);
             if (int rc = check_ref(d, ref)) return rc;
-            if (ref < 0 || state[ref] == 2) continue;
-            if (state[ref] == 1) return fail(RTX_ERR_INVALID_ARG, "BVH node graph has a cycle through node %d", ref);
-            state[ref] = 1;
-            st.push_back({ref, 0});
+            const int64_t v = vertex_of(d, ref);
+            if (v < 0 || state[v] == 2) continue;
+            if (state[v] == 1) return fail(RTX_ERR_INVALID_ARG, "BVH node / list graph has a cycle through ref %d", ref);
+            state[v] = 1;
+            st.push_back({v, 0});
         }
     }
     return RTX_OK;
@@ -228,7 +253,12 @@ int emit(const rtx_scene_desc* d, int32_t root, std::vector<rtx_entry>& out) {
         if (out.size() >= limit) return fail(RTX_ERR_INVALID_ARG, "BVH expands to more than %zu entries", limit);
         rtx_entry e;
         std::memset(&e, 0, sizeof(e));
-        if (f.ref >= 0) {
+        if (f.ref < 0 && (((uint32_t)(~f.ref)) >> 28) == RTX_PRIM_LIST) {
+            // a nested World (hittables.go:55-72): its items one after another, each against the
+            // running bound — the walk simply continues into the next item's entries
+            const rtx_list& l = d->lists[((uint32_t)(~f.ref)) & 0x0FFFFFFFu];
+            for (uint32_t k = l.count; k-- > 0;) stack.push_back({d->list_refs[l.first + k], -1});
+        } else if (f.ref >= 0) {
             const rtx_bvh_node& n = d->nodes[f.ref];
             e.a[0] = n.bmin[0]; e.a[1] = n.bmin[1]; e.a[2] = n.bmin[2];
             e.b[0] = n.bmax[0]; e.b[1] = n.bmax[1]; e.b[2] = n.bmax[2];
@@ -692,7 +722,7 @@ extern "C" {
 int rtx_version(void) { return RTX_ABI_VERSION; }
 
 const char* rtx_build_info(void) {
-    return "librtx gfx950 megakernel (ABI 4: persistent (pixel, sample) item waves, LDS scene, threaded pre-order BVH, "
+    return "librtx gfx950 megakernel (ABI 5: persistent (pixel, sample) item waves, LDS scene, threaded pre-order BVH, "
            "RGBA16 image texels, RCCL band gather); built " __DATE__ " " __TIME__;
 }
 
@@ -712,6 +742,8 @@ int rtx_scene_create(const rtx_scene_desc* d, rtx_scene** out) {
     *out = nullptr;
     if (d->n_roots == 0 || !d->roots) return fail(RTX_ERR_INVALID_ARG, "scene has no root");
     if (d->n_nodes && !d->nodes) return fail(RTX_ERR_INVALID_ARG, "nodes is NULL");
+    if (d->n_lists && !d->lists) return fail(RTX_ERR_INVALID_ARG, "lists is NULL");
+    if (d->n_list_refs && !d->list_refs) return fail(RTX_ERR_INVALID_ARG, "list_refs is NULL");
     if (int rc = validate_tables(d)) return rc;
     if (int rc = check_acyclic(d)) return rc;
     rtx_scene* s = new rtx_scene();

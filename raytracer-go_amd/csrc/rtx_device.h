@@ -985,6 +985,145 @@ __device__ __forceinline__ uint32_t trav_step_batched(Trav& t, const Ray& r, con
         "LR%=_" #K ":\n\t"                                                   \
         "s_mov_b64 exec, %[save]\n"                                          \
         "LE%=_" #K ":\n\t"
+// RTX_WALK_PREFETCH (default): the lane's entry stays in v0-v7 from one step to the next.  A box
+// step reads the node lanes' next entries at its end; a sphere step moves what its test needs
+// (centre, r^2, the entry index) to v10-v14 and issues the read of each primitive lane's successor
+// (b.z) BEFORE the test, so the LDS round trip runs under the ~60 instructions of the sphere test.
+// Lanes of the other kind, and lanes parked on the sentinel, keep their entry: no re-read.  Every
+// step starts with s_waitcnt; the phase starts with one read for all lanes and ends with a wait.
+#define RTX_WALK_STEP_PF(K)                                                  \
+        "s_waitcnt lgkmcnt(0)\n\t"                                           \
+        "v_cmp_gt_i32_e64 %[pm], -1, v7\n\t"                                 \
+        "v_cmp_lt_u32_e64 %[wm], %[pos], %[end]\n\t"                         \
+        "s_andn2_b64 %[wm], %[wm], %[pm]\n\t"                                \
+        "s_bcnt1_i32_b64 %[cnt], %[pm]\n\t"                                  \
+        "s_cmp_ge_u32 %[cnt], %[kmin]\n\t"                                   \
+        "s_cbranch_scc1 LP%=_" #K "\n\t"                                     \
+        "s_cmp_eq_u64 %[wm], 0\n\t"                                          \
+        "s_cbranch_scc1 LP%=_" #K "\n\t"                                     \
+        /* ---- box tests on the node lanes, then their next entries */      \
+        "s_and_saveexec_b64 %[save], %[wm]\n\t"                              \
+        "v_sub_f32 v0, v0, %[ox]\n\t"                                        \
+        "v_sub_f32 v4, v4, %[ox]\n\t"                                        \
+        "v_sub_f32 v1, v1, %[oy]\n\t"                                        \
+        "v_sub_f32 v5, v5, %[oy]\n\t"                                        \
+        "v_mul_f32 v0, v0, %[ix]\n\t"                                        \
+        "v_mul_f32 v4, v4, %[ix]\n\t"                                        \
+        "v_sub_f32 v2, v2, %[oz]\n\t"                                        \
+        "v_sub_f32 v6, v6, %[oz]\n\t"                                        \
+        "v_mul_f32 v1, v1, %[iy]\n\t"                                        \
+        "v_mul_f32 v5, v5, %[iy]\n\t"                                        \
+        "v_med3_f32 v8, %[tmin], v0, v4\n\t"                                 \
+        "v_med3_f32 v9, %[cl], v0, v4\n\t"                                   \
+        "v_mul_f32 v2, v2, %[iz]\n\t"                                        \
+        "v_mul_f32 v6, v6, %[iz]\n\t"                                        \
+        "v_med3_f32 v8, v8, v1, v5\n\t"                                      \
+        "v_med3_f32 v9, v9, v1, v5\n\t"                                      \
+        "v_med3_f32 v8, v8, v2, v6\n\t"                                      \
+        "v_med3_f32 v9, v9, v2, v6\n\t"                                      \
+        "v_cmp_lt_f32_e32 vcc, v8, v9\n\t"                                   \
+        "s_nop 1\n\t"                                                        \
+        "v_cndmask_b32_e32 %[pos], v3, v7, vcc\n\t"                          \
+        "ds_read_b128 v[0:3], %[pos]\n\t"                                    \
+        "ds_read_b128 v[4:7], %[pos] offset:32768\n\t" /* LDS_B */          \
+        "s_mov_b64 exec, %[save]\n\t"                                        \
+        "s_branch LE%=_" #K "\n"                                             \
+        /* ---- sphere tests on the primitive lanes, successor read first */ \
+        "LP%=_" #K ":\n\t"                                                   \
+        "s_and_saveexec_b64 %[save], %[pm]\n\t"                              \
+        "s_cbranch_execz LR%=_" #K "\n\t"                                    \
+        "v_sub_f32 v10, %[ox], v0\n\t" /* oc = o - center */                 \
+        "v_sub_f32 v11, %[oy], v1\n\t"                                       \
+        "v_sub_f32 v12, %[oz], v2\n\t"                                       \
+        "v_mov_b32 v13, v4\n\t"        /* r^2 */                             \
+        "v_lshrrev_b32_e32 v14, 4, %[pos]\n\t" /* this entry's index */      \
+        "v_mov_b32 %[pos], v6\n\t"     /* successor */                       \
+        "ds_read_b128 v[0:3], %[pos]\n\t"                                    \
+        "ds_read_b128 v[4:7], %[pos] offset:32768\n\t"                       \
+        "v_mul_f32 v8, %[dx], v10\n\t" /* hb = d.oc */                       \
+        "v_mul_f32 v9, %[dy], v11\n\t"                                       \
+        "v_add_f32 v8, v8, v9\n\t"                                           \
+        "v_mul_f32 v9, %[dz], v12\n\t"                                       \
+        "v_add_f32 v8, v8, v9\n\t"                                           \
+        "v_mul_f32 v10, v10, v10\n\t" /* c = |oc|^2 - r^2 */                 \
+        "v_mul_f32 v11, v11, v11\n\t"                                        \
+        "v_add_f32 v10, v10, v11\n\t"                                        \
+        "v_mul_f32 v12, v12, v12\n\t"                                        \
+        "v_add_f32 v10, v10, v12\n\t"                                        \
+        "v_sub_f32 v10, v10, v13\n\t"                                        \
+        "v_mul_f32 v10, %[a], v10\n\t" /* disc = hb*hb - a*c */              \
+        "v_mul_f32 v9, v8, v8\n\t"                                           \
+        "v_sub_f32 v10, v9, v10\n\t"                                         \
+        "v_cmp_le_f32_e64 %[pm], 0, v10\n\t"                                 \
+        "v_cmp_gt_f32_e32 vcc, 0xf800000, v10\n\t" /* x < 2^-96 */           \
+        "s_and_b64 %[g1], vcc, %[pm]\n\t"                                    \
+        "s_cbranch_scc1 LS%=_" #K "\n\t"                                     \
+        "v_sqrt_f32_e32 v12, v10\n\t" /* every lane: x >= 2^-96 or x < 0 */  \
+        "s_nop 0\n\t"                                                        \
+        "v_add_u32_e32 v9, -1, v12\n\t"                                      \
+        "v_add_u32_e32 v11, 1, v12\n\t"                                      \
+        "v_fma_f32 v13, -v9, v12, v10\n\t"                                   \
+        "v_fma_f32 v15, -v11, v12, v10\n\t"                                  \
+        "v_cmp_ge_f32_e64 %[g1], 0, v13\n\t"                                 \
+        "s_nop 1\n\t"                                                        \
+        "v_cndmask_b32_e64 v12, v12, v9, %[g1]\n\t"                          \
+        "v_cmp_lt_f32_e64 %[g1], 0, v15\n\t"                                 \
+        "s_nop 1\n\t"                                                        \
+        "v_cndmask_b32_e64 v12, v12, v11, %[g1]\n\t"                         \
+        "s_branch LQ%=_" #K "\n"                                             \
+        "LS%=_" #K ":\n\t" /* some lane: 0 <= x < 2^-96, scaled by 2^32 */   \
+        "v_mul_f32 v13, 0x4f800000, v10\n\t"                                 \
+        "v_cndmask_b32_e32 v13, v10, v13, vcc\n\t"                           \
+        "v_sqrt_f32_e32 v12, v13\n\t"                                        \
+        "s_nop 0\n\t"                                                        \
+        "v_add_u32_e32 v9, -1, v12\n\t"                                      \
+        "v_add_u32_e32 v11, 1, v12\n\t"                                      \
+        "v_fma_f32 v10, -v9, v12, v13\n\t"                                   \
+        "v_fma_f32 v15, -v11, v12, v13\n\t"                                  \
+        "v_cmp_ge_f32_e64 %[g1], 0, v10\n\t"                                 \
+        "s_nop 1\n\t"                                                        \
+        "v_cndmask_b32_e64 v12, v12, v9, %[g1]\n\t"                          \
+        "v_cmp_lt_f32_e64 %[g1], 0, v15\n\t"                                 \
+        "s_nop 1\n\t"                                                        \
+        "v_cndmask_b32_e64 v12, v12, v11, %[g1]\n\t"                         \
+        "v_mul_f32 v9, 0x37800000, v12\n\t" /* x 2^-16 when scaled */        \
+        "v_cndmask_b32_e32 v12, v12, v9, vcc\n"                              \
+        "LQ%=_" #K ":\n\t" /* v12 = sqrt(disc) */                            \
+        "v_sub_f32_e64 v11, -v8, v12\n\t" /* -hb - sq */                     \
+        "v_add_f32_e64 v13, -v8, v12\n\t" /* -hb + sq */                     \
+        "v_mul_f32 v15, v11, %[ra]\n\t"   /* div_by: q0 = n y */             \
+        "v_mul_f32 v16, v13, %[ra]\n\t"                                      \
+        "v_fma_f32 v11, -%[a], v15, v11\n\t" /* e = n - a q0 */              \
+        "v_fma_f32 v13, -%[a], v16, v13\n\t"                                 \
+        "v_fmac_f32 v15, v11, %[ra]\n\t" /* t1 = q0 + e y */                 \
+        "v_fmac_f32 v16, v13, %[ra]\n\t" /* t2 */                            \
+        "v_cmp_lt_f32_e64 %[g1], %[tmin], v15\n\t"                           \
+        "v_cmp_lt_f32_e64 %[l1], v15, %[cl]\n\t"                             \
+        "v_cmp_lt_f32_e64 %[l2], %[tmin], v16\n\t"                           \
+        "s_and_b64 %[l1], %[l1], %[g1]\n\t"                                  \
+        "s_andn2_b64 %[l2], %[l2], %[g1]\n\t"                                \
+        "v_cmp_lt_f32_e64 %[wm], v16, %[cl]\n\t"                             \
+        "s_and_b64 %[l2], %[l2], %[wm]\n\t"                                  \
+        "s_or_b64 %[l1], %[l1], %[l2]\n\t"                                   \
+        "s_and_b64 %[l1], %[l1], %[pm]\n\t"                                  \
+        "v_cndmask_b32_e64 v16, v16, v15, %[g1]\n\t"                         \
+        "v_cndmask_b32_e64 %[cl], %[cl], v16, %[l1]\n\t"                     \
+        "v_cndmask_b32_e64 %[hit], %[hit], v14, %[l1]\n"                     \
+        "LR%=_" #K ":\n\t"                                                   \
+        "s_mov_b64 exec, %[save]\n"                                          \
+        "LE%=_" #K ":\n\t"
+#ifndef RTX_WALK_PREFETCH
+#define RTX_WALK_PREFETCH 1
+#endif
+#if RTX_WALK_PREFETCH
+#define RTX_WALK_STEP RTX_WALK_STEP_PF
+#define RTX_WALK_BEGIN "ds_read_b128 v[0:3], %[pos]\n\tds_read_b128 v[4:7], %[pos] offset:32768\n"
+#define RTX_WALK_END "\n\ts_waitcnt lgkmcnt(0)"
+#else
+#define RTX_WALK_STEP RTX_WALK_STEP_ASM
+#define RTX_WALK_BEGIN ""
+#define RTX_WALK_END ""
+#endif
 // The whole traversal phase (traverse_loop's !COUNT body for this case): six asm steps, then the
 // vote — at_end = pos >= end, walking lanes W, waiting lanes P0 — until no lane walks or at
 // least `thresh` wait; returns the final at_end mask.  Positions only increase along a walk, so
@@ -994,9 +1133,10 @@ __device__ __forceinline__ uint64_t walk_phase_asm(Trav& t, const Ray& r, uint32
     static_assert(LDS_B == 32768, "the asm reads the 'b' halves at offset:32768");
     uint64_t pm, wm, save, g1, l1, l2;
     uint32_t cnt;
-    asm volatile("LW%=:\n\t"
-                 RTX_WALK_STEP_ASM(0) RTX_WALK_STEP_ASM(1) RTX_WALK_STEP_ASM(2) RTX_WALK_STEP_ASM(3)
-                 RTX_WALK_STEP_ASM(4) RTX_WALK_STEP_ASM(5)
+    asm volatile(RTX_WALK_BEGIN
+                 "LW%=:\n\t"
+                 RTX_WALK_STEP(0) RTX_WALK_STEP(1) RTX_WALK_STEP(2) RTX_WALK_STEP(3) RTX_WALK_STEP(4)
+                 RTX_WALK_STEP(5)
                  "v_cmp_ge_u32_e64 %[pm], %[pos], %[end]\n\t"
                  "s_andn2_b64 %[l1], %[W], %[pm]\n\t"  // still walking
                  "s_cmp_eq_u64 %[l1], 0\n\t"
@@ -1006,17 +1146,22 @@ __device__ __forceinline__ uint64_t walk_phase_asm(Trav& t, const Ray& r, uint32
                  "s_bcnt1_i32_b64 %[cnt], %[l1]\n\t"
                  "s_cmp_lt_u32 %[cnt], %[thresh]\n\t"
                  "s_cbranch_scc1 LW%=\n"
-                 "LX%=:"
+                 "LX%=:" RTX_WALK_END
                  : [pos] "+v"(t.i), [cl] "+v"(t.closest), [hit] "+v"(t.hit), [pm] "=&s"(pm), [wm] "=&s"(wm),
                    [save] "=&s"(save), [g1] "=&s"(g1), [l1] "=&s"(l1), [l2] "=&s"(l2), [cnt] "=&s"(cnt)
                  : [ox] "v"(r.o.x), [oy] "v"(r.o.y), [oz] "v"(r.o.z), [dx] "v"(r.d.x), [dy] "v"(r.d.y),
                    [dz] "v"(r.d.z), [ix] "v"(t.ix), [iy] "v"(t.iy), [iz] "v"(t.iz), [a] "v"(t.a), [ra] "v"(t.ra),
                    [end] "s"(end), [kmin] "s"(kmin), [tmin] "s"(tmin), [W] "s"(W), [P0] "s"(P0),
                    [thresh] "s"(thresh)
-                 : "v0", "v1", "v2", "v3", "v4", "v5", "v6", "v7", "v8", "v9", "vcc", "scc");
+                 : "v0", "v1", "v2", "v3", "v4", "v5", "v6", "v7", "v8", "v9", "v10", "v11", "v12", "v13", "v14",
+                   "v15", "v16", "vcc", "scc");
     return pm;  // at_end
 }
 #undef RTX_WALK_STEP_ASM
+#undef RTX_WALK_STEP_PF
+#undef RTX_WALK_STEP
+#undef RTX_WALK_BEGIN
+#undef RTX_WALK_END
 
 // Shade the result of segment `seg` (ray.go:36-53, materials.go:33-113).  Returns true
 // when the path ends, with its colour in `color`; otherwise r / thr hold the next

@@ -128,8 +128,8 @@ struct Flattener {
     bool ref(const HittablePtr& root, int32_t& out) {
         // child slots live in fs.nodes, which may reallocate: patch through indices
         struct Patch {
-            int32_t node;
-            int side;  // 0 left, 1 right, -1 external slot
+            int32_t node;  // side 2: the index into fs.list_refs
+            int side;      // 0 left, 1 right, 2 list item, -1 external slot
             int32_t* ext;
         };
         std::vector<std::pair<const Hittable*, Patch>> stack{{root.get(), Patch{-1, -1, &out}}};
@@ -170,14 +170,22 @@ struct Flattener {
                 r = RTX_REF_PRIM(RTX_PRIM_QUAD, fs.quads.size());
                 fs.quads.push_back(qd);
                 refs[h] = r;
-            } else if (dynamic_cast<const World*>(h)) {
-                return fail(RTX_ERR_UNSUPPORTED, "a World nested inside a BVH is not on the GPU path");
+            } else if (auto w = dynamic_cast<const World*>(h)) {  // a nested World: a list ref (ABI 5)
+                if (w->hittables.empty()) return fail(RTX_ERR_INVALID_ARG, "empty World nested in the tree");
+                rtx_list l{(uint32_t)fs.list_refs.size(), (uint32_t)w->hittables.size()};
+                r = RTX_REF_PRIM(RTX_PRIM_LIST, fs.lists.size());
+                fs.lists.push_back(l);
+                fs.list_refs.resize(fs.list_refs.size() + l.count, 0);
+                refs[h] = r;
+                for (uint32_t k = l.count; k-- > 0;)
+                    stack.push_back({w->hittables[k].get(), Patch{(int32_t)(l.first + k), 2, nullptr}});
             } else {
                 return fail(RTX_ERR_UNSUPPORTED, "unknown Hittable type");
             }
             if (patch.side < 0) *patch.ext = r;
             else if (patch.side == 0) fs.nodes[patch.node].left = r;
-            else fs.nodes[patch.node].right = r;
+            else if (patch.side == 1) fs.nodes[patch.node].right = r;
+            else fs.list_refs[(size_t)patch.node] = r;
         }
         return true;
     }
@@ -218,6 +226,10 @@ Error Flatten(const HittablePtr& world, FlatScene& fs) {
     d.n_textures = (uint32_t)fs.textures.size();
     d.texels = fs.texels.data();
     d.n_texels = fs.texels.size();
+    d.lists = fs.lists.data();
+    d.n_lists = (uint32_t)fs.lists.size();
+    d.list_refs = fs.list_refs.data();
+    d.n_list_refs = (uint32_t)fs.list_refs.size();
     return Error{};
 }
 

@@ -340,6 +340,8 @@ struct FlatScene {
     std::vector<rtx_material> materials;
     std::vector<rtx_texture> textures;
     std::vector<uint32_t> texels;
+    std::vector<rtx_list> lists;       // Worlds nested in the tree (RTX_PRIM_LIST refs)
+    std::vector<int32_t> list_refs;
     rtx_scene_desc desc{};  // views into the vectors above (valid while FlatScene lives)
     std::unordered_map<const Material*, uint32_t> mat_index;  // Material -> materials[]
 };

@@ -1,6 +1,7 @@
 // scenes.cpp — main.go scene builders restated over the seeded streams.
 #include "scenes.h"
 
+#include <algorithm>
 #include <cmath>
 
 namespace internal {
@@ -72,6 +73,44 @@ SceneSpec RandSpheres(uint64_t seed) {
     s.list = world;
     s.bvh_draw0 = GlobalRand().Drawn();
     s.world = NewBVHFromWorld(*world);                                                        // :287
+    return s;
+}
+
+SceneSpec NestedWorlds(uint64_t seed) {
+    SceneSpec s;
+    s.name = "nested_worlds";
+    s.opts = rand_spheres_camera();
+    Seed(seed);
+    auto randCtx = NewRand(seed);
+    auto flat = NewWorld();
+    grid_spheres(*flat, *randCtx, 0.8f, 0.95f);
+    // The grid in Worlds of up to 22 spheres (one per grid row, in Add order), handed to
+    // NewBVHFromWorld as children; row 3 holds a BVH of its first half and a World of the
+    // rest, itself holding a World of two big spheres (hittables.go:55-72 nested 3 deep).
+    auto top = NewWorld();
+    top->Add(NewSphere(NewVec3(0, -1000, 0), 1000, checkered_ground()));
+    const auto& hs = flat->hittables;
+    for (size_t r = 0; r * 22 < hs.size(); ++r) {
+        auto row = NewWorld();
+        const size_t a = r * 22, b = std::min(hs.size(), a + 22);
+        if (r == 3 && b - a > 4) {
+            auto half = NewWorld();
+            for (size_t k = a; k < (a + b) / 2; ++k) half->Add(hs[k]);
+            auto rest = NewWorld();
+            for (size_t k = (a + b) / 2; k < b; ++k) rest->Add(hs[k]);
+            auto big = NewWorld();
+            big->Add(NewSphere(NewVec3(0, 1, 0), 1, NewDielectric(1.5f)));
+            big->Add(NewSphere(NewVec3(-4, 1, 0), 1, NewLambertian(NewSolidColor(0.4f, 0.2f, 0.1f))));
+            rest->Add(big);
+            row->Add(NewBVHFromWorld(*half));
+            row->Add(rest);
+        } else {
+            for (size_t k = a; k < b; ++k) row->Add(hs[k]);
+        }
+        top->Add(row);
+    }
+    top->Add(NewSphere(NewVec3(4, 1, 0), 1, NewMetal(NewVec3(0.7f, 0.6f, 0.5f), 0)));
+    s.world = NewBVHFromWorld(*top);
     return s;
 }
 
@@ -328,6 +367,7 @@ bool BuildScene(const std::string& name, uint64_t seed, SceneSpec& out) {
     else if (name == "earth_far_side") out = Earth(seed, 2048, 1024, nullptr, -12.0f);
     else if (name == "quad_demo") out = QuadDemo(seed);
     else if (name == "cornell_box") out = CornellBox(seed);
+    else if (name == "nested_worlds") out = NestedWorlds(seed);
     else if (name == "perlin_demo") out = PerlinDemo(seed);
     else if (name == "simple_light_demo") out = SimpleLightDemo(seed);
     else return false;

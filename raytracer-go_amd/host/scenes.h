@@ -23,6 +23,9 @@ struct SceneSpec {
 
 // randSpheres, main.go:227-289 — the north-star scene (configs 1-3).
 SceneSpec RandSpheres(uint64_t seed);
+// randSpheres' grid in Worlds nested inside the BVH (a World as a BVH child, hittables.go:55-72;
+// main.go never builds one, the API allows it): the ABI 5 list refs.
+SceneSpec NestedWorlds(uint64_t seed);
 // Config 4: 100 000 r=0.2 spheres, centres uniform on the y=0.2 plane over
 // [-158,158)^2 (the randSpheres grid density), materials 80/15/5 as main.go:258-270,
 // plus the checkered ground sphere; randSpheres camera.

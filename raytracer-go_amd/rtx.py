@@ -23,6 +23,7 @@ RTX_ERR_OOM = -6
 
 RTX_PRIM_SPHERE = 0
 RTX_PRIM_QUAD = 1
+RTX_PRIM_LIST = 2  # a World nested in the tree (ABI 5)
 RTX_MAT_LAMBERTIAN, RTX_MAT_METAL, RTX_MAT_DIELECTRIC, RTX_MAT_DIFFUSE_LIGHT = 0, 1, 2, 3
 RTX_TEX_SOLID, RTX_TEX_CHECKERED, RTX_TEX_IMAGE, RTX_TEX_NOISE = 0, 1, 2, 3
 RTX_FLAG_COUNTERS = 1
@@ -64,12 +65,18 @@ class Texture(ctypes.Structure):
                 ("even", c_float * 3), ("texel_offset", c_uint32), ("odd", c_float * 3), ("pad", c_float)]
 
 
+class List(ctypes.Structure):  # rtx_list (ABI 5): a World nested in the tree
+    _fields_ = [("first", c_uint32), ("count", c_uint32)]
+
+
 class SceneDesc(ctypes.Structure):
     _fields_ = [("nodes", POINTER(BvhNode)), ("n_nodes", c_uint32), ("n_roots", c_uint32),
                 ("roots", POINTER(c_int32)), ("spheres", POINTER(Sphere)), ("n_spheres", c_uint32),
                 ("n_quads", c_uint32), ("quads", POINTER(Quad)), ("materials", POINTER(Material)),
                 ("n_materials", c_uint32), ("n_textures", c_uint32), ("textures", POINTER(Texture)),
-                ("texels", POINTER(c_uint32)), ("n_texels", c_uint64)]
+                ("texels", POINTER(c_uint32)), ("n_texels", c_uint64),
+                ("lists", POINTER(List)), ("n_lists", c_uint32), ("n_list_refs", c_uint32),
+                ("list_refs", POINTER(c_int32))]
 
 
 class Camera(ctypes.Structure):

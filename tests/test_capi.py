@@ -34,7 +34,7 @@ def test_binding_lists_match_headers(built):
 
 def test_version_and_build_info(built):
     L = rtx.load()
-    assert L.rtx_version() == 4
+    assert L.rtx_version() == 5
     assert b"gfx950" in L.rtx_build_info()
 
 
@@ -43,7 +43,7 @@ def test_struct_layout_matches_header(built, tmp_path):
     import subprocess
 
     structs = {"rtx_bvh_node": rtx.BvhNode, "rtx_sphere": rtx.Sphere, "rtx_quad": rtx.Quad,
-               "rtx_material": rtx.Material, "rtx_texture": rtx.Texture, "rtx_scene_desc": rtx.SceneDesc,
+               "rtx_material": rtx.Material, "rtx_texture": rtx.Texture, "rtx_scene_desc": rtx.SceneDesc, "rtx_list": rtx.List,
                "rtx_camera": rtx.Camera, "rtx_region": rtx.Region, "rtx_stats": rtx.Stats}
     src = tmp_path / "sizes.c"
     src.write_text('#include <stdio.h>\n#include "rtx.h"\nint main(void){\n' +
