@@ -991,8 +991,13 @@ __device__ __forceinline__ uint32_t trav_step_batched(Trav& t, const Ray& r, con
 // (b.z) BEFORE the test, so the LDS round trip runs under the ~60 instructions of the sphere test.
 // Lanes of the other kind, and lanes parked on the sentinel, keep their entry: no re-read.  Every
 // step starts with s_waitcnt; the phase starts with one read for all lanes and ends with a wait.
-#define RTX_WALK_STEP_PF(K)                                                  \
-        "s_waitcnt lgkmcnt(0)\n\t"                                           \
+// Entry read of the prefetching walk, under the current exec: both halves from the fixed layout.
+#define RTX_LOAD_LDS                                                         \
+        "ds_read_b128 v[0:3], %[pos]\n\t"                                    \
+        "ds_read_b128 v[4:7], %[pos] offset:32768\n\t" /* LDS_B */
+#define RTX_WAIT_LDS "s_waitcnt lgkmcnt(0)\n\t"
+#define RTX_WALK_STEP_PF(K, LOAD, WAIT)                                      \
+        WAIT                                                                 \
         "v_cmp_gt_i32_e64 %[pm], -1, v7\n\t"                                 \
         "v_cmp_lt_u32_e64 %[wm], %[pos], %[end]\n\t"                         \
         "s_andn2_b64 %[wm], %[wm], %[pm]\n\t"                                \
@@ -1024,8 +1029,7 @@ __device__ __forceinline__ uint32_t trav_step_batched(Trav& t, const Ray& r, con
         "v_cmp_lt_f32_e32 vcc, v8, v9\n\t"                                   \
         "s_nop 1\n\t"                                                        \
         "v_cndmask_b32_e32 %[pos], v3, v7, vcc\n\t"                          \
-        "ds_read_b128 v[0:3], %[pos]\n\t"                                    \
-        "ds_read_b128 v[4:7], %[pos] offset:32768\n\t" /* LDS_B */          \
+        LOAD                                                                 \
         "s_mov_b64 exec, %[save]\n\t"                                        \
         "s_branch LE%=_" #K "\n"                                             \
         /* ---- sphere tests on the primitive lanes, successor read first */ \
@@ -1038,8 +1042,7 @@ __device__ __forceinline__ uint32_t trav_step_batched(Trav& t, const Ray& r, con
         "v_mov_b32 v13, v4\n\t"        /* r^2 */                             \
         "v_lshrrev_b32_e32 v14, 4, %[pos]\n\t" /* this entry's index */      \
         "v_mov_b32 %[pos], v6\n\t"     /* successor */                       \
-        "ds_read_b128 v[0:3], %[pos]\n\t"                                    \
-        "ds_read_b128 v[4:7], %[pos] offset:32768\n\t"                       \
+        LOAD                                                                 \
         "v_mul_f32 v8, %[dx], v10\n\t" /* hb = d.oc */                       \
         "v_mul_f32 v9, %[dy], v11\n\t"                                       \
         "v_add_f32 v8, v8, v9\n\t"                                           \
@@ -1115,53 +1118,62 @@ __device__ __forceinline__ uint32_t trav_step_batched(Trav& t, const Ray& r, con
 #ifndef RTX_WALK_PREFETCH
 #define RTX_WALK_PREFETCH 1
 #endif
-#if RTX_WALK_PREFETCH
-#define RTX_WALK_STEP RTX_WALK_STEP_PF
-#define RTX_WALK_BEGIN "ds_read_b128 v[0:3], %[pos]\n\tds_read_b128 v[4:7], %[pos] offset:32768\n"
-#define RTX_WALK_END "\n\ts_waitcnt lgkmcnt(0)"
-#else
-#define RTX_WALK_STEP RTX_WALK_STEP_ASM
-#define RTX_WALK_BEGIN ""
-#define RTX_WALK_END ""
-#endif
 // The whole traversal phase (traverse_loop's !COUNT body for this case): six asm steps, then the
 // vote — at_end = pos >= end, walking lanes W, waiting lanes P0 — until no lane walks or at
 // least `thresh` wait; returns the final at_end mask.  Positions only increase along a walk, so
 // every lane reaches the sentinel and the loop ends.
+#define RTX_WALK_VOTE                                                        \
+        "v_cmp_ge_u32_e64 %[pm], %[pos], %[end]\n\t"                         \
+        "s_andn2_b64 %[l1], %[W], %[pm]\n\t" /* still walking */             \
+        "s_cmp_eq_u64 %[l1], 0\n\t"                                          \
+        "s_cbranch_scc1 LX%=\n\t"                                            \
+        "s_and_b64 %[l1], %[W], %[pm]\n\t"                                   \
+        "s_or_b64 %[l1], %[l1], %[P0]\n\t" /* waiting to shade */            \
+        "s_bcnt1_i32_b64 %[cnt], %[l1]\n\t"                                  \
+        "s_cmp_lt_u32 %[cnt], %[thresh]\n\t"                                 \
+        "s_cbranch_scc1 LW%=\n"                                               \
+        "LX%=:"
+#define RTX_WALK_OUTS                                                                                        \
+    [pos] "+v"(t.i), [cl] "+v"(t.closest), [hit] "+v"(t.hit), [pm] "=&s"(pm), [wm] "=&s"(wm),              \
+        [save] "=&s"(save), [g1] "=&s"(g1), [l1] "=&s"(l1), [l2] "=&s"(l2), [cnt] "=&s"(cnt)
+#define RTX_WALK_INS                                                                                         \
+    [ox] "v"(r.o.x), [oy] "v"(r.o.y), [oz] "v"(r.o.z), [dx] "v"(r.d.x), [dy] "v"(r.d.y), [dz] "v"(r.d.z),  \
+        [ix] "v"(t.ix), [iy] "v"(t.iy), [iz] "v"(t.iz), [a] "v"(t.a), [ra] "v"(t.ra), [end] "s"(end),      \
+        [kmin] "s"(kmin), [tmin] "s"(tmin), [W] "s"(W), [P0] "s"(P0), [thresh] "s"(thresh)
+#define RTX_WALK_CLOBBERS                                                                                    \
+    "v0", "v1", "v2", "v3", "v4", "v5", "v6", "v7", "v8", "v9", "v10", "v11", "v12", "v13", "v14", "v15",    \
+        "v16", "vcc", "scc"
 __device__ __forceinline__ uint64_t walk_phase_asm(Trav& t, const Ray& r, uint32_t end, uint32_t kmin, float tmin,
                                                    uint64_t W, uint64_t P0, uint32_t thresh) {
     static_assert(LDS_B == 32768, "the asm reads the 'b' halves at offset:32768");
     uint64_t pm, wm, save, g1, l1, l2;
     uint32_t cnt;
-    asm volatile(RTX_WALK_BEGIN
-                 "LW%=:\n\t"
-                 RTX_WALK_STEP(0) RTX_WALK_STEP(1) RTX_WALK_STEP(2) RTX_WALK_STEP(3) RTX_WALK_STEP(4)
-                 RTX_WALK_STEP(5)
-                 "v_cmp_ge_u32_e64 %[pm], %[pos], %[end]\n\t"
-                 "s_andn2_b64 %[l1], %[W], %[pm]\n\t"  // still walking
-                 "s_cmp_eq_u64 %[l1], 0\n\t"
-                 "s_cbranch_scc1 LX%=\n\t"
-                 "s_and_b64 %[l1], %[W], %[pm]\n\t"
-                 "s_or_b64 %[l1], %[l1], %[P0]\n\t"  // waiting to shade
-                 "s_bcnt1_i32_b64 %[cnt], %[l1]\n\t"
-                 "s_cmp_lt_u32 %[cnt], %[thresh]\n\t"
-                 "s_cbranch_scc1 LW%=\n"
-                 "LX%=:" RTX_WALK_END
-                 : [pos] "+v"(t.i), [cl] "+v"(t.closest), [hit] "+v"(t.hit), [pm] "=&s"(pm), [wm] "=&s"(wm),
-                   [save] "=&s"(save), [g1] "=&s"(g1), [l1] "=&s"(l1), [l2] "=&s"(l2), [cnt] "=&s"(cnt)
-                 : [ox] "v"(r.o.x), [oy] "v"(r.o.y), [oz] "v"(r.o.z), [dx] "v"(r.d.x), [dy] "v"(r.d.y),
-                   [dz] "v"(r.d.z), [ix] "v"(t.ix), [iy] "v"(t.iy), [iz] "v"(t.iz), [a] "v"(t.a), [ra] "v"(t.ra),
-                   [end] "s"(end), [kmin] "s"(kmin), [tmin] "s"(tmin), [W] "s"(W), [P0] "s"(P0),
-                   [thresh] "s"(thresh)
-                 : "v0", "v1", "v2", "v3", "v4", "v5", "v6", "v7", "v8", "v9", "v10", "v11", "v12", "v13", "v14",
-                   "v15", "v16", "vcc", "scc");
+    if constexpr (RTX_WALK_PREFETCH) {
+#define S(K) RTX_WALK_STEP_PF(K, RTX_LOAD_LDS, RTX_WAIT_LDS)
+        asm volatile(RTX_LOAD_LDS "\nLW%=:\n\t" S(0) S(1) S(2) S(3) S(4) S(5) RTX_WALK_VOTE
+                     "\n\ts_waitcnt lgkmcnt(0)"
+                     : RTX_WALK_OUTS
+                     : RTX_WALK_INS
+                     : RTX_WALK_CLOBBERS);
+#undef S
+    } else {
+#define S(K) RTX_WALK_STEP_ASM(K)
+        asm volatile("LW%=:\n\t" S(0) S(1) S(2) S(3) S(4) S(5) RTX_WALK_VOTE
+                     : RTX_WALK_OUTS
+                     : RTX_WALK_INS
+                     : RTX_WALK_CLOBBERS);
+#undef S
+    }
     return pm;  // at_end
 }
 #undef RTX_WALK_STEP_ASM
 #undef RTX_WALK_STEP_PF
-#undef RTX_WALK_STEP
-#undef RTX_WALK_BEGIN
-#undef RTX_WALK_END
+#undef RTX_LOAD_LDS
+#undef RTX_WAIT_LDS
+#undef RTX_WALK_VOTE
+#undef RTX_WALK_OUTS
+#undef RTX_WALK_INS
+#undef RTX_WALK_CLOBBERS
 
 // Shade the result of segment `seg` (ray.go:36-53, materials.go:33-113).  Returns true
 // when the path ends, with its colour in `color`; otherwise r / thr hold the next
