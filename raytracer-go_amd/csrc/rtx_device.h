@@ -46,8 +46,21 @@ __device__ __forceinline__ float rcp_ieee(float x) {
     if (__builtin_amdgcn_ballot_w64(!rcp_fast_ok(x)) == 0) return rcp_newton(x);
     return 1.0f / x;
 }
+// sqrt(x) correctly rounded, as the compiler expands an f32 sqrt: v_sqrt, then the neighbour
+// whose fma residual changes sign.  The expansion's 2^32 pre-scaling is needed only below 2^-96,
+// so it runs (the builtin) only when a lane of the wave has 0 <= x < 2^-96; its +-0 / +inf
+// pass-through is left out: v_sqrt returns those exactly and both residuals then keep them.
+__device__ __forceinline__ float sqrt_rn(float x) {
+    if (__builtin_amdgcn_ballot_w64(x < 0x1p-96f && x >= 0.0f) != 0) return __builtin_sqrtf(x);
+    float s = __builtin_amdgcn_sqrtf(x);
+    const float sp = __uint_as_float(__float_as_uint(s) - 1u), sn = __uint_as_float(__float_as_uint(s) + 1u);
+    const float rp = __builtin_fmaf(-sp, s, x), rn = __builtin_fmaf(-sn, s, x);
+    if (rp <= 0.0f) s = sp;
+    if (rn > 0.0f) s = sn;
+    return s;
+}
 __device__ __forceinline__ V3 unit(V3 v) {                                                         // vec3.go:103-113
-    float l = __builtin_sqrtf(lensq(v));
+    float l = sqrt_rn(lensq(v));
     return scale(v, rcp_ieee(l));
 }
 __device__ __forceinline__ bool near_zero(V3 v) {                                                  // vec3.go:170-172
@@ -57,7 +70,7 @@ __device__ __forceinline__ V3 reflect(V3 v, V3 n) { return sub(v, scale(n, 2.0f 
 __device__ __forceinline__ V3 refract(V3 uv, V3 n, float eta) {                                    // vec3.go:216-221
     float cos_t = dot(scale(uv, -1.0f), n);
     V3 perp = scale(add(uv, scale(n, cos_t)), eta);
-    float s = __builtin_sqrtf(__builtin_fabsf(1.0f - lensq(perp)));  // f64 sqrt of an f32, rounded back
+    float s = sqrt_rn(__builtin_fabsf(1.0f - lensq(perp)));  // f64 sqrt of an f32, rounded back
     V3 par = scale(n, -1.0f * s);
     return add(par, perp);
 }
@@ -551,13 +564,17 @@ __device__ __forceinline__ Scatter coop_scatter(const Params& p, const SceneRef 
     const uint64_t below_mask = (1ull << lane) - 1ull;
     for (uint32_t base = 1; pend != 0;) {
         const uint32_t np = (uint32_t)__popcll(pend);
-        const uint32_t K = 64u / np;  // attempts per owner this round
+        // K = 64 / np attempts per owner this round, and q = lane / K below, by float reciprocals:
+        // 64.5 / np and (lane + 0.5) / K lie at least 1/128 from the next integer, far beyond
+        // v_rcp_f32's 1-ulp error, so truncation gives the integer quotients (the compiler's
+        // integer divisions took ~25 VALU per round).
+        const uint32_t K = __builtin_amdgcn_readfirstlane((uint32_t)(64.5f * __builtin_amdgcn_rcpf((float)np)));
         const bool mine = (pend >> lane) & 1ull;
         const uint32_t below = (uint32_t)__popcll(pend & below_mask);
         // Lane q (< np) learns the lane id of the q-th pending lane (a permutation push).
         const uint32_t dst = mine ? below : np + (lane - below);
         const uint32_t owner_of = (uint32_t)__builtin_amdgcn_ds_permute((int)(dst * 4u), (int)lane);
-        const uint32_t q = lane / K, k = lane - q * K;
+        const uint32_t q = (uint32_t)(((float)lane + 0.5f) * __builtin_amdgcn_rcpf((float)K)), k = lane - q * K;
         const bool slot = q < np;
         const uint32_t owner = lane_pull(slot ? q : 0u, owner_of);
         const uint32_t opix = lane_pull(owner, rng.pixel), osmp = lane_pull(owner, rng.sample);
