@@ -410,9 +410,14 @@ int upload_copy(rtx_scene* s, DeviceCopy& c) {
         HIP_TRY(hipMalloc(&c.materials, std::max<size_t>(1, dm.size()) * sizeof(rtx_material)));
         if (!dm.empty()) HIP_TRY(hipMemcpy(c.materials, dm.data(), dm.size() * sizeof(rtx_material), hipMemcpyHostToDevice));
     }
-    HIP_TRY(hipMalloc(&c.textures, std::max<size_t>(1, s->textures.size()) * sizeof(rtx_texture)));
-    if (!s->textures.empty())
-        HIP_TRY(hipMemcpy(c.textures, s->textures.data(), s->textures.size() * sizeof(rtx_texture), hipMemcpyHostToDevice));
+    {  // device textures: a Checkered carries invScale = float32(1 / scale) (materials.go:128) in `pad`,
+       // the IEEE quotient computed once here instead of per lookup
+        std::vector<rtx_texture> dt(s->textures);
+        for (rtx_texture& t : dt)
+            if (t.type == RTX_TEX_CHECKERED) t.pad = 1.0f / t.scale;
+        HIP_TRY(hipMalloc(&c.textures, std::max<size_t>(1, dt.size()) * sizeof(rtx_texture)));
+        if (!dt.empty()) HIP_TRY(hipMemcpy(c.textures, dt.data(), dt.size() * sizeof(rtx_texture), hipMemcpyHostToDevice));
+    }
     HIP_TRY(hipMalloc(&c.texels, std::max<size_t>(1, s->texels.size()) * sizeof(uint32_t)));
     if (!s->texels.empty())
         HIP_TRY(hipMemcpy(c.texels, s->texels.data(), s->texels.size() * sizeof(uint32_t), hipMemcpyHostToDevice));

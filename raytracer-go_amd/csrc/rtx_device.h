@@ -495,11 +495,18 @@ __device__ __forceinline__ V3 texture_value(const Params& p, uint32_t ti, float 
     const rtx_texture& t = p.textures[ti];
     if (t.type == RTX_TEX_SOLID) return v3(t.even[0], t.even[1], t.even[2]);
     if (t.type == RTX_TEX_CHECKERED) {
-        const float inv = 1.0f / t.scale;
-        const int64_t x = (int64_t)__builtin_floorf(inv * pt.x);
-        const int64_t y = (int64_t)__builtin_floorf(inv * pt.y);
-        const int64_t z = (int64_t)__builtin_floorf(inv * pt.z);
-        return ((x + y + z) & 1) == 0 ? v3(t.even[0], t.even[1], t.even[2]) : v3(t.odd[0], t.odd[1], t.odd[2]);
+        const float inv = t.pad;  // float32(1 / scale), materials.go:128 (computed on the host, upload_copy)
+        const float fx = __builtin_floorf(inv * pt.x), fy = __builtin_floorf(inv * pt.y), fz = __builtin_floorf(inv * pt.z);
+        bool odd;
+        // int(math.Floor(...)) is an int64; only the parity of x + y + z matters, so when every lane's
+        // floors are below 2^31 in magnitude 32-bit conversions (wrapping sums keep the parity) do it
+        if (__builtin_amdgcn_ballot_w64(!(__builtin_fabsf(fx) < 0x1p31f && __builtin_fabsf(fy) < 0x1p31f &&
+                                          __builtin_fabsf(fz) < 0x1p31f)) == 0) {
+            odd = (((uint32_t)(int32_t)fx + (uint32_t)(int32_t)fy + (uint32_t)(int32_t)fz) & 1u) != 0;
+        } else {
+            odd = (((int64_t)fx + (int64_t)fy + (int64_t)fz) & 1) != 0;
+        }
+        return !odd ? v3(t.even[0], t.even[1], t.even[2]) : v3(t.odd[0], t.odd[1], t.odd[2]);
     }
     if (NOISE && t.type == RTX_TEX_NOISE) {
         const float g = noise_texture(p.texels + t.texel_offset, t.scale, pt.x, pt.y, pt.z);

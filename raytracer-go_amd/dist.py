@@ -38,8 +38,8 @@ def gather_image(shard, height: int, rank: int, world: int, dist=None):
     import torch
 
     if rank == 0:
-        bufs = [torch.empty_like(shard) for _ in range(world)]
-        dist.gather(shard, gather_list=bufs, dst=0)
-        return deinterleave(torch.stack(bufs), height)
+        stacked = torch.empty((world,) + tuple(shard.shape), dtype=shard.dtype, device=shard.device)
+        dist.gather(shard, gather_list=list(stacked.unbind(0)), dst=0)  # straight into one buffer
+        return deinterleave(stacked, height)
     dist.gather(shard, gather_list=None, dst=0)
     return None
