@@ -891,130 +891,6 @@ __device__ __forceinline__ uint32_t trav_step_batched(Trav& t, const Ray& r, con
 //     the first root when tmin < t1, else the second (hittables.go:110-114); disc >= 0.
 // gfx950 hazards: a VALU-written SGPR/VCC read as a v_cndmask mask by the next VALU needs
 // s_nop 1; a v_sqrt result read by the next VALU needs s_nop 0 (as the compiler emits them).
-#define RTX_WALK_STEP_ASM(K)                                                 \
-        "ds_read_b128 v[0:3], %[pos]\n\t"                                    \
-        "ds_read_b128 v[4:7], %[pos] offset:32768\n\t" /* LDS_B */          \
-        "s_waitcnt lgkmcnt(0)\n\t"                                           \
-        "v_cmp_gt_i32_e64 %[pm], -1, v7\n\t"                                 \
-        "v_cmp_lt_u32_e64 %[wm], %[pos], %[end]\n\t"                         \
-        "s_andn2_b64 %[wm], %[wm], %[pm]\n\t"                                \
-        "s_bcnt1_i32_b64 %[cnt], %[pm]\n\t"                                  \
-        "s_cmp_ge_u32 %[cnt], %[kmin]\n\t"                                   \
-        "s_cbranch_scc1 LP%=_" #K "\n\t"                                     \
-        "s_cmp_eq_u64 %[wm], 0\n\t"                                          \
-        "s_cbranch_scc1 LP%=_" #K "\n\t"                                     \
-        /* ---- box tests on the node lanes */                               \
-        "s_and_saveexec_b64 %[save], %[wm]\n\t"                              \
-        "v_sub_f32 v0, v0, %[ox]\n\t"                                        \
-        "v_sub_f32 v4, v4, %[ox]\n\t"                                        \
-        "v_sub_f32 v1, v1, %[oy]\n\t"                                        \
-        "v_sub_f32 v5, v5, %[oy]\n\t"                                        \
-        "v_mul_f32 v0, v0, %[ix]\n\t"                                        \
-        "v_mul_f32 v4, v4, %[ix]\n\t"                                        \
-        "v_sub_f32 v2, v2, %[oz]\n\t"                                        \
-        "v_sub_f32 v6, v6, %[oz]\n\t"                                        \
-        "v_mul_f32 v1, v1, %[iy]\n\t"                                        \
-        "v_mul_f32 v5, v5, %[iy]\n\t"                                        \
-        "v_med3_f32 v8, %[tmin], v0, v4\n\t"                                 \
-        "v_med3_f32 v9, %[cl], v0, v4\n\t"                                   \
-        "v_mul_f32 v2, v2, %[iz]\n\t"                                        \
-        "v_mul_f32 v6, v6, %[iz]\n\t"                                        \
-        "v_med3_f32 v8, v8, v1, v5\n\t"                                      \
-        "v_med3_f32 v9, v9, v1, v5\n\t"                                      \
-        "v_med3_f32 v8, v8, v2, v6\n\t"                                      \
-        "v_med3_f32 v9, v9, v2, v6\n\t"                                      \
-        "v_cmp_lt_f32_e32 vcc, v8, v9\n\t"                                   \
-        "s_nop 1\n\t"                                                        \
-        "v_cndmask_b32_e32 %[pos], v3, v7, vcc\n\t"                          \
-        "s_mov_b64 exec, %[save]\n\t"                                        \
-        "s_branch LE%=_" #K "\n"                                             \
-        /* ---- sphere tests on the primitive lanes */                       \
-        "LP%=_" #K ":\n\t"                                                   \
-        "s_and_saveexec_b64 %[save], %[pm]\n\t"                              \
-        "s_cbranch_execz LR%=_" #K "\n\t"                                    \
-        "v_sub_f32 v0, %[ox], v0\n\t" /* oc = o - center */                  \
-        "v_sub_f32 v1, %[oy], v1\n\t"                                        \
-        "v_sub_f32 v2, %[oz], v2\n\t"                                        \
-        "v_mul_f32 v8, %[dx], v0\n\t" /* hb = d.oc */                        \
-        "v_mul_f32 v9, %[dy], v1\n\t"                                        \
-        "v_add_f32 v8, v8, v9\n\t"                                           \
-        "v_mul_f32 v9, %[dz], v2\n\t"                                        \
-        "v_add_f32 v8, v8, v9\n\t"                                           \
-        "v_mul_f32 v0, v0, v0\n\t" /* c = |oc|^2 - r^2 */                    \
-        "v_mul_f32 v1, v1, v1\n\t"                                           \
-        "v_add_f32 v0, v0, v1\n\t"                                           \
-        "v_mul_f32 v2, v2, v2\n\t"                                           \
-        "v_add_f32 v0, v0, v2\n\t"                                           \
-        "v_sub_f32 v0, v0, v4\n\t"                                           \
-        "v_mul_f32 v0, %[a], v0\n\t" /* disc = hb*hb - a*c */                \
-        "v_mul_f32 v9, v8, v8\n\t"                                           \
-        "v_sub_f32 v0, v9, v0\n\t"                                           \
-        "v_cmp_le_f32_e64 %[pm], 0, v0\n\t"                                 \
-        "v_cmp_gt_f32_e32 vcc, 0xf800000, v0\n\t" /* x < 2^-96 */            \
-        "s_and_b64 %[g1], vcc, %[pm]\n\t"                                   \
-        "s_cbranch_scc1 LS%=_" #K "\n\t"                                     \
-        "v_sqrt_f32_e32 v2, v0\n\t" /* every lane: x >= 2^-96 or x < 0 */    \
-        "s_nop 0\n\t"                                                        \
-        "v_add_u32_e32 v9, -1, v2\n\t"                                       \
-        "v_add_u32_e32 v3, 1, v2\n\t"                                        \
-        "v_fma_f32 v5, -v9, v2, v0\n\t"                                      \
-        "v_fma_f32 v7, -v3, v2, v0\n\t"                                      \
-        "v_cmp_ge_f32_e64 %[g1], 0, v5\n\t"                                  \
-        "s_nop 1\n\t"                                                        \
-        "v_cndmask_b32_e64 v2, v2, v9, %[g1]\n\t"                            \
-        "v_cmp_lt_f32_e64 %[g1], 0, v7\n\t"                                  \
-        "s_nop 1\n\t"                                                        \
-        "v_cndmask_b32_e64 v2, v2, v3, %[g1]\n\t"                            \
-        "s_branch LQ%=_" #K "\n"                                             \
-        "LS%=_" #K ":\n\t" /* some lane: 0 <= x < 2^-96, scaled by 2^32 */   \
-        "v_mul_f32 v1, 0x4f800000, v0\n\t"                                   \
-        "v_cndmask_b32_e32 v1, v0, v1, vcc\n\t"                              \
-        "v_sqrt_f32_e32 v2, v1\n\t"                                          \
-        "s_nop 0\n\t"                                                        \
-        "v_add_u32_e32 v9, -1, v2\n\t"                                       \
-        "v_add_u32_e32 v3, 1, v2\n\t"                                        \
-        "v_fma_f32 v5, -v9, v2, v1\n\t"                                      \
-        "v_fma_f32 v7, -v3, v2, v1\n\t"                                      \
-        "v_cmp_ge_f32_e64 %[g1], 0, v5\n\t"                                  \
-        "s_nop 1\n\t"                                                        \
-        "v_cndmask_b32_e64 v2, v2, v9, %[g1]\n\t"                            \
-        "v_cmp_lt_f32_e64 %[g1], 0, v7\n\t"                                  \
-        "s_nop 1\n\t"                                                        \
-        "v_cndmask_b32_e64 v2, v2, v3, %[g1]\n\t"                            \
-        "v_mul_f32 v9, 0x37800000, v2\n\t" /* x 2^-16 when scaled */         \
-        "v_cndmask_b32_e32 v2, v2, v9, vcc\n"                                \
-        "LQ%=_" #K ":\n\t" /* v2 = sqrt(disc) */                             \
-        "v_sub_f32_e64 v1, -v8, v2\n\t" /* -hb - sq */                       \
-        "v_add_f32_e64 v3, -v8, v2\n\t" /* -hb + sq */                       \
-        "v_mul_f32 v5, v1, %[ra]\n\t"   /* div_by: q0 = n y */               \
-        "v_mul_f32 v7, v3, %[ra]\n\t"                                        \
-        "v_fma_f32 v1, -%[a], v5, v1\n\t" /* e = n - a q0 */                 \
-        "v_fma_f32 v3, -%[a], v7, v3\n\t"                                    \
-        "v_fmac_f32 v5, v1, %[ra]\n\t" /* t1 = q0 + e y */                   \
-        "v_fmac_f32 v7, v3, %[ra]\n\t" /* t2 */                              \
-        "v_cmp_lt_f32_e64 %[g1], %[tmin], v5\n\t"                            \
-        "v_cmp_lt_f32_e64 %[l1], v5, %[cl]\n\t"                              \
-        "v_cmp_lt_f32_e64 %[l2], %[tmin], v7\n\t"                            \
-        "s_and_b64 %[l1], %[l1], %[g1]\n\t"                                  \
-        "s_andn2_b64 %[l2], %[l2], %[g1]\n\t"                                \
-        "v_cmp_lt_f32_e64 %[wm], v7, %[cl]\n\t"                              \
-        "s_and_b64 %[l2], %[l2], %[wm]\n\t"                                  \
-        "s_or_b64 %[l1], %[l1], %[l2]\n\t"                                   \
-        "s_and_b64 %[l1], %[l1], %[pm]\n\t"                                 \
-        "v_cndmask_b32_e64 v7, v7, v5, %[g1]\n\t"                            \
-        "v_lshrrev_b32_e32 v1, 4, %[pos]\n\t"                                \
-        "v_cndmask_b32_e64 %[cl], %[cl], v7, %[l1]\n\t"                      \
-        "v_cndmask_b32_e64 %[hit], %[hit], v1, %[l1]\n\t"                    \
-        "v_mov_b32_e32 %[pos], v6\n"                                         \
-        "LR%=_" #K ":\n\t"                                                   \
-        "s_mov_b64 exec, %[save]\n"                                          \
-        "LE%=_" #K ":\n\t"
-// RTX_WALK_PREFETCH (default): the lane's entry stays in v0-v7 from one step to the next.  A box
-// step reads the node lanes' next entries at its end; a sphere step moves what its test needs
-// (centre, r^2, the entry index) to v10-v14 and issues the read of each primitive lane's successor
-// (b.z) BEFORE the test, so the LDS round trip runs under the ~60 instructions of the sphere test.
-// Lanes of the other kind, and lanes parked on the sentinel, keep their entry: no re-read.  Every
-// step starts with s_waitcnt; the phase starts with one read for all lanes and ends with a wait.
 // Entry read of the prefetching walk, under the current exec: both halves from the fixed layout.
 #define RTX_LOAD_LDS                                                         \
         "ds_read_b128 v[0:3], %[pos]\n\t"                                    \
@@ -1139,9 +1015,215 @@ __device__ __forceinline__ uint32_t trav_step_batched(Trav& t, const Ray& r, con
         "LR%=_" #K ":\n\t"                                                   \
         "s_mov_b64 exec, %[save]\n"                                          \
         "LE%=_" #K ":\n\t"
-#ifndef RTX_WALK_PREFETCH
-#define RTX_WALK_PREFETCH 1
-#endif
+#define RTX_WALK_STEP_PFQ(K, LOAD, WAIT)                                     \
+        WAIT                                                                 \
+        "v_cmp_gt_i32_e64 %[pm], -1, v7\n\t"                                 \
+        "v_cmp_lt_u32_e64 %[wm], %[pos], %[end]\n\t"                         \
+        "s_andn2_b64 %[wm], %[wm], %[pm]\n\t"                                \
+        "s_bcnt1_i32_b64 %[cnt], %[pm]\n\t"                                  \
+        "s_cmp_ge_u32 %[cnt], %[kmin]\n\t"                                   \
+        "s_cbranch_scc1 LP%=_" #K "\n\t"                                     \
+        "s_cmp_eq_u64 %[wm], 0\n\t"                                          \
+        "s_cbranch_scc1 LP%=_" #K "\n\t"                                     \
+        /* ---- box tests on the node lanes, then their next entries */      \
+        "s_and_saveexec_b64 %[save], %[wm]\n\t"                              \
+        "v_sub_f32 v0, v0, %[ox]\n\t"                                        \
+        "v_sub_f32 v4, v4, %[ox]\n\t"                                        \
+        "v_sub_f32 v1, v1, %[oy]\n\t"                                        \
+        "v_sub_f32 v5, v5, %[oy]\n\t"                                        \
+        "v_mul_f32 v0, v0, %[ix]\n\t"                                        \
+        "v_mul_f32 v4, v4, %[ix]\n\t"                                        \
+        "v_sub_f32 v2, v2, %[oz]\n\t"                                        \
+        "v_sub_f32 v6, v6, %[oz]\n\t"                                        \
+        "v_mul_f32 v1, v1, %[iy]\n\t"                                        \
+        "v_mul_f32 v5, v5, %[iy]\n\t"                                        \
+        "v_med3_f32 v8, %[tmin], v0, v4\n\t"                                 \
+        "v_med3_f32 v9, %[cl], v0, v4\n\t"                                   \
+        "v_mul_f32 v2, v2, %[iz]\n\t"                                        \
+        "v_mul_f32 v6, v6, %[iz]\n\t"                                        \
+        "v_med3_f32 v8, v8, v1, v5\n\t"                                      \
+        "v_med3_f32 v9, v9, v1, v5\n\t"                                      \
+        "v_med3_f32 v8, v8, v2, v6\n\t"                                      \
+        "v_med3_f32 v9, v9, v2, v6\n\t"                                      \
+        "v_cmp_lt_f32_e32 vcc, v8, v9\n\t"                                   \
+        "s_nop 1\n\t"                                                        \
+        "v_cndmask_b32_e32 %[pos], v3, v7, vcc\n\t"                          \
+        LOAD                                                                 \
+        "s_mov_b64 exec, %[save]\n\t"                                        \
+        "s_branch LE%=_" #K "\n"                                             \
+        /* ---- sphere tests on the primitive lanes, successor read first */ \
+        "LP%=_" #K ":\n\t"                                                   \
+        "s_and_saveexec_b64 %[save], %[pm]\n\t"                              \
+        "s_cbranch_execz LR%=_" #K "\n\t"                                    \
+        "v_mov_b32 v10, v0\n\t" /* centre / normal */                        \
+        "v_mov_b32 v11, v1\n\t"                                              \
+        "v_mov_b32 v12, v2\n\t"                                              \
+        "v_mov_b32 v19, v3\n\t" /* quad: D */                                \
+        "v_mov_b32 v13, v4\n\t" /* r^2 / quad index */                       \
+        "v_mov_b32 v18, v7\n\t" /* tag */                                    \
+        "v_lshrrev_b32_e32 v14, 4, %[pos]\n\t" /* this entry's index */      \
+        "v_mov_b32 %[pos], v6\n\t" /* successor */                           \
+        LOAD                                                                 \
+        "v_cmp_gt_i32_e64 %[qs], -2, v18\n\t" /* sphere: tag < -2 */         \
+        "s_and_saveexec_b64 %[qm], %[qs]\n\t"                                \
+        "s_cbranch_execz LT%=_" #K "\n\t"                                    \
+        "v_sub_f32 v10, %[ox], v10\n\t" /* oc = o - center */                \
+        "v_sub_f32 v11, %[oy], v11\n\t"                                      \
+        "v_sub_f32 v12, %[oz], v12\n\t"                                      \
+        "v_mul_f32 v8, %[dx], v10\n\t" /* hb = d.oc */                       \
+        "v_mul_f32 v9, %[dy], v11\n\t"                                       \
+        "v_add_f32 v8, v8, v9\n\t"                                           \
+        "v_mul_f32 v9, %[dz], v12\n\t"                                       \
+        "v_add_f32 v8, v8, v9\n\t"                                           \
+        "v_mul_f32 v10, v10, v10\n\t" /* c = |oc|^2 - r^2 */                 \
+        "v_mul_f32 v11, v11, v11\n\t"                                        \
+        "v_add_f32 v10, v10, v11\n\t"                                        \
+        "v_mul_f32 v12, v12, v12\n\t"                                        \
+        "v_add_f32 v10, v10, v12\n\t"                                        \
+        "v_sub_f32 v10, v10, v13\n\t"                                        \
+        "v_mul_f32 v10, %[a], v10\n\t" /* disc = hb*hb - a*c */              \
+        "v_mul_f32 v9, v8, v8\n\t"                                           \
+        "v_sub_f32 v10, v9, v10\n\t"                                         \
+        "v_cmp_le_f32_e64 %[pm], 0, v10\n\t"                                 \
+        "v_cmp_gt_f32_e32 vcc, 0xf800000, v10\n\t" /* x < 2^-96 */           \
+        "s_and_b64 %[g1], vcc, %[pm]\n\t"                                    \
+        "s_cbranch_scc1 LS%=_" #K "\n\t"                                     \
+        "v_sqrt_f32_e32 v12, v10\n\t" /* every lane: x >= 2^-96 or x < 0 */  \
+        "s_nop 0\n\t"                                                        \
+        "v_add_u32_e32 v9, -1, v12\n\t"                                      \
+        "v_add_u32_e32 v11, 1, v12\n\t"                                      \
+        "v_fma_f32 v13, -v9, v12, v10\n\t"                                   \
+        "v_fma_f32 v15, -v11, v12, v10\n\t"                                  \
+        "v_cmp_ge_f32_e64 %[g1], 0, v13\n\t"                                 \
+        "s_nop 1\n\t"                                                        \
+        "v_cndmask_b32_e64 v12, v12, v9, %[g1]\n\t"                          \
+        "v_cmp_lt_f32_e64 %[g1], 0, v15\n\t"                                 \
+        "s_nop 1\n\t"                                                        \
+        "v_cndmask_b32_e64 v12, v12, v11, %[g1]\n\t"                         \
+        "s_branch LQ%=_" #K "\n"                                             \
+        "LS%=_" #K ":\n\t" /* some lane: 0 <= x < 2^-96, scaled by 2^32 */   \
+        "v_mul_f32 v13, 0x4f800000, v10\n\t"                                 \
+        "v_cndmask_b32_e32 v13, v10, v13, vcc\n\t"                           \
+        "v_sqrt_f32_e32 v12, v13\n\t"                                        \
+        "s_nop 0\n\t"                                                        \
+        "v_add_u32_e32 v9, -1, v12\n\t"                                      \
+        "v_add_u32_e32 v11, 1, v12\n\t"                                      \
+        "v_fma_f32 v10, -v9, v12, v13\n\t"                                   \
+        "v_fma_f32 v15, -v11, v12, v13\n\t"                                  \
+        "v_cmp_ge_f32_e64 %[g1], 0, v10\n\t"                                 \
+        "s_nop 1\n\t"                                                        \
+        "v_cndmask_b32_e64 v12, v12, v9, %[g1]\n\t"                          \
+        "v_cmp_lt_f32_e64 %[g1], 0, v15\n\t"                                 \
+        "s_nop 1\n\t"                                                        \
+        "v_cndmask_b32_e64 v12, v12, v11, %[g1]\n\t"                         \
+        "v_mul_f32 v9, 0x37800000, v12\n\t" /* x 2^-16 when scaled */        \
+        "v_cndmask_b32_e32 v12, v12, v9, vcc\n"                              \
+        "LQ%=_" #K ":\n\t" /* v12 = sqrt(disc) */                            \
+        "v_sub_f32_e64 v11, -v8, v12\n\t" /* -hb - sq */                     \
+        "v_add_f32_e64 v13, -v8, v12\n\t" /* -hb + sq */                     \
+        "v_mul_f32 v15, v11, %[ra]\n\t"   /* div_by: q0 = n y */             \
+        "v_mul_f32 v16, v13, %[ra]\n\t"                                      \
+        "v_fma_f32 v11, -%[a], v15, v11\n\t" /* e = n - a q0 */              \
+        "v_fma_f32 v13, -%[a], v16, v13\n\t"                                 \
+        "v_fmac_f32 v15, v11, %[ra]\n\t" /* t1 = q0 + e y */                 \
+        "v_fmac_f32 v16, v13, %[ra]\n\t" /* t2 */                            \
+        "v_cmp_lt_f32_e64 %[g1], %[tmin], v15\n\t"                           \
+        "v_cmp_lt_f32_e64 %[l1], v15, %[cl]\n\t"                             \
+        "v_cmp_lt_f32_e64 %[l2], %[tmin], v16\n\t"                           \
+        "s_and_b64 %[l1], %[l1], %[g1]\n\t"                                  \
+        "s_andn2_b64 %[l2], %[l2], %[g1]\n\t"                                \
+        "v_cmp_lt_f32_e64 %[wm], v16, %[cl]\n\t"                             \
+        "s_and_b64 %[l2], %[l2], %[wm]\n\t"                                  \
+        "s_or_b64 %[l1], %[l1], %[l2]\n\t"                                   \
+        "s_and_b64 %[l1], %[l1], %[pm]\n\t"                                  \
+        "v_cndmask_b32_e64 v16, v16, v15, %[g1]\n\t"                         \
+        "v_cndmask_b32_e64 %[cl], %[cl], v16, %[l1]\n\t"                     \
+        "v_cndmask_b32_e64 %[hit], %[hit], v14, %[l1]\n"                     \
+        "LT%=_" #K ":\n\t"                                                   \
+        "s_andn2_b64 exec, %[qm], %[qs]\n\t" /* quad lanes */                \
+        "s_cbranch_execz LR%=_" #K "\n\t"                                    \
+        "v_mul_f32 v8, %[dx], v10\n\t" /* denom = d . n (hittables.go:168) */\
+        "v_mul_f32 v9, %[dy], v11\n\t"                                       \
+        "v_add_f32 v8, v8, v9\n\t"                                           \
+        "v_mul_f32 v9, %[dz], v12\n\t"                                       \
+        "v_add_f32 v8, v8, v9\n\t"                                           \
+        "v_mul_f32 v15, v10, %[ox]\n\t" /* n . o */                          \
+        "v_mul_f32 v16, v11, %[oy]\n\t"                                      \
+        "v_add_f32 v15, v15, v16\n\t"                                        \
+        "v_mul_f32 v16, v12, %[oz]\n\t"                                      \
+        "v_add_f32 v15, v15, v16\n\t"                                        \
+        "v_sub_f32 v15, v19, v15\n\t" /* D - n . o  (:174) */                \
+        "v_rcp_f32_e32 v16, v8\n\t" /* y = RN(1 / denom): fma Newton step */ \
+        "v_and_b32_e32 v9, 0x7fffffff, v8\n\t"                               \
+        "v_cmp_gt_f32_e32 vcc, 0x322bcc78, v9\n\t" /* |denom| < 1e-8 (:170): parallel */\
+        "v_fma_f32 v17, -v8, v16, 1.0\n\t"                                   \
+        "v_fma_f32 v16, v17, v16, v16\n\t"                                   \
+        "v_mul_f32 v17, v15, v16\n\t" /* div_by: t = (D - n.o) / denom */    \
+        "v_fma_f32 v15, -v8, v17, v15\n\t"                                   \
+        "v_fmac_f32 v17, v15, v16\n\t" /* t */                               \
+        "v_cmp_lt_f32_e64 %[l1], %[tmin], v17\n\t" /* tmin < t < closest (:176) */\
+        "v_cmp_lt_f32_e64 %[l2], v17, %[cl]\n\t"                             \
+        "s_and_b64 %[l1], %[l1], %[l2]\n\t"                                  \
+        "s_andn2_b64 %[l1], %[l1], vcc\n\t"                                  \
+        "s_and_saveexec_b64 %[g1], %[l1]\n\t" /* lanes on the plane inside the bound */\
+        "s_cbranch_execz LR%=_" #K "\n\t"                                    \
+        "v_lshlrev_b32_e32 v9, 6, v13\n\t" /* the quad record: Q, u, v, w (rtx_layout.h) */\
+        "v_add_u32_e32 v9, %[qbase], v9\n\t"                                 \
+        "ds_read_b96 v[20:22], v9\n\t"                                       \
+        "ds_read_b96 v[24:26], v9 offset:16\n\t"                             \
+        "ds_read_b96 v[28:30], v9 offset:32\n\t"                             \
+        "ds_read_b96 v[32:34], v9 offset:48\n\t"                             \
+        "v_mul_f32 v10, %[dx], v17\n\t" /* r.At(t) = d t + o (:180) */       \
+        "v_mul_f32 v11, %[dy], v17\n\t"                                      \
+        "v_mul_f32 v12, %[dz], v17\n\t"                                      \
+        "v_add_f32 v10, v10, %[ox]\n\t"                                      \
+        "v_add_f32 v11, v11, %[oy]\n\t"                                      \
+        "v_add_f32 v12, v12, %[oz]\n\t"                                      \
+        "s_waitcnt lgkmcnt(0)\n\t" /* (the successor read returns first) */  \
+        "v_sub_f32 v10, v10, v20\n\t" /* php = p - Q (:181) */               \
+        "v_sub_f32 v11, v11, v21\n\t"                                        \
+        "v_sub_f32 v12, v12, v22\n\t"                                        \
+        "v_mul_f32 v15, v11, v30\n\t" /* cross(php, v) (:182) */             \
+        "v_mul_f32 v16, v12, v29\n\t"                                        \
+        "v_sub_f32 v15, v15, v16\n\t"                                        \
+        "v_mul_f32 v16, v12, v28\n\t"                                        \
+        "v_mul_f32 v19, v10, v30\n\t"                                        \
+        "v_sub_f32 v16, v16, v19\n\t"                                        \
+        "v_mul_f32 v19, v10, v29\n\t"                                        \
+        "v_mul_f32 v20, v11, v28\n\t"                                        \
+        "v_sub_f32 v19, v19, v20\n\t"                                        \
+        "v_mul_f32 v15, v32, v15\n\t" /* alpha = w . c */                    \
+        "v_mul_f32 v16, v33, v16\n\t"                                        \
+        "v_add_f32 v15, v15, v16\n\t"                                        \
+        "v_mul_f32 v16, v34, v19\n\t"                                        \
+        "v_add_f32 v15, v15, v16\n\t"                                        \
+        "v_mul_f32 v16, v25, v12\n\t" /* cross(u, php) (:183) */             \
+        "v_mul_f32 v19, v26, v11\n\t"                                        \
+        "v_sub_f32 v16, v16, v19\n\t"                                        \
+        "v_mul_f32 v19, v26, v10\n\t"                                        \
+        "v_mul_f32 v20, v24, v12\n\t"                                        \
+        "v_sub_f32 v19, v19, v20\n\t"                                        \
+        "v_mul_f32 v20, v24, v11\n\t"                                        \
+        "v_mul_f32 v21, v25, v10\n\t"                                        \
+        "v_sub_f32 v20, v20, v21\n\t"                                        \
+        "v_mul_f32 v16, v32, v16\n\t" /* beta = w . c */                     \
+        "v_mul_f32 v19, v33, v19\n\t"                                        \
+        "v_add_f32 v16, v16, v19\n\t"                                        \
+        "v_mul_f32 v19, v34, v20\n\t"                                        \
+        "v_add_f32 v16, v16, v19\n\t"                                        \
+        "v_cmp_gt_f32_e64 %[l1], 0, v15\n\t" /* outside: a < 0 || 1 < a || b < 0 || 1 < b (:185) */\
+        "v_cmp_lt_f32_e64 %[l2], 1.0, v15\n\t"                               \
+        "s_or_b64 %[l1], %[l1], %[l2]\n\t"                                   \
+        "v_cmp_gt_f32_e64 %[l2], 0, v16\n\t"                                 \
+        "s_or_b64 %[l1], %[l1], %[l2]\n\t"                                   \
+        "v_cmp_lt_f32_e64 %[l2], 1.0, v16\n\t"                               \
+        "s_or_b64 %[l1], %[l1], %[l2]\n\t"                                   \
+        "s_andn2_b64 %[l1], exec, %[l1]\n\t" /* hit (NaN alpha or beta: inside, as in Go) */\
+        "v_cndmask_b32_e64 %[cl], %[cl], v17, %[l1]\n\t"                     \
+        "v_cndmask_b32_e64 %[hit], %[hit], v14, %[l1]\n\t"                   \
+        "LR%=_" #K ":\n\t"                                                   \
+        "s_mov_b64 exec, %[save]\n\t"                                        \
+        "LE%=_" #K ":\n\t"
 // The whole traversal phase (traverse_loop's !COUNT body for this case): six asm steps, then the
 // vote — at_end = pos >= end, walking lanes W, waiting lanes P0 — until no lane walks or at
 // least `thresh` wait; returns the final at_end mask.  Positions only increase along a walk, so
@@ -1167,12 +1249,24 @@ __device__ __forceinline__ uint32_t trav_step_batched(Trav& t, const Ray& r, con
 #define RTX_WALK_CLOBBERS                                                                                    \
     "v0", "v1", "v2", "v3", "v4", "v5", "v6", "v7", "v8", "v9", "v10", "v11", "v12", "v13", "v14", "v15",    \
         "v16", "vcc", "scc"
+// QUADS: the scene holds quads (RTX_WALK_STEP_PFQ; the quad table at LDS byte qbase).
+template <bool QUADS = false>
 __device__ __forceinline__ uint64_t walk_phase_asm(Trav& t, const Ray& r, uint32_t end, uint32_t kmin, float tmin,
-                                                   uint64_t W, uint64_t P0, uint32_t thresh) {
+                                                   uint64_t W, uint64_t P0, uint32_t thresh, uint32_t qbase = 0) {
     static_assert(LDS_B == 32768, "the asm reads the 'b' halves at offset:32768");
     uint64_t pm, wm, save, g1, l1, l2;
     uint32_t cnt;
-    if constexpr (RTX_WALK_PREFETCH) {
+    if constexpr (QUADS) {
+        uint64_t qm, qs;
+#define S(K) RTX_WALK_STEP_PFQ(K, RTX_LOAD_LDS, RTX_WAIT_LDS)
+        asm volatile(RTX_LOAD_LDS "\nLW%=:\n\t" S(0) S(1) S(2) S(3) S(4) S(5) RTX_WALK_VOTE
+                     "\n\ts_waitcnt lgkmcnt(0)"
+                     : RTX_WALK_OUTS, [qm] "=&s"(qm), [qs] "=&s"(qs)
+                     : RTX_WALK_INS, [qbase] "s"(qbase)
+                     : RTX_WALK_CLOBBERS, "v17", "v18", "v19", "v20", "v21", "v22", "v23", "v24", "v25", "v26", "v27",
+                       "v28", "v29", "v30", "v31", "v32", "v33", "v34");
+#undef S
+    } else {
 #define S(K) RTX_WALK_STEP_PF(K, RTX_LOAD_LDS, RTX_WAIT_LDS)
         asm volatile(RTX_LOAD_LDS "\nLW%=:\n\t" S(0) S(1) S(2) S(3) S(4) S(5) RTX_WALK_VOTE
                      "\n\ts_waitcnt lgkmcnt(0)"
@@ -1180,18 +1274,11 @@ __device__ __forceinline__ uint64_t walk_phase_asm(Trav& t, const Ray& r, uint32
                      : RTX_WALK_INS
                      : RTX_WALK_CLOBBERS);
 #undef S
-    } else {
-#define S(K) RTX_WALK_STEP_ASM(K)
-        asm volatile("LW%=:\n\t" S(0) S(1) S(2) S(3) S(4) S(5) RTX_WALK_VOTE
-                     : RTX_WALK_OUTS
-                     : RTX_WALK_INS
-                     : RTX_WALK_CLOBBERS);
-#undef S
     }
     return pm;  // at_end
 }
-#undef RTX_WALK_STEP_ASM
 #undef RTX_WALK_STEP_PF
+#undef RTX_WALK_STEP_PFQ
 #undef RTX_LOAD_LDS
 #undef RTX_WAIT_LDS
 #undef RTX_WALK_VOTE

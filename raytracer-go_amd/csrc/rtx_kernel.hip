@@ -70,12 +70,13 @@ __device__ __forceinline__ void traverse_loop(uint32_t& mode, Trav& t, const Ray
     // lanes P0, lanes without an item D; per iteration only `at_end` is voted.
     const uint64_t W = ballot(mode == 0), P0 = ballot(mode - 1u < 2u);
     const uint64_t D = COUNT ? ballot(mode == 3) : 0ull;
-    // The asm walk (walk_phase_asm) for sphere scenes in LDS.  (For config 4's scene in HBM with
+    // The asm walk (walk_phase_asm) for scenes in LDS (spheres, and quads).  (For config 4's scene in HBM with
     // its top levels in LDS an asm walk lost to this C++ one: +9 % batched, +23 % running both
     // kinds per step)
-    if constexpr (RTX_ASM_STEP && BATCH && !COUNT && !QUADS && FIXED && !HYB && MED3) {
+    if constexpr (RTX_ASM_STEP && BATCH && !COUNT && FIXED && !HYB && MED3) {
         static_assert(STEPS == 6, "walk_phase_asm takes six steps per vote");
-        const uint64_t at_end = walk_phase_asm(t, r, 16 * n_entries, prim_batch, 0.001f, W, P0, thresh);
+        const uint64_t at_end = walk_phase_asm<QUADS>(t, r, 16 * n_entries, prim_batch, 0.001f, W, P0, thresh,
+                                                      LDS_B + 16 * (n_entries + 1));  // the quad table (fixed layout)
         if (__builtin_amdgcn_inverse_ballot_w64(W & at_end)) mode = 1;  // walked to the end
         return;
     }
