@@ -957,38 +957,34 @@ __device__ __forceinline__ uint32_t trav_step_batched(Trav& t, const Ray& r, con
         "v_mul_f32 v10, %[a], v10\n\t" /* disc = hb*hb - a*c */              \
         "v_mul_f32 v9, v8, v8\n\t"                                           \
         "v_sub_f32 v10, v9, v10\n\t"                                         \
-        "v_cmp_le_f32_e64 %[pm], 0, v10\n\t"                                 \
-        "v_cmp_gt_f32_e32 vcc, 0xf800000, v10\n\t" /* x < 2^-96 */           \
-        "s_and_b64 %[g1], vcc, %[pm]\n\t"                                    \
-        "s_cbranch_scc1 LS%=_" #K "\n\t"                                     \
-        "v_sqrt_f32_e32 v12, v10\n\t" /* every lane: x >= 2^-96 or x < 0 */  \
-        "s_nop 0\n\t"                                                        \
+        "v_cmp_gt_u32_e32 vcc, 0xf800000, v10\n\t" /* 0 <= x < 2^-96 (by its bits) */\
+        "s_cbranch_vccnz LS%=_" #K "\n\t"                                    \
+        "v_sqrt_f32_e32 v12, v10\n\t" /* every lane: x >= 2^-96, -0 or x < 0 */\
+        "v_cmp_le_f32_e64 %[pm], 0, v10\n\t" /* disc >= 0 (fills the v_sqrt hazard slot) */\
         "v_add_u32_e32 v9, -1, v12\n\t"                                      \
         "v_add_u32_e32 v11, 1, v12\n\t"                                      \
         "v_fma_f32 v13, -v9, v12, v10\n\t"                                   \
         "v_fma_f32 v15, -v11, v12, v10\n\t"                                  \
         "v_cmp_ge_f32_e64 %[g1], 0, v13\n\t"                                 \
-        "s_nop 1\n\t"                                                        \
+        "v_cmp_lt_f32_e64 %[l1], 0, v15\n\t"                                 \
+        "s_nop 0\n\t"                                                        \
         "v_cndmask_b32_e64 v12, v12, v9, %[g1]\n\t"                          \
-        "v_cmp_lt_f32_e64 %[g1], 0, v15\n\t"                                 \
-        "s_nop 1\n\t"                                                        \
-        "v_cndmask_b32_e64 v12, v12, v11, %[g1]\n\t"                         \
+        "v_cndmask_b32_e64 v12, v12, v11, %[l1]\n\t"                         \
         "s_branch LQ%=_" #K "\n"                                             \
         "LS%=_" #K ":\n\t" /* some lane: 0 <= x < 2^-96, scaled by 2^32 */   \
         "v_mul_f32 v13, 0x4f800000, v10\n\t"                                 \
         "v_cndmask_b32_e32 v13, v10, v13, vcc\n\t"                           \
         "v_sqrt_f32_e32 v12, v13\n\t"                                        \
-        "s_nop 0\n\t"                                                        \
+        "v_cmp_le_f32_e64 %[pm], 0, v10\n\t" /* disc >= 0 */                 \
         "v_add_u32_e32 v9, -1, v12\n\t"                                      \
         "v_add_u32_e32 v11, 1, v12\n\t"                                      \
         "v_fma_f32 v10, -v9, v12, v13\n\t"                                   \
         "v_fma_f32 v15, -v11, v12, v13\n\t"                                  \
         "v_cmp_ge_f32_e64 %[g1], 0, v10\n\t"                                 \
-        "s_nop 1\n\t"                                                        \
+        "v_cmp_lt_f32_e64 %[l1], 0, v15\n\t"                                 \
+        "s_nop 0\n\t"                                                        \
         "v_cndmask_b32_e64 v12, v12, v9, %[g1]\n\t"                          \
-        "v_cmp_lt_f32_e64 %[g1], 0, v15\n\t"                                 \
-        "s_nop 1\n\t"                                                        \
-        "v_cndmask_b32_e64 v12, v12, v11, %[g1]\n\t"                         \
+        "v_cndmask_b32_e64 v12, v12, v11, %[l1]\n\t"                         \
         "v_mul_f32 v9, 0x37800000, v12\n\t" /* x 2^-16 when scaled */        \
         "v_cndmask_b32_e32 v12, v12, v9, vcc\n"                              \
         "LQ%=_" #K ":\n\t" /* v12 = sqrt(disc) */                            \
@@ -1084,38 +1080,34 @@ __device__ __forceinline__ uint32_t trav_step_batched(Trav& t, const Ray& r, con
         "v_mul_f32 v10, %[a], v10\n\t" /* disc = hb*hb - a*c */              \
         "v_mul_f32 v9, v8, v8\n\t"                                           \
         "v_sub_f32 v10, v9, v10\n\t"                                         \
-        "v_cmp_le_f32_e64 %[pm], 0, v10\n\t"                                 \
-        "v_cmp_gt_f32_e32 vcc, 0xf800000, v10\n\t" /* x < 2^-96 */           \
-        "s_and_b64 %[g1], vcc, %[pm]\n\t"                                    \
-        "s_cbranch_scc1 LS%=_" #K "\n\t"                                     \
-        "v_sqrt_f32_e32 v12, v10\n\t" /* every lane: x >= 2^-96 or x < 0 */  \
-        "s_nop 0\n\t"                                                        \
+        "v_cmp_gt_u32_e32 vcc, 0xf800000, v10\n\t" /* 0 <= x < 2^-96 (by its bits) */\
+        "s_cbranch_vccnz LS%=_" #K "\n\t"                                    \
+        "v_sqrt_f32_e32 v12, v10\n\t" /* every lane: x >= 2^-96, -0 or x < 0 */\
+        "v_cmp_le_f32_e64 %[pm], 0, v10\n\t" /* disc >= 0 (fills the v_sqrt hazard slot) */\
         "v_add_u32_e32 v9, -1, v12\n\t"                                      \
         "v_add_u32_e32 v11, 1, v12\n\t"                                      \
         "v_fma_f32 v13, -v9, v12, v10\n\t"                                   \
         "v_fma_f32 v15, -v11, v12, v10\n\t"                                  \
         "v_cmp_ge_f32_e64 %[g1], 0, v13\n\t"                                 \
-        "s_nop 1\n\t"                                                        \
+        "v_cmp_lt_f32_e64 %[l1], 0, v15\n\t"                                 \
+        "s_nop 0\n\t"                                                        \
         "v_cndmask_b32_e64 v12, v12, v9, %[g1]\n\t"                          \
-        "v_cmp_lt_f32_e64 %[g1], 0, v15\n\t"                                 \
-        "s_nop 1\n\t"                                                        \
-        "v_cndmask_b32_e64 v12, v12, v11, %[g1]\n\t"                         \
+        "v_cndmask_b32_e64 v12, v12, v11, %[l1]\n\t"                         \
         "s_branch LQ%=_" #K "\n"                                             \
         "LS%=_" #K ":\n\t" /* some lane: 0 <= x < 2^-96, scaled by 2^32 */   \
         "v_mul_f32 v13, 0x4f800000, v10\n\t"                                 \
         "v_cndmask_b32_e32 v13, v10, v13, vcc\n\t"                           \
         "v_sqrt_f32_e32 v12, v13\n\t"                                        \
-        "s_nop 0\n\t"                                                        \
+        "v_cmp_le_f32_e64 %[pm], 0, v10\n\t" /* disc >= 0 */                 \
         "v_add_u32_e32 v9, -1, v12\n\t"                                      \
         "v_add_u32_e32 v11, 1, v12\n\t"                                      \
         "v_fma_f32 v10, -v9, v12, v13\n\t"                                   \
         "v_fma_f32 v15, -v11, v12, v13\n\t"                                  \
         "v_cmp_ge_f32_e64 %[g1], 0, v10\n\t"                                 \
-        "s_nop 1\n\t"                                                        \
+        "v_cmp_lt_f32_e64 %[l1], 0, v15\n\t"                                 \
+        "s_nop 0\n\t"                                                        \
         "v_cndmask_b32_e64 v12, v12, v9, %[g1]\n\t"                          \
-        "v_cmp_lt_f32_e64 %[g1], 0, v15\n\t"                                 \
-        "s_nop 1\n\t"                                                        \
-        "v_cndmask_b32_e64 v12, v12, v11, %[g1]\n\t"                         \
+        "v_cndmask_b32_e64 v12, v12, v11, %[l1]\n\t"                         \
         "v_mul_f32 v9, 0x37800000, v12\n\t" /* x 2^-16 when scaled */        \
         "v_cndmask_b32_e32 v12, v12, v9, vcc\n"                              \
         "LQ%=_" #K ":\n\t" /* v12 = sqrt(disc) */                            \
