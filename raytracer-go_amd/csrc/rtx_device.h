@@ -909,12 +909,11 @@ __device__ __forceinline__ uint32_t trav_step_batched(Trav& t, const Ray& r, con
 #define RTX_WALK_STEP_PF(K, LOAD, WAIT)                                      \
         WAIT                                                                 \
         "v_cmp_gt_i32_e64 %[pm], -1, v7\n\t"                                 \
-        "s_andn2_b64 %[wm], %[wk], %[pm]\n\t"                                \
         "s_bcnt1_i32_b64 %[cnt], %[pm]\n\t"                                  \
         "s_cmp_ge_u32 %[cnt], %[kmin]\n\t"                                   \
         "s_cbranch_scc1 LP%=_" #K "\n\t"                                     \
-        "s_cmp_eq_u64 %[wm], 0\n\t"                                          \
-        "s_cbranch_scc1 LP%=_" #K "\n\t"                                     \
+        "s_andn2_b64 %[wm], %[wk], %[pm]\n\t" /* scc: a node lane */         \
+        "s_cbranch_scc0 LP%=_" #K "\n\t"                                     \
         /* ---- box tests on the node lanes, then their next entries */      \
         "s_and_saveexec_b64 %[save], %[wm]\n\t"                              \
         "v_sub_f32 v0, v0, %[ox]\n\t"                                        \
@@ -1023,12 +1022,11 @@ __device__ __forceinline__ uint32_t trav_step_batched(Trav& t, const Ray& r, con
 #define RTX_WALK_STEP_PFQ(K, LOAD, WAIT)                                     \
         WAIT                                                                 \
         "v_cmp_gt_i32_e64 %[pm], -1, v7\n\t"                                 \
-        "s_andn2_b64 %[wm], %[wk], %[pm]\n\t"                                \
         "s_bcnt1_i32_b64 %[cnt], %[pm]\n\t"                                  \
         "s_cmp_ge_u32 %[cnt], %[kmin]\n\t"                                   \
         "s_cbranch_scc1 LP%=_" #K "\n\t"                                     \
-        "s_cmp_eq_u64 %[wm], 0\n\t"                                          \
-        "s_cbranch_scc1 LP%=_" #K "\n\t"                                     \
+        "s_andn2_b64 %[wm], %[wk], %[pm]\n\t" /* scc: a node lane */         \
+        "s_cbranch_scc0 LP%=_" #K "\n\t"                                     \
         /* ---- box tests on the node lanes, then their next entries */      \
         "s_and_saveexec_b64 %[save], %[wm]\n\t"                              \
         "v_sub_f32 v0, v0, %[ox]\n\t"                                        \
@@ -1230,9 +1228,8 @@ __device__ __forceinline__ uint32_t trav_step_batched(Trav& t, const Ray& r, con
 // every lane reaches the sentinel and the loop ends.
 #define RTX_WALK_VOTE                                                        \
         "v_cmp_ge_u32_e64 %[pm], %[pos], %[end]\n\t"                         \
-        "s_andn2_b64 %[wk], %[W], %[pm]\n\t" /* still walking */             \
-        "s_cmp_eq_u64 %[wk], 0\n\t"                                          \
-        "s_cbranch_scc1 LX%=\n\t"                                            \
+        "s_andn2_b64 %[wk], %[W], %[pm]\n\t" /* still walking (scc: any) */  \
+        "s_cbranch_scc0 LX%=\n\t"                                            \
         "s_and_b64 %[l1], %[W], %[pm]\n\t"                                   \
         "s_or_b64 %[l1], %[l1], %[P0]\n\t" /* waiting to shade */            \
         "s_bcnt1_i32_b64 %[cnt], %[l1]\n\t"                                  \
