@@ -58,6 +58,8 @@ struct DeviceCopy {
     unsigned long long* counters = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     uint32_t hot = 0;  // entries stored first and cached in LDS by v3 (scenes too big for the LDS copy)
+    uint32_t start = 0;     // walk position of the first entry of the walk (the root)
+    uint32_t prim_end = 0;  // scenes in the LDS copy: primitives stored first, below this position
 };
 
 // Sample-colour scratch, one per device, shared by all scenes (grown on demand).  `last`
@@ -327,7 +329,9 @@ int upload_copy(rtx_scene* s, DeviceCopy& c) {
     {  // device layout: all 'a' halves, then all 'b' halves (rtxd::SceneRef), each ending
        // with the sentinel entry (rtx_layout.h).  Every entry names its successor (node: next
        // and escape, primitive: next), so the storage order is free: a scene too big for the
-       // LDS copy stores its top levels first (c.hot entries), which v3 caches in LDS.
+       // LDS copy stores its top levels first (c.hot entries), which v3 caches in LDS; a scene
+       // in the LDS copy stores its primitives first (below c.prim_end), so the asm walk knows
+       // an entry's kind from its position before the entry's read returns (walk_phase_asm).
         const size_t n = s->entries.size(), m = n + 1;
         std::vector<uint32_t> pos(m);  // storage index of entry i; the sentinel stays last
         for (size_t i = 0; i <= n; ++i) pos[i] = (uint32_t)i;
@@ -354,7 +358,21 @@ int upload_copy(rtx_scene* s, DeviceCopy& c) {
             for (size_t i = 0; i < n; ++i)
                 if (depth[i] >= levels) pos[i] = k++;
             c.hot = hot;
+        } else {
+            uint32_t k = 0;
+            for (int pass = 0; pass < 2; ++pass)
+                for (size_t i = 0; i < n; ++i) {
+                    int32_t tag;
+                    std::memcpy(&tag, &s->entries[i].b[3], 4);
+                    if ((tag != RTX_E_NODE) == (pass == 0)) pos[i] = k++;
+                }
+            for (size_t i = 0; i < n; ++i) {
+                int32_t tag;
+                std::memcpy(&tag, &s->entries[i].b[3], 4);
+                if (tag != RTX_E_NODE) c.prim_end = 16 * (pos[i] + 1) > c.prim_end ? 16 * (pos[i] + 1) : c.prim_end;
+            }
         }
+        c.start = 16 * pos[0];
         std::vector<float> soa(m * 8 + s->quadtab.size(), 0.0f);
         for (size_t i = 0; i < n; ++i) {
             const size_t j = pos[i];
@@ -529,6 +547,8 @@ rtxd::Params make_params(const rtx_scene* s, const DeviceCopy* c, const rtx_came
     p.has_uv = s->has_image ? 1u : 0u;
     p.has_noise = s->has_noise ? 1u : 0u;
     p.n_hot = c->hot;
+    p.start = c->start;
+    p.prim_end = c->prim_end;
     return p;
 }
 

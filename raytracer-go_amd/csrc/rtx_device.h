@@ -371,10 +371,11 @@ struct SceneRef {
     const float4* la;
     const float4* lb;
     uint32_t hot;
+    uint32_t prim_end;  // the fixed layout: primitives stored below this position (Params::prim_end)
 };
 __device__ __forceinline__ SceneRef scene_ref(const float4* base, uint32_t n_entries, const rtx_material* mats) {
     const uint32_t m = n_entries + 1;  // + the sentinel
-    return SceneRef{base, base + m, base + 2 * m, mats, nullptr, nullptr, 0u};
+    return SceneRef{base, base + m, base + 2 * m, mats, nullptr, nullptr, 0u, 0u};
 }
 // v3's LDS layout: the 'a' halves from LDS byte 0, the 'b' halves from byte LDS_B, the
 // quad table after them.  A walk position is then the LDS address of its 'a' half and
@@ -395,7 +396,7 @@ __device__ __forceinline__ SceneRef scene_ref_fixed(const float4* lds, uint32_t 
                                                     uint32_t n_mats) {
     return SceneRef{lds, lds + LDS_B / 16, lds + LDS_B / 16 + n_entries + 1,
                     reinterpret_cast<const rtx_material*>(lds + lds_mat_offset(n_entries, n_quads, n_mats) / 16),
-                    nullptr, nullptr, 0u};
+                    nullptr, nullptr, 0u, 0u};
 }
 // The LDS cache of a scene too big for the fixed layout: its first entries (whole top
 // levels, rtx_capi.hip ensure_device) in the fixed layout's places.  Up to HOT_ENTRIES_8W
@@ -446,6 +447,8 @@ struct Params {
     uint32_t debug_launch;  // RTX_DEBUG_LAUNCH=1: v3 prints its launch shape to stderr
     uint32_t grid_pct;    // v3: percent of the resident grid launched (A/B knob; 100 = all resident waves)
     uint32_t prim_batch;  // v3: primitive tests wait for this many lanes (trav_step_batched); 0 = off
+    uint32_t start;       // walk position of the walk's first entry (the root)
+    uint32_t prim_end;    // scene in the LDS copy: its primitives are stored below this position
 };
 
 struct Ray {
@@ -632,7 +635,7 @@ struct Trav {
     bool safe;  // 1/dir and the origin finite, a in [2^-60, 2^60]: the SAFE step forms are exact
 };
 
-__device__ __forceinline__ void trav_begin(Trav& t, const Ray& r) {
+__device__ __forceinline__ void trav_begin(Trav& t, const Ray& r, uint32_t start) {
     // InBoundary computes 1/dir per node; hoisting it is bit-identical.
     if (__builtin_amdgcn_ballot_w64(!(rcp_fast_ok(r.d.x) && rcp_fast_ok(r.d.y) && rcp_fast_ok(r.d.z))) == 0) {
         t.ix = rcp_newton(r.d.x);
@@ -653,7 +656,7 @@ __device__ __forceinline__ void trav_begin(Trav& t, const Ray& r) {
              t.a >= 0x1p-60f && t.a <= 0x1p60f;
     t.closest = __builtin_inff();
     t.hit = -1;
-    t.i = 0;
+    t.i = start;
 }
 
 // Entry index of a walk position (a byte offset, 16 per entry: Trav::i).
@@ -907,14 +910,14 @@ __device__ __forceinline__ uint32_t trav_step_batched(Trav& t, const Ray& r, con
         "ds_read_b128 v[4:7], %[pos] offset:32768\n\t" /* LDS_B */
 #define RTX_WAIT_LDS "s_waitcnt lgkmcnt(0)\n\t"
 #define RTX_WALK_STEP_PF(K, LOAD, WAIT)                                      \
-        WAIT                                                                 \
-        "v_cmp_gt_i32_e64 %[pm], -1, v7\n\t"                                 \
+        "v_cmp_gt_u32_e64 %[pm], %[pe], %[pos]\n\t" /* primitive: pos < prim_end */\
         "s_bcnt1_i32_b64 %[cnt], %[pm]\n\t"                                  \
         "s_cmp_ge_u32 %[cnt], %[kmin]\n\t"                                   \
         "s_cbranch_scc1 LP%=_" #K "\n\t"                                     \
         "s_andn2_b64 %[wm], %[wk], %[pm]\n\t" /* scc: a node lane */         \
         "s_cbranch_scc0 LP%=_" #K "\n\t"                                     \
         /* ---- box tests on the node lanes, then their next entries */      \
+        WAIT                                                                 \
         "s_and_saveexec_b64 %[save], %[wm]\n\t"                              \
         "v_sub_f32 v0, v0, %[ox]\n\t"                                        \
         "v_sub_f32 v4, v4, %[ox]\n\t"                                        \
@@ -942,6 +945,7 @@ __device__ __forceinline__ uint32_t trav_step_batched(Trav& t, const Ray& r, con
         "s_branch LE%=_" #K "\n"                                             \
         /* ---- sphere tests on the primitive lanes, successor read first */ \
         "LP%=_" #K ":\n\t"                                                   \
+        WAIT                                                                 \
         "s_and_saveexec_b64 %[save], %[pm]\n\t"                              \
         "s_cbranch_execz LR%=_" #K "\n\t"                                    \
         "v_sub_f32 v10, %[ox], v0\n\t" /* oc = o - center */                 \
@@ -1020,14 +1024,14 @@ __device__ __forceinline__ uint32_t trav_step_batched(Trav& t, const Ray& r, con
         "s_mov_b64 exec, %[save]\n"                                          \
         "LE%=_" #K ":\n\t"
 #define RTX_WALK_STEP_PFQ(K, LOAD, WAIT)                                     \
-        WAIT                                                                 \
-        "v_cmp_gt_i32_e64 %[pm], -1, v7\n\t"                                 \
+        "v_cmp_gt_u32_e64 %[pm], %[pe], %[pos]\n\t" /* primitive: pos < prim_end */\
         "s_bcnt1_i32_b64 %[cnt], %[pm]\n\t"                                  \
         "s_cmp_ge_u32 %[cnt], %[kmin]\n\t"                                   \
         "s_cbranch_scc1 LP%=_" #K "\n\t"                                     \
         "s_andn2_b64 %[wm], %[wk], %[pm]\n\t" /* scc: a node lane */         \
         "s_cbranch_scc0 LP%=_" #K "\n\t"                                     \
         /* ---- box tests on the node lanes, then their next entries */      \
+        WAIT                                                                 \
         "s_and_saveexec_b64 %[save], %[wm]\n\t"                              \
         "v_sub_f32 v0, v0, %[ox]\n\t"                                        \
         "v_sub_f32 v4, v4, %[ox]\n\t"                                        \
@@ -1055,6 +1059,7 @@ __device__ __forceinline__ uint32_t trav_step_batched(Trav& t, const Ray& r, con
         "s_branch LE%=_" #K "\n"                                             \
         /* ---- sphere tests on the primitive lanes, successor read first */ \
         "LP%=_" #K ":\n\t"                                                   \
+        WAIT                                                                 \
         "s_and_saveexec_b64 %[save], %[pm]\n\t"                              \
         "s_cbranch_execz LR%=_" #K "\n\t"                                    \
         "v_mov_b32 v10, v0\n\t" /* centre / normal */                        \
@@ -1242,14 +1247,15 @@ __device__ __forceinline__ uint32_t trav_step_batched(Trav& t, const Ray& r, con
 #define RTX_WALK_INS                                                                                         \
     [ox] "v"(r.o.x), [oy] "v"(r.o.y), [oz] "v"(r.o.z), [dx] "v"(r.d.x), [dy] "v"(r.d.y), [dz] "v"(r.d.z),  \
         [ix] "v"(t.ix), [iy] "v"(t.iy), [iz] "v"(t.iz), [a] "v"(t.a), [ra] "v"(t.ra), [end] "s"(end),      \
-        [kmin] "s"(kmin), [tmin] "s"(tmin), [W] "s"(W), [P0] "s"(P0), [thresh] "s"(thresh)
+        [kmin] "s"(kmin), [tmin] "s"(tmin), [W] "s"(W), [P0] "s"(P0), [thresh] "s"(thresh), [pe] "s"(prim_end)
 #define RTX_WALK_CLOBBERS                                                                                    \
     "v0", "v1", "v2", "v3", "v4", "v5", "v6", "v7", "v8", "v9", "v10", "v11", "v12", "v13", "v14", "v15",    \
         "v16", "vcc", "scc"
 // QUADS: the scene holds quads (RTX_WALK_STEP_PFQ; the quad table at LDS byte qbase).
 template <bool QUADS = false>
 __device__ __forceinline__ uint64_t walk_phase_asm(Trav& t, const Ray& r, uint32_t end, uint32_t kmin, float tmin,
-                                                   uint64_t W, uint64_t P0, uint32_t thresh, uint32_t qbase = 0) {
+                                                   uint64_t W, uint64_t P0, uint32_t thresh, uint32_t prim_end,
+                                                   uint32_t qbase = 0) {
     static_assert(LDS_B == 32768, "the asm reads the 'b' halves at offset:32768");
     uint64_t pm, wm, save, g1, l1, l2, wk;
     uint32_t cnt;

@@ -76,7 +76,7 @@ __device__ __forceinline__ void traverse_loop(uint32_t& mode, Trav& t, const Ray
     if constexpr (RTX_ASM_STEP && BATCH && !COUNT && FIXED && !HYB && MED3) {
         static_assert(STEPS == 6, "walk_phase_asm takes six steps per vote");
         const uint64_t at_end = walk_phase_asm<QUADS>(t, r, 16 * n_entries, prim_batch, 0.001f, W, P0, thresh,
-                                                      LDS_B + 16 * (n_entries + 1));  // the quad table (fixed layout)
+                                                      E.prim_end, LDS_B + 16 * (n_entries + 1));  // quad table
         if (__builtin_amdgcn_inverse_ballot_w64(W & at_end)) mode = 1;  // walked to the end
         return;
     }
@@ -188,6 +188,7 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
         for (uint32_t t = threadIdx.x; t < 2 * p.n_materials; t += WAVE_BLOCK) lds_entries[mo + t] = mg[t];
         __syncthreads();
         E = scene_ref_fixed(lds_entries, p.n_entries, p.n_quads, p.n_materials);
+        E.prim_end = p.prim_end;
     } else {
         E = scene_ref(p.entries, p.n_entries, p.materials);
         if constexpr (HYB) {  // the scene's top levels, stored first, cached in LDS (fixed layout)
@@ -341,7 +342,7 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
         if (COUNT) split_clk(split[2], clk);
         if (ready) {  // begin a segment: world.Hit (ray.go:36)
             if (COUNT) ++cnt.segments;
-            trav_begin(t, r);
+            trav_begin(t, r, p.start);
             mode = n_entries > 0 ? M_TRAV : M_SHADE;
         }
         if (COUNT) split_clk(split[3], clk);
