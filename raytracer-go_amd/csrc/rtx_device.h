@@ -893,7 +893,9 @@ __device__ __forceinline__ uint32_t trav_step_batched(Trav& t, const Ray& r, con
 //     pos < end at the last vote (an SGPR mask: no compare per step; a lane that reaches the
 //     sentinel between two votes stays a node lane there, and a box step on the sentinel
 //     changes nothing; -1.7 % at 100 spp)
-//   - the primitive tests run when >= kmin lanes wait on one or no node lane is left
+//   - the primitive tests run when >= kmin lanes wait on one or no node lane is left; after a box
+//     step the count test is skipped and box steps follow while a node lane is left (box runs,
+//     RTX_BOX_RUNS: the primitive tests gather more lanes; -1.8 % at 100 spp, Cornell box -7.4 %)
 //   - box (MED3, box_step): per axis (min - o) * inv, (max - o) * inv; lo/hi clamped by v_med3
 //   - sphere (sphere_test<false, true>): hb, c, disc as hittables.go:97-102; sqrt correctly
 //     rounded as the compiler expands an f32 sqrt — v_sqrt, then the neighbour whose fma
@@ -909,11 +911,20 @@ __device__ __forceinline__ uint32_t trav_step_batched(Trav& t, const Ray& r, con
         "ds_read_b128 v[0:3], %[pos]\n\t"                                    \
         "ds_read_b128 v[4:7], %[pos] offset:32768\n\t" /* LDS_B */
 #define RTX_WAIT_LDS "s_waitcnt lgkmcnt(0)\n\t"
-#define RTX_WALK_STEP_PF(K, LOAD, WAIT)                                      \
+// End of a box step: back to the full wave, then the next step's header (RTX_BOX_NEXT), or straight
+// to its node test with its primitive mask taken here (RTX_BOX_FAST: after a box step the next step
+// skips the primitive-count test and runs the box tests again while a node lane is left).
+#define RTX_BOX_NEXT(K) "s_mov_b64 exec, %[save]\n\t" "s_branch LE%=_" #K "\n"
+#define RTX_BOX_FAST(KN)                                                     \
+        "s_mov_b64 exec, %[save]\n\t"                                        \
+        "v_cmp_gt_u32_e64 %[pm], %[pe], %[pos]\n\t"                          \
+        "s_branch LN%=_" #KN "\n"
+#define RTX_WALK_STEP_PF(K, LOAD, WAIT, BEND)                                      \
         "v_cmp_gt_u32_e64 %[pm], %[pe], %[pos]\n\t" /* primitive: pos < prim_end */\
         "s_bcnt1_i32_b64 %[cnt], %[pm]\n\t"                                  \
         "s_cmp_ge_u32 %[cnt], %[kmin]\n\t"                                   \
         "s_cbranch_scc1 LP%=_" #K "\n\t"                                     \
+        "LN%=_" #K ":\n\t"                                                   \
         "s_andn2_b64 %[wm], %[wk], %[pm]\n\t" /* scc: a node lane */         \
         "s_cbranch_scc0 LP%=_" #K "\n\t"                                     \
         /* ---- box tests on the node lanes, then their next entries */      \
@@ -941,8 +952,7 @@ __device__ __forceinline__ uint32_t trav_step_batched(Trav& t, const Ray& r, con
         "s_nop 1\n\t"                                                        \
         "v_cndmask_b32_e32 %[pos], v3, v7, vcc\n\t"                          \
         LOAD                                                                 \
-        "s_mov_b64 exec, %[save]\n\t"                                        \
-        "s_branch LE%=_" #K "\n"                                             \
+        BEND                                                                 \
         /* ---- sphere tests on the primitive lanes, successor read first */ \
         "LP%=_" #K ":\n\t"                                                   \
         WAIT                                                                 \
@@ -1023,11 +1033,12 @@ __device__ __forceinline__ uint32_t trav_step_batched(Trav& t, const Ray& r, con
         "LR%=_" #K ":\n\t"                                                   \
         "s_mov_b64 exec, %[save]\n"                                          \
         "LE%=_" #K ":\n\t"
-#define RTX_WALK_STEP_PFQ(K, LOAD, WAIT)                                     \
+#define RTX_WALK_STEP_PFQ(K, LOAD, WAIT, BEND)                                      \
         "v_cmp_gt_u32_e64 %[pm], %[pe], %[pos]\n\t" /* primitive: pos < prim_end */\
         "s_bcnt1_i32_b64 %[cnt], %[pm]\n\t"                                  \
         "s_cmp_ge_u32 %[cnt], %[kmin]\n\t"                                   \
         "s_cbranch_scc1 LP%=_" #K "\n\t"                                     \
+        "LN%=_" #K ":\n\t"                                                   \
         "s_andn2_b64 %[wm], %[wk], %[pm]\n\t" /* scc: a node lane */         \
         "s_cbranch_scc0 LP%=_" #K "\n\t"                                     \
         /* ---- box tests on the node lanes, then their next entries */      \
@@ -1055,8 +1066,7 @@ __device__ __forceinline__ uint32_t trav_step_batched(Trav& t, const Ray& r, con
         "s_nop 1\n\t"                                                        \
         "v_cndmask_b32_e32 %[pos], v3, v7, vcc\n\t"                          \
         LOAD                                                                 \
-        "s_mov_b64 exec, %[save]\n\t"                                        \
-        "s_branch LE%=_" #K "\n"                                             \
+        BEND                                                                 \
         /* ---- sphere tests on the primitive lanes, successor read first */ \
         "LP%=_" #K ":\n\t"                                                   \
         WAIT                                                                 \
@@ -1251,6 +1261,22 @@ __device__ __forceinline__ uint32_t trav_step_batched(Trav& t, const Ray& r, con
 #define RTX_WALK_CLOBBERS                                                                                    \
     "v0", "v1", "v2", "v3", "v4", "v5", "v6", "v7", "v8", "v9", "v10", "v11", "v12", "v13", "v14", "v15",    \
         "v16", "vcc", "scc"
+#ifndef RTX_BOX_RUNS  // 1: steps 1, 3, 5 after a box step skip the primitive-count test; 2: steps 1-5
+#define RTX_BOX_RUNS 2
+#endif
+#if RTX_BOX_RUNS == 2
+#define RTX_WALK_SIX                                                                                      \
+    S(0, RTX_BOX_FAST(1)) S(1, RTX_BOX_FAST(2)) S(2, RTX_BOX_FAST(3)) S(3, RTX_BOX_FAST(4))                \
+        S(4, RTX_BOX_FAST(5)) S(5, RTX_BOX_NEXT(5))
+#elif RTX_BOX_RUNS == 1
+#define RTX_WALK_SIX                                                                                      \
+    S(0, RTX_BOX_FAST(1)) S(1, RTX_BOX_NEXT(1)) S(2, RTX_BOX_FAST(3)) S(3, RTX_BOX_NEXT(3))                \
+        S(4, RTX_BOX_FAST(5)) S(5, RTX_BOX_NEXT(5))
+#else
+#define RTX_WALK_SIX                                                                                      \
+    S(0, RTX_BOX_NEXT(0)) S(1, RTX_BOX_NEXT(1)) S(2, RTX_BOX_NEXT(2)) S(3, RTX_BOX_NEXT(3))                \
+        S(4, RTX_BOX_NEXT(4)) S(5, RTX_BOX_NEXT(5))
+#endif
 // QUADS: the scene holds quads (RTX_WALK_STEP_PFQ; the quad table at LDS byte qbase).
 template <bool QUADS = false>
 __device__ __forceinline__ uint64_t walk_phase_asm(Trav& t, const Ray& r, uint32_t end, uint32_t kmin, float tmin,
@@ -1261,8 +1287,8 @@ __device__ __forceinline__ uint64_t walk_phase_asm(Trav& t, const Ray& r, uint32
     uint32_t cnt;
     if constexpr (QUADS) {
         uint64_t qm, qs;
-#define S(K) RTX_WALK_STEP_PFQ(K, RTX_LOAD_LDS, RTX_WAIT_LDS)
-        asm volatile(RTX_LOAD_LDS "v_cmp_lt_u32_e64 %[wk], %[pos], %[end]\nLW%=:\n\t" S(0) S(1) S(2) S(3) S(4) S(5) RTX_WALK_VOTE
+#define S(K, BEND) RTX_WALK_STEP_PFQ(K, RTX_LOAD_LDS, RTX_WAIT_LDS, BEND)
+        asm volatile(RTX_LOAD_LDS "v_cmp_lt_u32_e64 %[wk], %[pos], %[end]\nLW%=:\n\t" RTX_WALK_SIX RTX_WALK_VOTE
                      "\n\ts_waitcnt lgkmcnt(0)"
                      : RTX_WALK_OUTS, [qm] "=&s"(qm), [qs] "=&s"(qs)
                      : RTX_WALK_INS, [qbase] "s"(qbase)
@@ -1270,8 +1296,8 @@ __device__ __forceinline__ uint64_t walk_phase_asm(Trav& t, const Ray& r, uint32
                        "v28", "v29", "v30", "v31", "v32", "v33", "v34");
 #undef S
     } else {
-#define S(K) RTX_WALK_STEP_PF(K, RTX_LOAD_LDS, RTX_WAIT_LDS)
-        asm volatile(RTX_LOAD_LDS "v_cmp_lt_u32_e64 %[wk], %[pos], %[end]\nLW%=:\n\t" S(0) S(1) S(2) S(3) S(4) S(5) RTX_WALK_VOTE
+#define S(K, BEND) RTX_WALK_STEP_PF(K, RTX_LOAD_LDS, RTX_WAIT_LDS, BEND)
+        asm volatile(RTX_LOAD_LDS "v_cmp_lt_u32_e64 %[wk], %[pos], %[end]\nLW%=:\n\t" RTX_WALK_SIX RTX_WALK_VOTE
                      "\n\ts_waitcnt lgkmcnt(0)"
                      : RTX_WALK_OUTS
                      : RTX_WALK_INS
@@ -1282,6 +1308,9 @@ __device__ __forceinline__ uint64_t walk_phase_asm(Trav& t, const Ray& r, uint32
 }
 #undef RTX_WALK_STEP_PF
 #undef RTX_WALK_STEP_PFQ
+#undef RTX_WALK_SIX
+#undef RTX_BOX_NEXT
+#undef RTX_BOX_FAST
 #undef RTX_LOAD_LDS
 #undef RTX_WAIT_LDS
 #undef RTX_WALK_VOTE
