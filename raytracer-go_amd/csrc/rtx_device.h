@@ -894,8 +894,8 @@ __device__ __forceinline__ uint32_t trav_step_batched(Trav& t, const Ray& r, con
 //     sentinel between two votes stays a node lane there, and a box step on the sentinel
 //     changes nothing; -1.7 % at 100 spp)
 //   - the primitive tests run when >= kmin lanes wait on one or no node lane is left; after a box
-//     step the count test is skipped and box steps follow while a node lane is left (box runs,
-//     RTX_BOX_RUNS: the primitive tests gather more lanes; -1.8 % at 100 spp, Cornell box -7.4 %)
+//     step the count test is skipped and box steps follow while a node lane is left (box runs:
+//     the primitive tests gather more lanes; -1.8 % at 100 spp, Cornell box -7.4 %)
 //   - box (MED3, box_step): per axis (min - o) * inv, (max - o) * inv; lo/hi clamped by v_med3
 //   - sphere (sphere_test<false, true>): hb, c, disc as hittables.go:97-102; sqrt correctly
 //     rounded as the compiler expands an f32 sqrt — v_sqrt, then the neighbour whose fma
@@ -1237,7 +1237,8 @@ __device__ __forceinline__ uint32_t trav_step_batched(Trav& t, const Ray& r, con
         "LR%=_" #K ":\n\t"                                                   \
         "s_mov_b64 exec, %[save]\n\t"                                        \
         "LE%=_" #K ":\n\t"
-// The whole traversal phase (traverse_loop's !COUNT body for this case): six asm steps, then the
+// The whole traversal phase (traverse_loop's !COUNT body for this case): RTX_ASM_BLOCK asm steps
+// (RTX_ASM_BLOCK_Q with quads), then the
 // vote — at_end = pos >= end, walking lanes W, waiting lanes P0 — until no lane walks or at
 // least `thresh` wait; returns the final at_end mask.  Positions only increase along a walk, so
 // every lane reaches the sentinel and the loop ends.
@@ -1261,22 +1262,26 @@ __device__ __forceinline__ uint32_t trav_step_batched(Trav& t, const Ray& r, con
 #define RTX_WALK_CLOBBERS                                                                                    \
     "v0", "v1", "v2", "v3", "v4", "v5", "v6", "v7", "v8", "v9", "v10", "v11", "v12", "v13", "v14", "v15",    \
         "v16", "vcc", "scc"
-#ifndef RTX_BOX_RUNS  // 1: steps 1, 3, 5 after a box step skip the primitive-count test; 2: steps 1-5
-#define RTX_BOX_RUNS 2
+// Steps per vote (A/B with box runs, 100 spp / Cornell box 600x600x50: 4 steps -0.1 % / -2.4 %,
+// 5 -0.4 % / +2.4 %, 8 +0.6 % / +2.5 %, 12 +6 % / +14 % against 6).  Every step but a block's last
+// continues a box run into the next step (RTX_BOX_FAST).
+#ifndef RTX_ASM_BLOCK  // sphere scenes
+#define RTX_ASM_BLOCK 6
 #endif
-#if RTX_BOX_RUNS == 2
-#define RTX_WALK_SIX                                                                                      \
-    S(0, RTX_BOX_FAST(1)) S(1, RTX_BOX_FAST(2)) S(2, RTX_BOX_FAST(3)) S(3, RTX_BOX_FAST(4))                \
-        S(4, RTX_BOX_FAST(5)) S(5, RTX_BOX_NEXT(5))
-#elif RTX_BOX_RUNS == 1
-#define RTX_WALK_SIX                                                                                      \
-    S(0, RTX_BOX_FAST(1)) S(1, RTX_BOX_NEXT(1)) S(2, RTX_BOX_FAST(3)) S(3, RTX_BOX_NEXT(3))                \
-        S(4, RTX_BOX_FAST(5)) S(5, RTX_BOX_NEXT(5))
-#else
-#define RTX_WALK_SIX                                                                                      \
-    S(0, RTX_BOX_NEXT(0)) S(1, RTX_BOX_NEXT(1)) S(2, RTX_BOX_NEXT(2)) S(3, RTX_BOX_NEXT(3))                \
-        S(4, RTX_BOX_NEXT(4)) S(5, RTX_BOX_NEXT(5))
+#ifndef RTX_ASM_BLOCK_Q  // scenes with quads
+#define RTX_ASM_BLOCK_Q 4
 #endif
+#define RTX_WALK_4 S(0, RTX_BOX_FAST(1)) S(1, RTX_BOX_FAST(2)) S(2, RTX_BOX_FAST(3)) S(3, RTX_BOX_NEXT(3))
+#define RTX_WALK_5 \
+    S(0, RTX_BOX_FAST(1)) S(1, RTX_BOX_FAST(2)) S(2, RTX_BOX_FAST(3)) S(3, RTX_BOX_FAST(4)) S(4, RTX_BOX_NEXT(4))
+#define RTX_WALK_6                                                                                          \
+    S(0, RTX_BOX_FAST(1)) S(1, RTX_BOX_FAST(2)) S(2, RTX_BOX_FAST(3)) S(3, RTX_BOX_FAST(4)) S(4, RTX_BOX_FAST(5)) \
+        S(5, RTX_BOX_NEXT(5))
+#define RTX_WALK_8                                                                                          \
+    S(0, RTX_BOX_FAST(1)) S(1, RTX_BOX_FAST(2)) S(2, RTX_BOX_FAST(3)) S(3, RTX_BOX_FAST(4)) S(4, RTX_BOX_FAST(5)) \
+        S(5, RTX_BOX_FAST(6)) S(6, RTX_BOX_FAST(7)) S(7, RTX_BOX_NEXT(7))
+#define RTX_WALK_BLOCK_(n) RTX_WALK_##n
+#define RTX_WALK_BLOCK(n) RTX_WALK_BLOCK_(n)
 // QUADS: the scene holds quads (RTX_WALK_STEP_PFQ; the quad table at LDS byte qbase).
 template <bool QUADS = false>
 __device__ __forceinline__ uint64_t walk_phase_asm(Trav& t, const Ray& r, uint32_t end, uint32_t kmin, float tmin,
@@ -1288,7 +1293,7 @@ __device__ __forceinline__ uint64_t walk_phase_asm(Trav& t, const Ray& r, uint32
     if constexpr (QUADS) {
         uint64_t qm, qs;
 #define S(K, BEND) RTX_WALK_STEP_PFQ(K, RTX_LOAD_LDS, RTX_WAIT_LDS, BEND)
-        asm volatile(RTX_LOAD_LDS "v_cmp_lt_u32_e64 %[wk], %[pos], %[end]\nLW%=:\n\t" RTX_WALK_SIX RTX_WALK_VOTE
+        asm volatile(RTX_LOAD_LDS "v_cmp_lt_u32_e64 %[wk], %[pos], %[end]\nLW%=:\n\t" RTX_WALK_BLOCK(RTX_ASM_BLOCK_Q) RTX_WALK_VOTE
                      "\n\ts_waitcnt lgkmcnt(0)"
                      : RTX_WALK_OUTS, [qm] "=&s"(qm), [qs] "=&s"(qs)
                      : RTX_WALK_INS, [qbase] "s"(qbase)
@@ -1297,7 +1302,7 @@ __device__ __forceinline__ uint64_t walk_phase_asm(Trav& t, const Ray& r, uint32
 #undef S
     } else {
 #define S(K, BEND) RTX_WALK_STEP_PF(K, RTX_LOAD_LDS, RTX_WAIT_LDS, BEND)
-        asm volatile(RTX_LOAD_LDS "v_cmp_lt_u32_e64 %[wk], %[pos], %[end]\nLW%=:\n\t" RTX_WALK_SIX RTX_WALK_VOTE
+        asm volatile(RTX_LOAD_LDS "v_cmp_lt_u32_e64 %[wk], %[pos], %[end]\nLW%=:\n\t" RTX_WALK_BLOCK(RTX_ASM_BLOCK) RTX_WALK_VOTE
                      "\n\ts_waitcnt lgkmcnt(0)"
                      : RTX_WALK_OUTS
                      : RTX_WALK_INS
@@ -1308,7 +1313,12 @@ __device__ __forceinline__ uint64_t walk_phase_asm(Trav& t, const Ray& r, uint32
 }
 #undef RTX_WALK_STEP_PF
 #undef RTX_WALK_STEP_PFQ
-#undef RTX_WALK_SIX
+#undef RTX_WALK_4
+#undef RTX_WALK_5
+#undef RTX_WALK_6
+#undef RTX_WALK_8
+#undef RTX_WALK_BLOCK_
+#undef RTX_WALK_BLOCK
 #undef RTX_BOX_NEXT
 #undef RTX_BOX_FAST
 #undef RTX_LOAD_LDS

@@ -74,7 +74,6 @@ __device__ __forceinline__ void traverse_loop(uint32_t& mode, Trav& t, const Ray
     // its top levels in LDS an asm walk lost to this C++ one: +9 % batched, +23 % running both
     // kinds per step)
     if constexpr (RTX_ASM_STEP && BATCH && !COUNT && FIXED && !HYB && MED3) {
-        static_assert(STEPS == 6, "walk_phase_asm takes six steps per vote");
         const uint64_t at_end = walk_phase_asm<QUADS>(t, r, 16 * n_entries, prim_batch, 0.001f, W, P0, thresh,
                                                       E.prim_end, LDS_B + 16 * (n_entries + 1));  // quad table
         if (__builtin_amdgcn_inverse_ballot_w64(W & at_end)) mode = 1;  // walked to the end
