@@ -992,23 +992,6 @@ __device__ __forceinline__ uint32_t trav_step_batched(Trav& t, const Ray& r, con
         "s_nop 0\n\t"                                                        \
         "v_cndmask_b32_e64 v12, v12, v9, %[g1]\n\t"                          \
         "v_cndmask_b32_e64 v12, v12, v11, %[l1]\n\t"                         \
-        "s_branch LQ%=_" #K "\n"                                             \
-        "LS%=_" #K ":\n\t" /* some lane: 0 <= x < 2^-96, scaled by 2^32 */   \
-        "v_mul_f32 v13, 0x4f800000, v10\n\t"                                 \
-        "v_cndmask_b32_e32 v13, v10, v13, vcc\n\t"                           \
-        "v_sqrt_f32_e32 v12, v13\n\t"                                        \
-        "v_cmp_le_f32_e64 %[pm], 0, v10\n\t" /* disc >= 0 */                 \
-        "v_add_u32_e32 v9, -1, v12\n\t"                                      \
-        "v_add_u32_e32 v11, 1, v12\n\t"                                      \
-        "v_fma_f32 v10, -v9, v12, v13\n\t"                                   \
-        "v_fma_f32 v15, -v11, v12, v13\n\t"                                  \
-        "v_cmp_ge_f32_e64 %[g1], 0, v10\n\t"                                 \
-        "v_cmp_lt_f32_e64 %[l1], 0, v15\n\t"                                 \
-        "s_nop 0\n\t"                                                        \
-        "v_cndmask_b32_e64 v12, v12, v9, %[g1]\n\t"                          \
-        "v_cndmask_b32_e64 v12, v12, v11, %[l1]\n\t"                         \
-        "v_mul_f32 v9, 0x37800000, v12\n\t" /* x 2^-16 when scaled */        \
-        "v_cndmask_b32_e32 v12, v12, v9, vcc\n"                              \
         "LQ%=_" #K ":\n\t" /* v12 = sqrt(disc) */                            \
         "v_sub_f32_e64 v11, -v8, v12\n\t" /* -hb - sq */                     \
         "v_add_f32_e64 v13, -v8, v12\n\t" /* -hb + sq */                     \
@@ -1114,23 +1097,6 @@ __device__ __forceinline__ uint32_t trav_step_batched(Trav& t, const Ray& r, con
         "s_nop 0\n\t"                                                        \
         "v_cndmask_b32_e64 v12, v12, v9, %[g1]\n\t"                          \
         "v_cndmask_b32_e64 v12, v12, v11, %[l1]\n\t"                         \
-        "s_branch LQ%=_" #K "\n"                                             \
-        "LS%=_" #K ":\n\t" /* some lane: 0 <= x < 2^-96, scaled by 2^32 */   \
-        "v_mul_f32 v13, 0x4f800000, v10\n\t"                                 \
-        "v_cndmask_b32_e32 v13, v10, v13, vcc\n\t"                           \
-        "v_sqrt_f32_e32 v12, v13\n\t"                                        \
-        "v_cmp_le_f32_e64 %[pm], 0, v10\n\t" /* disc >= 0 */                 \
-        "v_add_u32_e32 v9, -1, v12\n\t"                                      \
-        "v_add_u32_e32 v11, 1, v12\n\t"                                      \
-        "v_fma_f32 v10, -v9, v12, v13\n\t"                                   \
-        "v_fma_f32 v15, -v11, v12, v13\n\t"                                  \
-        "v_cmp_ge_f32_e64 %[g1], 0, v10\n\t"                                 \
-        "v_cmp_lt_f32_e64 %[l1], 0, v15\n\t"                                 \
-        "s_nop 0\n\t"                                                        \
-        "v_cndmask_b32_e64 v12, v12, v9, %[g1]\n\t"                          \
-        "v_cndmask_b32_e64 v12, v12, v11, %[l1]\n\t"                         \
-        "v_mul_f32 v9, 0x37800000, v12\n\t" /* x 2^-16 when scaled */        \
-        "v_cndmask_b32_e32 v12, v12, v9, vcc\n"                              \
         "LQ%=_" #K ":\n\t" /* v12 = sqrt(disc) */                            \
         "v_sub_f32_e64 v11, -v8, v12\n\t" /* -hb - sq */                     \
         "v_add_f32_e64 v13, -v8, v12\n\t" /* -hb + sq */                     \
@@ -1282,6 +1248,32 @@ __device__ __forceinline__ uint32_t trav_step_batched(Trav& t, const Ray& r, con
         S(5, RTX_BOX_FAST(6)) S(6, RTX_BOX_FAST(7)) S(7, RTX_BOX_NEXT(7))
 #define RTX_WALK_BLOCK_(n) RTX_WALK_##n
 #define RTX_WALK_BLOCK(n) RTX_WALK_BLOCK_(n)
+// The sqrt of a primitive step when some lane has 0 <= disc < 2^-96 (scaled by 2^32), out of the
+// hot path: placed after the loop, it returns to the step (one taken branch fewer per step).
+#define RTX_WALK_COLD(K)                                                     \
+        "LS%=_" #K ":\n\t" /* some lane: 0 <= x < 2^-96, scaled by 2^32 */   \
+        "v_mul_f32 v13, 0x4f800000, v10\n\t"                                 \
+        "v_cndmask_b32_e32 v13, v10, v13, vcc\n\t"                           \
+        "v_sqrt_f32_e32 v12, v13\n\t"                                        \
+        "v_cmp_le_f32_e64 %[pm], 0, v10\n\t" /* disc >= 0 */                 \
+        "v_add_u32_e32 v9, -1, v12\n\t"                                      \
+        "v_add_u32_e32 v11, 1, v12\n\t"                                      \
+        "v_fma_f32 v10, -v9, v12, v13\n\t"                                   \
+        "v_fma_f32 v15, -v11, v12, v13\n\t"                                  \
+        "v_cmp_ge_f32_e64 %[g1], 0, v10\n\t"                                 \
+        "v_cmp_lt_f32_e64 %[l1], 0, v15\n\t"                                 \
+        "s_nop 0\n\t"                                                        \
+        "v_cndmask_b32_e64 v12, v12, v9, %[g1]\n\t"                          \
+        "v_cndmask_b32_e64 v12, v12, v11, %[l1]\n\t"                         \
+        "v_mul_f32 v9, 0x37800000, v12\n\t" /* x 2^-16 when scaled */        \
+        "v_cndmask_b32_e32 v12, v12, v9, vcc\n"                              \
+        "s_branch LQ%=_" #K "\n"
+#define RTX_COLD_4 RTX_WALK_COLD(0) RTX_WALK_COLD(1) RTX_WALK_COLD(2) RTX_WALK_COLD(3)
+#define RTX_COLD_5 RTX_COLD_4 RTX_WALK_COLD(4)
+#define RTX_COLD_6 RTX_COLD_5 RTX_WALK_COLD(5)
+#define RTX_COLD_8 RTX_COLD_6 RTX_WALK_COLD(6) RTX_WALK_COLD(7)
+#define RTX_COLD_BLOCK_(n) RTX_COLD_##n
+#define RTX_COLD_BLOCK(n) RTX_COLD_BLOCK_(n)
 // QUADS: the scene holds quads (RTX_WALK_STEP_PFQ; the quad table at LDS byte qbase).
 template <bool QUADS = false>
 __device__ __forceinline__ uint64_t walk_phase_asm(Trav& t, const Ray& r, uint32_t end, uint32_t kmin, float tmin,
@@ -1294,7 +1286,7 @@ __device__ __forceinline__ uint64_t walk_phase_asm(Trav& t, const Ray& r, uint32
         uint64_t qm, qs;
 #define S(K, BEND) RTX_WALK_STEP_PFQ(K, RTX_LOAD_LDS, RTX_WAIT_LDS, BEND)
         asm volatile(RTX_LOAD_LDS "v_cmp_lt_u32_e64 %[wk], %[pos], %[end]\nLW%=:\n\t" RTX_WALK_BLOCK(RTX_ASM_BLOCK_Q) RTX_WALK_VOTE
-                     "\n\ts_waitcnt lgkmcnt(0)"
+                     "\n\ts_branch LZ%=\n" RTX_COLD_BLOCK(RTX_ASM_BLOCK_Q) "LZ%=:\n\ts_waitcnt lgkmcnt(0)"
                      : RTX_WALK_OUTS, [qm] "=&s"(qm), [qs] "=&s"(qs)
                      : RTX_WALK_INS, [qbase] "s"(qbase)
                      : RTX_WALK_CLOBBERS, "v17", "v18", "v19", "v20", "v21", "v22", "v23", "v24", "v25", "v26", "v27",
@@ -1303,7 +1295,7 @@ __device__ __forceinline__ uint64_t walk_phase_asm(Trav& t, const Ray& r, uint32
     } else {
 #define S(K, BEND) RTX_WALK_STEP_PF(K, RTX_LOAD_LDS, RTX_WAIT_LDS, BEND)
         asm volatile(RTX_LOAD_LDS "v_cmp_lt_u32_e64 %[wk], %[pos], %[end]\nLW%=:\n\t" RTX_WALK_BLOCK(RTX_ASM_BLOCK) RTX_WALK_VOTE
-                     "\n\ts_waitcnt lgkmcnt(0)"
+                     "\n\ts_branch LZ%=\n" RTX_COLD_BLOCK(RTX_ASM_BLOCK) "LZ%=:\n\ts_waitcnt lgkmcnt(0)"
                      : RTX_WALK_OUTS
                      : RTX_WALK_INS
                      : RTX_WALK_CLOBBERS);
@@ -1319,6 +1311,13 @@ __device__ __forceinline__ uint64_t walk_phase_asm(Trav& t, const Ray& r, uint32
 #undef RTX_WALK_8
 #undef RTX_WALK_BLOCK_
 #undef RTX_WALK_BLOCK
+#undef RTX_WALK_COLD
+#undef RTX_COLD_4
+#undef RTX_COLD_5
+#undef RTX_COLD_6
+#undef RTX_COLD_8
+#undef RTX_COLD_BLOCK_
+#undef RTX_COLD_BLOCK
 #undef RTX_BOX_NEXT
 #undef RTX_BOX_FAST
 #undef RTX_LOAD_LDS
