@@ -961,7 +961,12 @@ __device__ __forceinline__ uint32_t trav_step_batched(Trav& t, const Ray& r, con
         "v_sub_f32 v10, %[ox], v0\n\t" /* oc = o - center */                 \
         "v_sub_f32 v11, %[oy], v1\n\t"                                       \
         "v_sub_f32 v12, %[oz], v2\n\t"                                       \
-        "v_mov_b32 v13, v4\n\t"        /* r^2 */                             \
+        "v_mul_f32 v13, v10, v10\n\t" /* c = |oc|^2 - r^2 */                 \
+        "v_mul_f32 v9, v11, v11\n\t"                                         \
+        "v_add_f32 v13, v13, v9\n\t"                                         \
+        "v_mul_f32 v9, v12, v12\n\t"                                         \
+        "v_add_f32 v13, v13, v9\n\t"                                         \
+        "v_sub_f32 v13, v13, v4\n\t"                                         \
         "v_lshrrev_b32_e32 v14, 4, %[pos]\n\t" /* this entry's index */      \
         "v_mov_b32 %[pos], v6\n\t"     /* successor */                       \
         LOAD                                                                 \
@@ -970,13 +975,7 @@ __device__ __forceinline__ uint32_t trav_step_batched(Trav& t, const Ray& r, con
         "v_add_f32 v8, v8, v9\n\t"                                           \
         "v_mul_f32 v9, %[dz], v12\n\t"                                       \
         "v_add_f32 v8, v8, v9\n\t"                                           \
-        "v_mul_f32 v10, v10, v10\n\t" /* c = |oc|^2 - r^2 */                 \
-        "v_mul_f32 v11, v11, v11\n\t"                                        \
-        "v_add_f32 v10, v10, v11\n\t"                                        \
-        "v_mul_f32 v12, v12, v12\n\t"                                        \
-        "v_add_f32 v10, v10, v12\n\t"                                        \
-        "v_sub_f32 v10, v10, v13\n\t"                                        \
-        "v_mul_f32 v10, %[a], v10\n\t" /* disc = hb*hb - a*c */              \
+        "v_mul_f32 v10, %[a], v13\n\t" /* disc = hb*hb - a*c */              \
         "v_mul_f32 v9, v8, v8\n\t"                                           \
         "v_sub_f32 v10, v9, v10\n\t"                                         \
         "v_cmp_gt_u32_e32 vcc, 0xf800000, v10\n\t" /* 0 <= x < 2^-96 (by its bits) */\
@@ -998,19 +997,15 @@ __device__ __forceinline__ uint32_t trav_step_batched(Trav& t, const Ray& r, con
         "v_mul_f32 v15, v11, %[ra]\n\t"   /* div_by: q0 = n y */             \
         "v_mul_f32 v16, v13, %[ra]\n\t"                                      \
         "v_fma_f32 v11, -%[a], v15, v11\n\t" /* e = n - a q0 */              \
-        "v_fma_f32 v13, -%[a], v16, v13\n\t"                                 \
         "v_fmac_f32 v15, v11, %[ra]\n\t" /* t1 = q0 + e y */                 \
+        "v_cmp_lt_f32_e64 %[g1], %[tmin], v15\n\t" /* tmin < t1 */           \
+        "v_fma_f32 v13, -%[a], v16, v13\n\t" /* (2 wait states for g1) */    \
         "v_fmac_f32 v16, v13, %[ra]\n\t" /* t2 */                            \
-        "v_cmp_lt_f32_e64 %[g1], %[tmin], v15\n\t"                           \
-        "v_cmp_lt_f32_e64 %[l1], v15, %[cl]\n\t"                             \
-        "v_cmp_lt_f32_e64 %[l2], %[tmin], v16\n\t"                           \
-        "s_and_b64 %[l1], %[l1], %[g1]\n\t"                                  \
-        "s_andn2_b64 %[l2], %[l2], %[g1]\n\t"                                \
-        "v_cmp_lt_f32_e64 %[wm], v16, %[cl]\n\t"                             \
-        "s_and_b64 %[l2], %[l2], %[wm]\n\t"                                  \
-        "s_or_b64 %[l1], %[l1], %[l2]\n\t"                                   \
-        "s_and_b64 %[l1], %[l1], %[pm]\n\t"                                  \
-        "v_cndmask_b32_e64 v16, v16, v15, %[g1]\n\t"                         \
+        "v_cndmask_b32_e64 v16, v16, v15, %[g1]\n\t" /* t: t1 if tmin < t1, else t2 */\
+        "v_cmp_lt_f32_e64 %[l1], %[tmin], v16\n\t" /* tmin < t < closest */  \
+        "v_cmp_lt_f32_e64 %[l2], v16, %[cl]\n\t"                             \
+        "s_and_b64 %[l1], %[l1], %[l2]\n\t"                                  \
+        "s_and_b64 %[l1], %[l1], %[pm]\n\t" /* and disc >= 0 */              \
         "v_cndmask_b32_e64 %[cl], %[cl], v16, %[l1]\n\t"                     \
         "v_cndmask_b32_e64 %[hit], %[hit], v14, %[l1]\n"                     \
         "LR%=_" #K ":\n\t"                                                   \
@@ -1103,19 +1098,15 @@ __device__ __forceinline__ uint32_t trav_step_batched(Trav& t, const Ray& r, con
         "v_mul_f32 v15, v11, %[ra]\n\t"   /* div_by: q0 = n y */             \
         "v_mul_f32 v16, v13, %[ra]\n\t"                                      \
         "v_fma_f32 v11, -%[a], v15, v11\n\t" /* e = n - a q0 */              \
-        "v_fma_f32 v13, -%[a], v16, v13\n\t"                                 \
         "v_fmac_f32 v15, v11, %[ra]\n\t" /* t1 = q0 + e y */                 \
+        "v_cmp_lt_f32_e64 %[g1], %[tmin], v15\n\t" /* tmin < t1 */           \
+        "v_fma_f32 v13, -%[a], v16, v13\n\t" /* (2 wait states for g1) */    \
         "v_fmac_f32 v16, v13, %[ra]\n\t" /* t2 */                            \
-        "v_cmp_lt_f32_e64 %[g1], %[tmin], v15\n\t"                           \
-        "v_cmp_lt_f32_e64 %[l1], v15, %[cl]\n\t"                             \
-        "v_cmp_lt_f32_e64 %[l2], %[tmin], v16\n\t"                           \
-        "s_and_b64 %[l1], %[l1], %[g1]\n\t"                                  \
-        "s_andn2_b64 %[l2], %[l2], %[g1]\n\t"                                \
-        "v_cmp_lt_f32_e64 %[wm], v16, %[cl]\n\t"                             \
-        "s_and_b64 %[l2], %[l2], %[wm]\n\t"                                  \
-        "s_or_b64 %[l1], %[l1], %[l2]\n\t"                                   \
-        "s_and_b64 %[l1], %[l1], %[pm]\n\t"                                  \
-        "v_cndmask_b32_e64 v16, v16, v15, %[g1]\n\t"                         \
+        "v_cndmask_b32_e64 v16, v16, v15, %[g1]\n\t" /* t: t1 if tmin < t1, else t2 */\
+        "v_cmp_lt_f32_e64 %[l1], %[tmin], v16\n\t" /* tmin < t < closest */  \
+        "v_cmp_lt_f32_e64 %[l2], v16, %[cl]\n\t"                             \
+        "s_and_b64 %[l1], %[l1], %[l2]\n\t"                                  \
+        "s_and_b64 %[l1], %[l1], %[pm]\n\t" /* and disc >= 0 */              \
         "v_cndmask_b32_e64 %[cl], %[cl], v16, %[l1]\n\t"                     \
         "v_cndmask_b32_e64 %[hit], %[hit], v14, %[l1]\n"                     \
         "LT%=_" #K ":\n\t"                                                   \
