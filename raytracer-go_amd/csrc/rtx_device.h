@@ -903,7 +903,8 @@ __device__ __forceinline__ uint32_t trav_step_batched(Trav& t, const Ray& r, con
 //     after, a path taken only when some lane has 0 <= disc < 2^-96.  (The expansion's last
 //     step, passing +-0 and +inf through, is left out: v_sqrt returns them exactly and both
 //     neighbour residuals are then NaN or a zero, which keeps them.)  Both roots by div_by;
-//     the first root when tmin < t1, else the second (hittables.go:110-114); disc >= 0.
+//     the first root when tmin < t1, else the second (hittables.go:110-114).  disc < 0 needs no
+//     test of its own (:104): v_sqrt returns NaN there, and NaN roots fail tmin < t.
 // gfx950 hazards: a VALU-written SGPR/VCC read as a v_cndmask mask by the next VALU needs
 // s_nop 1; a v_sqrt result read by the next VALU needs s_nop 0 (as the compiler emits them).
 // Entry read of the prefetching walk, under the current exec: both halves from the fixed layout.
@@ -978,10 +979,9 @@ __device__ __forceinline__ uint32_t trav_step_batched(Trav& t, const Ray& r, con
         "v_mul_f32 v10, %[a], v13\n\t" /* disc = hb*hb - a*c */              \
         "v_mul_f32 v9, v8, v8\n\t"                                           \
         "v_sub_f32 v10, v9, v10\n\t"                                         \
-        "v_cmp_gt_u32_e32 vcc, 0xf800000, v10\n\t" /* 0 <= x < 2^-96 (by its bits) */\
-        "s_cbranch_vccnz LS%=_" #K "\n\t"                                    \
-        "v_sqrt_f32_e32 v12, v10\n\t" /* every lane: x >= 2^-96, -0 or x < 0 */\
-        "v_cmp_le_f32_e64 %[pm], 0, v10\n\t" /* disc >= 0 (fills the v_sqrt hazard slot) */\
+        "v_sqrt_f32_e32 v12, v10\n\t"                                        \
+        "v_cmp_gt_u32_e32 vcc, 0xf800000, v10\n\t" /* 0 <= x < 2^-96 (by its bits; in the v_sqrt hazard slot) */\
+        "s_cbranch_vccnz LS%=_" #K "\n\t" /* here: x >= 2^-96, -0 or x < 0 (NaN root: no hit) */\
         "v_add_u32_e32 v9, -1, v12\n\t"                                      \
         "v_add_u32_e32 v11, 1, v12\n\t"                                      \
         "v_fma_f32 v13, -v9, v12, v10\n\t"                                   \
@@ -1004,8 +1004,7 @@ __device__ __forceinline__ uint32_t trav_step_batched(Trav& t, const Ray& r, con
         "v_cndmask_b32_e64 v16, v16, v15, %[g1]\n\t" /* t: t1 if tmin < t1, else t2 */\
         "v_cmp_lt_f32_e64 %[l1], %[tmin], v16\n\t" /* tmin < t < closest */  \
         "v_cmp_lt_f32_e64 %[l2], v16, %[cl]\n\t"                             \
-        "s_and_b64 %[l1], %[l1], %[l2]\n\t"                                  \
-        "s_and_b64 %[l1], %[l1], %[pm]\n\t" /* and disc >= 0 */              \
+        "s_and_b64 %[l1], %[l1], %[l2]\n\t" /* (disc < 0: NaN roots fail) */ \
         "v_cndmask_b32_e64 %[cl], %[cl], v16, %[l1]\n\t"                     \
         "v_cndmask_b32_e64 %[hit], %[hit], v14, %[l1]\n"                     \
         "LR%=_" #K ":\n\t"                                                   \
@@ -1079,10 +1078,9 @@ __device__ __forceinline__ uint32_t trav_step_batched(Trav& t, const Ray& r, con
         "v_mul_f32 v10, %[a], v10\n\t" /* disc = hb*hb - a*c */              \
         "v_mul_f32 v9, v8, v8\n\t"                                           \
         "v_sub_f32 v10, v9, v10\n\t"                                         \
-        "v_cmp_gt_u32_e32 vcc, 0xf800000, v10\n\t" /* 0 <= x < 2^-96 (by its bits) */\
-        "s_cbranch_vccnz LS%=_" #K "\n\t"                                    \
-        "v_sqrt_f32_e32 v12, v10\n\t" /* every lane: x >= 2^-96, -0 or x < 0 */\
-        "v_cmp_le_f32_e64 %[pm], 0, v10\n\t" /* disc >= 0 (fills the v_sqrt hazard slot) */\
+        "v_sqrt_f32_e32 v12, v10\n\t"                                        \
+        "v_cmp_gt_u32_e32 vcc, 0xf800000, v10\n\t" /* 0 <= x < 2^-96 (by its bits; in the v_sqrt hazard slot) */\
+        "s_cbranch_vccnz LS%=_" #K "\n\t" /* here: x >= 2^-96, -0 or x < 0 (NaN root: no hit) */\
         "v_add_u32_e32 v9, -1, v12\n\t"                                      \
         "v_add_u32_e32 v11, 1, v12\n\t"                                      \
         "v_fma_f32 v13, -v9, v12, v10\n\t"                                   \
@@ -1105,8 +1103,7 @@ __device__ __forceinline__ uint32_t trav_step_batched(Trav& t, const Ray& r, con
         "v_cndmask_b32_e64 v16, v16, v15, %[g1]\n\t" /* t: t1 if tmin < t1, else t2 */\
         "v_cmp_lt_f32_e64 %[l1], %[tmin], v16\n\t" /* tmin < t < closest */  \
         "v_cmp_lt_f32_e64 %[l2], v16, %[cl]\n\t"                             \
-        "s_and_b64 %[l1], %[l1], %[l2]\n\t"                                  \
-        "s_and_b64 %[l1], %[l1], %[pm]\n\t" /* and disc >= 0 */              \
+        "s_and_b64 %[l1], %[l1], %[l2]\n\t" /* (disc < 0: NaN roots fail) */ \
         "v_cndmask_b32_e64 %[cl], %[cl], v16, %[l1]\n\t"                     \
         "v_cndmask_b32_e64 %[hit], %[hit], v14, %[l1]\n"                     \
         "LT%=_" #K ":\n\t"                                                   \
@@ -1246,7 +1243,7 @@ __device__ __forceinline__ uint32_t trav_step_batched(Trav& t, const Ray& r, con
         "v_mul_f32 v13, 0x4f800000, v10\n\t"                                 \
         "v_cndmask_b32_e32 v13, v10, v13, vcc\n\t"                           \
         "v_sqrt_f32_e32 v12, v13\n\t"                                        \
-        "v_cmp_le_f32_e64 %[pm], 0, v10\n\t" /* disc >= 0 */                 \
+        "s_nop 0\n\t"                                                        \
         "v_add_u32_e32 v9, -1, v12\n\t"                                      \
         "v_add_u32_e32 v11, 1, v12\n\t"                                      \
         "v_fma_f32 v10, -v9, v12, v13\n\t"                                   \
