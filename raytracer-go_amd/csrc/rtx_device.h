@@ -912,25 +912,28 @@ __device__ __forceinline__ uint32_t trav_step_batched(Trav& t, const Ray& r, con
         "ds_read_b128 v[0:3], %[pos]\n\t"                                    \
         "ds_read_b128 v[4:7], %[pos] offset:32768\n\t" /* LDS_B */
 #define RTX_WAIT_LDS "s_waitcnt lgkmcnt(0)\n\t"
-// End of a box step: back to the full wave, then the next step's header (RTX_BOX_NEXT), or straight
-// to its node test with its primitive mask taken here (RTX_BOX_FAST: after a box step the next step
-// skips the primitive-count test and runs the box tests again while a node lane is left).
+// End of a box step: back to the full wave, then the next step's header (RTX_BOX_NEXT), or a box run
+// (RTX_BOX_FAST): the lanes of this step still on a node test their next box at once, under the
+// same exec minus the lanes now on a primitive (only these lanes moved), without the next step's
+// primitive-count test; back to the full wave and the header when no node lane is left.
 #define RTX_BOX_NEXT(K) "s_mov_b64 exec, %[save]\n\t" "s_branch LE%=_" #K "\n"
-#define RTX_BOX_FAST(KN)                                                     \
+#define RTX_BOX_FAST(K, KN)                                                  \
+        "v_cmp_gt_u32_e64 %[pm], %[pe], %[pos]\n\t" /* (exec: node lanes) now on a primitive */\
+        "s_andn2_b64 exec, exec, %[pm]\n\t" /* the node lanes left (scc) */  \
+        "s_cbranch_scc1 LB%=_" #KN "\n\t"                                    \
         "s_mov_b64 exec, %[save]\n\t"                                        \
-        "v_cmp_gt_u32_e64 %[pm], %[pe], %[pos]\n\t"                          \
-        "s_branch LN%=_" #KN "\n"
+        "s_branch LE%=_" #K "\n"
 #define RTX_WALK_STEP_PF(K, LOAD, WAIT, BEND)                                      \
         "v_cmp_gt_u32_e64 %[pm], %[pe], %[pos]\n\t" /* primitive: pos < prim_end */\
         "s_bcnt1_i32_b64 %[cnt], %[pm]\n\t"                                  \
         "s_cmp_ge_u32 %[cnt], %[kmin]\n\t"                                   \
         "s_cbranch_scc1 LP%=_" #K "\n\t"                                     \
-        "LN%=_" #K ":\n\t"                                                   \
         "s_andn2_b64 %[wm], %[wk], %[pm]\n\t" /* scc: a node lane */         \
         "s_cbranch_scc0 LP%=_" #K "\n\t"                                     \
         /* ---- box tests on the node lanes, then their next entries */      \
-        WAIT                                                                 \
         "s_and_saveexec_b64 %[save], %[wm]\n\t"                              \
+        "LB%=_" #K ":\n\t" /* a box run continues here, exec = its node lanes */\
+        WAIT                                                                 \
         "v_sub_f32 v0, v0, %[ox]\n\t"                                        \
         "v_sub_f32 v4, v4, %[ox]\n\t"                                        \
         "v_sub_f32 v1, v1, %[oy]\n\t"                                        \
@@ -1015,12 +1018,12 @@ __device__ __forceinline__ uint32_t trav_step_batched(Trav& t, const Ray& r, con
         "s_bcnt1_i32_b64 %[cnt], %[pm]\n\t"                                  \
         "s_cmp_ge_u32 %[cnt], %[kmin]\n\t"                                   \
         "s_cbranch_scc1 LP%=_" #K "\n\t"                                     \
-        "LN%=_" #K ":\n\t"                                                   \
         "s_andn2_b64 %[wm], %[wk], %[pm]\n\t" /* scc: a node lane */         \
         "s_cbranch_scc0 LP%=_" #K "\n\t"                                     \
         /* ---- box tests on the node lanes, then their next entries */      \
-        WAIT                                                                 \
         "s_and_saveexec_b64 %[save], %[wm]\n\t"                              \
+        "LB%=_" #K ":\n\t" /* a box run continues here, exec = its node lanes */\
+        WAIT                                                                 \
         "v_sub_f32 v0, v0, %[ox]\n\t"                                        \
         "v_sub_f32 v4, v4, %[ox]\n\t"                                        \
         "v_sub_f32 v1, v1, %[oy]\n\t"                                        \
@@ -1225,15 +1228,15 @@ __device__ __forceinline__ uint32_t trav_step_batched(Trav& t, const Ray& r, con
 #ifndef RTX_ASM_BLOCK_Q  // scenes with quads
 #define RTX_ASM_BLOCK_Q 4
 #endif
-#define RTX_WALK_4 S(0, RTX_BOX_FAST(1)) S(1, RTX_BOX_FAST(2)) S(2, RTX_BOX_FAST(3)) S(3, RTX_BOX_NEXT(3))
+#define RTX_WALK_4 S(0, RTX_BOX_FAST(0, 1)) S(1, RTX_BOX_FAST(1, 2)) S(2, RTX_BOX_FAST(2, 3)) S(3, RTX_BOX_NEXT(3))
 #define RTX_WALK_5 \
-    S(0, RTX_BOX_FAST(1)) S(1, RTX_BOX_FAST(2)) S(2, RTX_BOX_FAST(3)) S(3, RTX_BOX_FAST(4)) S(4, RTX_BOX_NEXT(4))
+    S(0, RTX_BOX_FAST(0, 1)) S(1, RTX_BOX_FAST(1, 2)) S(2, RTX_BOX_FAST(2, 3)) S(3, RTX_BOX_FAST(3, 4)) S(4, RTX_BOX_NEXT(4))
 #define RTX_WALK_6                                                                                          \
-    S(0, RTX_BOX_FAST(1)) S(1, RTX_BOX_FAST(2)) S(2, RTX_BOX_FAST(3)) S(3, RTX_BOX_FAST(4)) S(4, RTX_BOX_FAST(5)) \
+    S(0, RTX_BOX_FAST(0, 1)) S(1, RTX_BOX_FAST(1, 2)) S(2, RTX_BOX_FAST(2, 3)) S(3, RTX_BOX_FAST(3, 4)) S(4, RTX_BOX_FAST(4, 5)) \
         S(5, RTX_BOX_NEXT(5))
 #define RTX_WALK_8                                                                                          \
-    S(0, RTX_BOX_FAST(1)) S(1, RTX_BOX_FAST(2)) S(2, RTX_BOX_FAST(3)) S(3, RTX_BOX_FAST(4)) S(4, RTX_BOX_FAST(5)) \
-        S(5, RTX_BOX_FAST(6)) S(6, RTX_BOX_FAST(7)) S(7, RTX_BOX_NEXT(7))
+    S(0, RTX_BOX_FAST(0, 1)) S(1, RTX_BOX_FAST(1, 2)) S(2, RTX_BOX_FAST(2, 3)) S(3, RTX_BOX_FAST(3, 4)) S(4, RTX_BOX_FAST(4, 5)) \
+        S(5, RTX_BOX_FAST(5, 6)) S(6, RTX_BOX_FAST(6, 7)) S(7, RTX_BOX_NEXT(7))
 #define RTX_WALK_BLOCK_(n) RTX_WALK_##n
 #define RTX_WALK_BLOCK(n) RTX_WALK_BLOCK_(n)
 // The sqrt of a primitive step when some lane has 0 <= disc < 2^-96 (scaled by 2^32), out of the
