@@ -58,6 +58,7 @@ struct DeviceCopy {
     unsigned long long* counters = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     uint32_t hot = 0;  // entries stored first and cached in LDS by v3 (scenes too big for the LDS copy)
+    uint32_t n_textures = 0;  // device textures: those materials read (checkered, image, noise)
     uint32_t start = 0;     // walk position of the first entry of the walk (the root)
     uint32_t prim_end = 0;  // scenes in the LDS copy: primitives stored first, below this position
 };
@@ -406,14 +407,25 @@ int upload_copy(rtx_scene* s, DeviceCopy& c) {
         if (!s->quadtab.empty()) std::memcpy(&soa[8 * m], s->quadtab.data(), s->quadtab.size() * sizeof(float));
         HIP_TRY(hipMemcpy(c.entries, soa.data(), soa.size() * sizeof(float), hipMemcpyHostToDevice));
     }
-    {  // device materials: a Lambertian or DiffuseLight with a SolidColor texture carries the
-       // colour itself (rtxd::RTX_DEV_TEX_INLINE), so shading reads no texture record
+    // device materials: a Lambertian or DiffuseLight with a SolidColor texture carries the
+    // colour itself (rtxd::RTX_DEV_TEX_INLINE), so shading reads no texture record; the other
+    // textures they read are numbered anew in the device texture table, which holds only those
+    // (small enough for the LDS copy: randSpheres' 488 SolidColors leave one checkered texture)
+    std::vector<rtx_texture> dt;
+    {
         std::vector<rtx_material> dm(s->materials);
+        std::vector<int64_t> renum(s->textures.size(), -1);
         for (rtx_material& m : dm) {
             if ((m.type == RTX_MAT_LAMBERTIAN || m.type == RTX_MAT_DIFFUSE_LIGHT) &&
                 s->textures[m.texture].type == RTX_TEX_SOLID) {
                 std::memcpy(m.albedo, s->textures[m.texture].even, sizeof(m.albedo));
                 m.texture = rtxd::RTX_DEV_TEX_INLINE;
+            } else if (m.type == RTX_MAT_LAMBERTIAN || m.type == RTX_MAT_DIFFUSE_LIGHT) {
+                if (renum[m.texture] < 0) {
+                    renum[m.texture] = (int64_t)dt.size();
+                    dt.push_back(s->textures[m.texture]);
+                }
+                m.texture = (uint32_t)renum[m.texture];
             }
             if (m.type == RTX_MAT_DIELECTRIC) {  // (albedo unused: attenuation is (1,1,1))
                 // per-material float32 quotients of materials.go:98, 116-117, computed once here
@@ -430,11 +442,11 @@ int upload_copy(rtx_scene* s, DeviceCopy& c) {
     }
     {  // device textures: a Checkered carries invScale = float32(1 / scale) (materials.go:128) in `pad`,
        // the IEEE quotient computed once here instead of per lookup
-        std::vector<rtx_texture> dt(s->textures);
         for (rtx_texture& t : dt)
             if (t.type == RTX_TEX_CHECKERED) t.pad = 1.0f / t.scale;
         HIP_TRY(hipMalloc(&c.textures, std::max<size_t>(1, dt.size()) * sizeof(rtx_texture)));
         if (!dt.empty()) HIP_TRY(hipMemcpy(c.textures, dt.data(), dt.size() * sizeof(rtx_texture), hipMemcpyHostToDevice));
+        c.n_textures = (uint32_t)dt.size();
     }
     HIP_TRY(hipMalloc(&c.texels, std::max<size_t>(1, s->texels.size()) * sizeof(uint32_t)));
     if (!s->texels.empty())
@@ -529,6 +541,7 @@ rtxd::Params make_params(const rtx_scene* s, const DeviceCopy* c, const rtx_came
     p.n_materials = (uint32_t)s->materials.size();
     p.materials = c->materials;
     p.textures = c->textures;
+    p.n_textures = c->n_textures;
     p.texels = c->texels;
     p.cam = *cam;
     p.seed = seed;

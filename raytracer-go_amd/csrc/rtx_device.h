@@ -366,6 +366,7 @@ struct SceneRef {
     const float4* __restrict__ b;
     const float4* __restrict__ q;          // quad table, 4 float4 per quad (rtx_layout.h)
     const rtx_material* __restrict__ m;    // device materials (RTX_DEV_TEX_INLINE recoding)
+    const rtx_texture* __restrict__ tx;    // device textures (only those materials reference; after m in LDS)
     // v3 on a scene too big for LDS: its first `hot` bytes of positions (the top levels,
     // stored first) are also in LDS, halves at la / lb (load_entry<HYB>)
     const float4* la;
@@ -375,28 +376,34 @@ struct SceneRef {
 };
 __device__ __forceinline__ SceneRef scene_ref(const float4* base, uint32_t n_entries, const rtx_material* mats) {
     const uint32_t m = n_entries + 1;  // + the sentinel
-    return SceneRef{base, base + m, base + 2 * m, mats, nullptr, nullptr, 0u, 0u};
+    return SceneRef{base, base + m, base + 2 * m, mats, nullptr, nullptr, nullptr, 0u, 0u};
 }
 // v3's LDS layout: the 'a' halves from LDS byte 0, the 'b' halves from byte LDS_B, the
 // quad table after them.  A walk position is then the LDS address of its 'a' half and
 // both halves load from one register (ds_read_b128 offset:0 / offset:LDS_B): no address
-// arithmetic per step.  The material table goes into the gap after the 'a' halves when
-// it fits there (randSpheres: 15.9 KB of halves + 15.6 KB of materials < 32 KB), else
-// after the quad table.
+// arithmetic per step.  The material table, then the texture table (48 B per texture that a
+// material reads: checkered, image, noise), go into the gap after the 'a' halves when they fit
+// there (randSpheres: 15.5 KB of halves + 15.6 KB of materials + one checkered texture < 32 KB),
+// else after the quad table.  (The texture record in LDS: a texture lookup used to be a chain of
+// global loads, each waiting for the wave's outstanding sample-scratch stores.)
 constexpr uint32_t LDS_B = 32768;
-__host__ __device__ __forceinline__ uint32_t lds_mat_offset(uint32_t n_entries, uint32_t n_quads, uint32_t n_mats) {
+__host__ __device__ __forceinline__ uint32_t lds_mat_offset(uint32_t n_entries, uint32_t n_quads, uint32_t n_mats,
+                                                            uint32_t n_tex) {
     const uint32_t halves = (n_entries + 1) * 16;
-    return halves + n_mats * 32 <= LDS_B ? halves : LDS_B + halves + n_quads * 64;
+    return halves + n_mats * 32 + n_tex * 48 <= LDS_B ? halves : LDS_B + halves + n_quads * 64;
 }
-__host__ __device__ __forceinline__ uint32_t lds_fixed_bytes(uint32_t n_entries, uint32_t n_quads, uint32_t n_mats) {
-    const uint32_t end = LDS_B + (n_entries + 1) * 16 + n_quads * 64, mo = lds_mat_offset(n_entries, n_quads, n_mats);
-    return mo < LDS_B ? end : mo + n_mats * 32;
+__host__ __device__ __forceinline__ uint32_t lds_fixed_bytes(uint32_t n_entries, uint32_t n_quads, uint32_t n_mats,
+                                                             uint32_t n_tex) {
+    const uint32_t end = LDS_B + (n_entries + 1) * 16 + n_quads * 64,
+                   mo = lds_mat_offset(n_entries, n_quads, n_mats, n_tex);
+    return mo < LDS_B ? end : mo + n_mats * 32 + n_tex * 48;
 }
 __device__ __forceinline__ SceneRef scene_ref_fixed(const float4* lds, uint32_t n_entries, uint32_t n_quads,
-                                                    uint32_t n_mats) {
+                                                    uint32_t n_mats, uint32_t n_tex) {
+    const uint32_t mo = lds_mat_offset(n_entries, n_quads, n_mats, n_tex) / 16;
     return SceneRef{lds, lds + LDS_B / 16, lds + LDS_B / 16 + n_entries + 1,
-                    reinterpret_cast<const rtx_material*>(lds + lds_mat_offset(n_entries, n_quads, n_mats) / 16),
-                    nullptr, nullptr, 0u, 0u};
+                    reinterpret_cast<const rtx_material*>(lds + mo),
+                    reinterpret_cast<const rtx_texture*>(lds + mo + 2 * n_mats), nullptr, nullptr, 0u, 0u};
 }
 // The LDS cache of a scene too big for the fixed layout: its first entries (whole top
 // levels, rtx_capi.hip ensure_device) in the fixed layout's places.  Up to HOT_ENTRIES_8W
@@ -425,7 +432,8 @@ struct Params {
     uint32_t n_quads;
     uint32_t n_materials;
     const rtx_material* materials;
-    const rtx_texture* textures;
+    const rtx_texture* textures;   // only the textures materials reference (ensure_device compacts them)
+    uint32_t n_textures;
     const uint32_t* texels;
     rtx_camera cam;
     uint64_t seed;
@@ -501,8 +509,9 @@ __device__ __forceinline__ V3 pixel_base(const rtx_camera& c, uint32_t x, uint32
 // texture (its evaluation is an out-of-line call that costs the caller registers, so
 // only kernels built for such scenes contain it).
 template <bool COUNT, bool NOISE = false>
-__device__ __forceinline__ V3 texture_value(const Params& p, uint32_t ti, float u, float v, V3 pt, Counters& cnt) {
-    const rtx_texture& t = p.textures[ti];
+__device__ __forceinline__ V3 texture_value(const Params& p, const SceneRef E, uint32_t ti, float u, float v, V3 pt,
+                                            Counters& cnt) {
+    const rtx_texture& t = E.tx[ti];
     if (t.type == RTX_TEX_SOLID) return v3(t.even[0], t.even[1], t.even[2]);
     if (t.type == RTX_TEX_CHECKERED) {
         const float inv = t.pad;  // float32(1 / scale), materials.go:128 (computed on the host, upload_copy)
@@ -1358,7 +1367,7 @@ __device__ __forceinline__ bool shade(const Params& p, const SceneRef E, const T
     float u = 0.0f, v = 0.0f;
     const bool inl = m.texture == RTX_DEV_TEX_INLINE;  // SolidColor, colour in m.albedo
     if (p.has_uv && (m.type == RTX_MAT_LAMBERTIAN || m.type == RTX_MAT_DIFFUSE_LIGHT) && !inl &&
-        p.textures[m.texture].type == RTX_TEX_IMAGE) {           // only an image texture reads UV
+        E.tx[m.texture].type == RTX_TEX_IMAGE) {           // only an image texture reads UV
         if (quad) {  // (alpha, beta) of the hit, recomputed as quad_test did (hittables.go:181-183)
             const V3 php = sub(pt, v3(q0.x, q0.y, q0.z));
             const V3 w = v3(q3.x, q3.y, q3.z);
@@ -1393,7 +1402,7 @@ __device__ __forceinline__ bool shade(const Params& p, const SceneRef E, const T
             V3 dir = add(n, s);
             if (near_zero(dir)) dir = n;
             const V3 att = inl ? v3(m.albedo[0], m.albedo[1], m.albedo[2])
-                               : texture_value<COUNT, NOISE>(p, m.texture, u, v, pt, cnt);
+                               : texture_value<COUNT, NOISE>(p, E, m.texture, u, v, pt, cnt);
             thr = mul(thr, att);
             r = Ray{pt, dir};
             return false;
@@ -1425,7 +1434,7 @@ __device__ __forceinline__ bool shade(const Params& p, const SceneRef E, const T
         return false;
     }
     // DiffuseLight: emit, never scatters (materials.go:303-313)
-    const V3 em = inl ? v3(m.albedo[0], m.albedo[1], m.albedo[2]) : texture_value<COUNT, NOISE>(p, m.texture, u, v, pt, cnt);
+    const V3 em = inl ? v3(m.albedo[0], m.albedo[1], m.albedo[2]) : texture_value<COUNT, NOISE>(p, E, m.texture, u, v, pt, cnt);
     color = add(acc, mul(thr, em));
     return true;
 }

@@ -182,14 +182,18 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
             lds_entries[LDS_B / 16 + t] = p.entries[m + t];
         }
         for (uint32_t t = threadIdx.x; t < nq4; t += WAVE_BLOCK) lds_entries[LDS_B / 16 + m + t] = p.entries[2 * m + t];
-        const uint32_t mo = lds_mat_offset(p.n_entries, p.n_quads, p.n_materials) / 16;
+        const uint32_t mo = lds_mat_offset(p.n_entries, p.n_quads, p.n_materials, p.n_textures) / 16;
         const float4* mg = reinterpret_cast<const float4*>(p.materials);
         for (uint32_t t = threadIdx.x; t < 2 * p.n_materials; t += WAVE_BLOCK) lds_entries[mo + t] = mg[t];
+        const float4* tg = reinterpret_cast<const float4*>(p.textures);  // 48 B = 3 float4 each
+        for (uint32_t t = threadIdx.x; t < 3 * p.n_textures; t += WAVE_BLOCK)
+            lds_entries[mo + 2 * p.n_materials + t] = tg[t];
         __syncthreads();
-        E = scene_ref_fixed(lds_entries, p.n_entries, p.n_quads, p.n_materials);
+        E = scene_ref_fixed(lds_entries, p.n_entries, p.n_quads, p.n_materials, p.n_textures);
         E.prim_end = p.prim_end;
     } else {
         E = scene_ref(p.entries, p.n_entries, p.materials);
+        E.tx = p.textures;
         if constexpr (HYB) {  // the scene's top levels, stored first, cached in LDS (fixed layout)
             if ((uint32_t)(uintptr_t)(__attribute__((address_space(3))) float4*)lds_entries != 0u) __builtin_trap();
             const uint32_t m = p.n_entries + 1;
@@ -406,7 +410,7 @@ hipError_t launch_items(Params p, bool use_lds, hipStream_t stream) {
     // a scene too big for LDS: its top levels (p.n_hot entries) cached in LDS when the
     // device layout stored them first (RTX_HOT_ENTRIES=0 turns that off)
     const bool hyb = !use_lds && p.n_hot > 0 && !NOISE;
-    const size_t shmem = use_lds ? lds_fixed_bytes(p.n_entries, p.n_quads, p.n_materials)
+    const size_t shmem = use_lds ? lds_fixed_bytes(p.n_entries, p.n_quads, p.n_materials, p.n_textures)
                                  : (hyb ? lds_hot_bytes(p.n_hot) : 0);
     const auto kern = use_lds ? render_items<COUNT, true, QUADS, NOISE, WAVES, MINW>
                               : (hyb ? render_items<COUNT, false, QUADS, NOISE, WAVES, MINW, !NOISE>
@@ -479,7 +483,7 @@ hipError_t launch_render(const Params& p, uint32_t flags, hipStream_t stream) {
     // the whole scene in LDS (fixed layout) when its 'a' halves fit below LDS_B and all of it
     // in 64 KB; else from HBM, with the top levels cached in LDS when stored first (n_hot)
     const bool use_lds = !(flags & RTX_FLAG_NO_LDS) && (p.n_entries + 1) * 16 <= LDS_B &&
-                         lds_fixed_bytes(p.n_entries, p.n_quads, p.n_materials) <= LDS_MAX_BYTES;
+                         lds_fixed_bytes(p.n_entries, p.n_quads, p.n_materials, p.n_textures) <= LDS_MAX_BYTES;
     return count ? launch_items_for<true>(p, use_lds, stream) : launch_items_for<false>(p, use_lds, stream);
 }
 
