@@ -676,17 +676,29 @@ template <bool FIXED, bool HYB = false>
 __device__ __forceinline__ void load_entry(const SceneRef E, uint32_t pos, float4& ea, float4& eb) {
     if constexpr (HYB) {
         // The top levels from the LDS cache (v3's fixed layout at LDS address 0), the rest from
-        // HBM.  A branch, not one flat load for both: a wave whose lanes are all on one side
-        // runs one kind of load, and a flat load cost +4.6 % over a global one (config 4).
-        if (pos < E.hot) {
-            asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %2 offset:%3\n\ts_waitcnt lgkmcnt(0)"
-                         : "=&v"(ea), "=&v"(eb)
-                         : "v"(pos), "i"(LDS_B));
-        } else {
-            ea = *reinterpret_cast<const float4*>(reinterpret_cast<const char*>(E.a) + pos);
-            eb = *reinterpret_cast<const float4*>(reinterpret_cast<const char*>(E.b) + pos);
-            asm volatile("" ::"v"(ea.x), "v"(ea.y), "v"(ea.z), "v"(ea.w), "v"(eb.x), "v"(eb.y), "v"(eb.z), "v"(eb.w));
-        }
+        // HBM: the global reads of the lanes past the cache and the LDS reads of the others are
+        // both issued, under their exec masks, before one wait, so a wave with lanes on both sides
+        // waits for the slower read only (two branches, each with its own wait, paid both in
+        // turn).  The global reads take the table bases in SGPRs and the position as the offset.
+        // (A flat load for both cost +4.6 % over a global one, config 4.)
+        uint64_t sv, m;
+        asm volatile("s_mov_b64 %[sv], exec\n\t"
+                     "v_cmp_gt_u32_e64 %[m], %[hot], %[pos]\n\t" /* the LDS cache's lanes */
+                     "s_andn2_b64 exec, %[sv], %[m]\n\t"
+                     "s_cbranch_execz LG%=\n\t"
+                     "global_load_dwordx4 %[ea], %[pos], %[ba]\n\t"
+                     "global_load_dwordx4 %[eb], %[pos], %[bb]\n"
+                     "LG%=:\n\t"
+                     "s_and_b64 exec, %[sv], %[m]\n\t"
+                     "s_cbranch_execz LL%=\n\t"
+                     "ds_read_b128 %[ea], %[pos]\n\t"
+                     "ds_read_b128 %[eb], %[pos] offset:%[lb]\n"
+                     "LL%=:\n\t"
+                     "s_mov_b64 exec, %[sv]\n\t"
+                     "s_waitcnt vmcnt(0) lgkmcnt(0)"
+                     : [ea] "=&v"(ea), [eb] "=&v"(eb), [sv] "=&s"(sv), [m] "=&s"(m)
+                     : [pos] "v"(pos), [hot] "s"(E.hot), [ba] "s"(E.a), [bb] "s"(E.b), [lb] "i"(LDS_B)
+                     : "scc");
     } else if constexpr (FIXED) {
         asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %2 offset:%3\n\ts_waitcnt lgkmcnt(0)"
                      : "=&v"(ea), "=&v"(eb)
