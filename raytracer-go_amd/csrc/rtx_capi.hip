@@ -87,6 +87,50 @@ struct PpmScratch {
 std::mutex g_ppm_mu;
 std::map<int, PpmScratch> g_ppm;
 
+// Two pinned host stages for copies into the caller's (pageable) buffer, allocated on first
+// use and freed by rtx_release_device_memory(-1): the DMA of chunk k+1 runs while the CPU copies
+// chunk k out.  (hipMemcpy into pageable memory stages through the runtime's own buffers: the
+// 24.9 MB image of C2 cost ~7 ms that way.)
+struct HostStage {
+    void* buf[2] = {nullptr, nullptr};
+    hipEvent_t ev[2] = {nullptr, nullptr};
+};
+constexpr size_t kStageBytes = 4u << 20;
+std::mutex g_stage_mu;
+HostStage g_stage;
+
+hipError_t copy_to_host(void* dst, const void* src, size_t bytes, hipStream_t st) {
+    std::lock_guard<std::mutex> lk(g_stage_mu);
+    hipError_t e = hipSuccess;
+    for (int i = 0; i < 2 && e == hipSuccess; ++i) {
+        if (!g_stage.buf[i]) e = hipHostMalloc(&g_stage.buf[i], kStageBytes, hipHostMallocDefault);
+        if (e == hipSuccess && !g_stage.ev[i]) e = hipEventCreateWithFlags(&g_stage.ev[i], hipEventDisableTiming);
+    }
+    const size_t n = (bytes + kStageBytes - 1) / kStageBytes;
+    auto len = [&](size_t k) { return std::min(kStageBytes, bytes - k * kStageBytes); };
+    for (size_t k = 0; k <= n && e == hipSuccess; ++k) {
+        if (k < n) {  // chunk k into stage k % 2 (its previous chunk, k - 2, is already copied out)
+            e = hipMemcpyAsync(g_stage.buf[k % 2], static_cast<const char*>(src) + k * kStageBytes, len(k),
+                               hipMemcpyDeviceToHost, st);
+            if (e == hipSuccess) e = hipEventRecord(g_stage.ev[k % 2], st);
+        }
+        if (k >= 1 && e == hipSuccess) {  // chunk k - 1 out of its stage while chunk k is in flight
+            e = hipEventSynchronize(g_stage.ev[(k - 1) % 2]);
+            if (e == hipSuccess)
+                std::memcpy(static_cast<char*>(dst) + (k - 1) * kStageBytes, g_stage.buf[(k - 1) % 2], len(k - 1));
+        }
+    }
+    return e;
+}
+
+void release_stage_locked() {
+    for (int i = 0; i < 2; ++i) {
+        if (g_stage.ev[i]) (void)hipEventDestroy(g_stage.ev[i]);
+        if (g_stage.buf[i]) (void)hipHostFree(g_stage.buf[i]);
+    }
+    g_stage = HostStage{};
+}
+
 // Free a device's scratch buffers (g_scratch_mu held).
 void release_scratch_locked(int device) {
     auto it = g_scratch.find(device);
@@ -958,8 +1002,7 @@ int rtx_render(rtx_scene* s, const rtx_camera* cam, uint64_t seed, int n_gpus, f
                                gathered, img, (uint32_t)n, R, H, W * 3);
             hipError_t e = hipGetLastError();
             if (e == hipSuccess) e = hipEventRecord(g1, streams[0]);
-            if (e == hipSuccess) e = hipMemcpyAsync(out_rgb, img, total_floats * sizeof(float), hipMemcpyDeviceToHost, streams[0]);
-            if (e == hipSuccess) e = hipStreamSynchronize(streams[0]);
+            if (e == hipSuccess) e = copy_to_host(out_rgb, img, total_floats * sizeof(float), streams[0]);
             for (int d = 1; d < n && e == hipSuccess; ++d)
                 if ((e = hipSetDevice(d)) == hipSuccess) e = hipStreamSynchronize(streams[d]);
             float ms = 0.0f;
@@ -969,8 +1012,7 @@ int rtx_render(rtx_scene* s, const rtx_camera* cam, uint64_t seed, int n_gpus, f
         }
     } else if (rc == RTX_OK) {  // one device, no RCCL: the band is the image
         (void)hipSetDevice(0);
-        hipError_t e = hipMemcpyAsync(out_rgb, bufs[0], (size_t)H * W * 3 * sizeof(float), hipMemcpyDeviceToHost, streams[0]);
-        if (e == hipSuccess) e = hipStreamSynchronize(streams[0]);
+        hipError_t e = copy_to_host(out_rgb, bufs[0], (size_t)H * W * 3 * sizeof(float), streams[0]);
         if (e != hipSuccess) rc = fail(RTX_ERR_HIP, "copy image: %s", hipGetErrorString(e));
     }
     for (int d = 0; d < n; ++d) {
@@ -1010,6 +1052,10 @@ int rtx_release_device_memory(int device) {
                 kv.second = PpmScratch{};
             }
         (void)hipSetDevice(cur);
+    }
+    if (device < 0) {
+        std::lock_guard<std::mutex> lk(g_stage_mu);
+        release_stage_locked();
     }
     {  // communicators span devices 0..n-1: any release drops them all
         std::lock_guard<std::mutex> lk(g_rccl_mu);
@@ -1096,7 +1142,7 @@ int rtx_render_ppm(rtx_scene* s, const rtx_camera* cam, uint64_t seed, char* out
     if (rc == RTX_OK) rc = rtx_encode_ppm_device(rgb, W, H, text, need, &len, st);
     if (rc == RTX_OK && len > capacity) rc = fail(RTX_ERR_INVALID_ARG, "capacity %llu < PPM length %llu",
                                                   (unsigned long long)capacity, (unsigned long long)len);
-    if (rc == RTX_OK && hipMemcpy(out_text, text, len, hipMemcpyDeviceToHost) != hipSuccess)
+    if (rc == RTX_OK && copy_to_host(out_text, text, len, st) != hipSuccess)
         rc = fail(RTX_ERR_HIP, "copying the PPM text to the host");
     cleanup();
     if (rc == RTX_OK) *out_len = len;

@@ -134,6 +134,13 @@ def load() -> ctypes.CDLL:
     path = os.environ.get("RTX_LIB") or lib_path("librtx.so")  # RTX_LIB: A/B against another build
     if not os.path.exists(path):
         raise OSError(f"librtx.so not built at {path}: run __graft_entry__.build() (no CPU fallback exists)")
+    # One HIP runtime per process: PyTorch-ROCm ships its own libamdhip64.so.7 (the SONAME of
+    # /opt/rocm's), and whichever loads first serves both.  With librtx first, torch then bound to
+    # the system runtime and reported no GPU (torch.cuda.is_available() False); torch first works.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = ctypes.CDLL(path)
     L.rtx_version.restype = c_int
     L.rtx_build_info.restype = c_char_p
