@@ -56,6 +56,9 @@ def parse():
     ap.add_argument("--valu", default=os.path.join(ROOT, "profiles", "valu_r02.json"))
     # launcher self-test on the CPU (tests/test_bench_launcher.py): gloo, no GPU, shards filled
     # with a known function of the global pixel instead of rendered
+    ap.add_argument("--rehearse-one-gpu", action="store_true",
+                    help="N > 1 rank processes all on cuda:0 with a gloo gather (host copies): the multi-rank "
+                         "render path on a one-GPU box; not a scaling number")
     ap.add_argument("--selftest-gloo", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--selftest-fail-rank", type=int, default=-1, help=argparse.SUPPRESS)
     return ap.parse_args()
@@ -244,9 +247,13 @@ def main():
 
     import rtx
 
-    torch.cuda.set_device(local_rank)
+    shared = args.rehearse_one_gpu and world > 1  # every rank on cuda:0 (RCCL needs one GPU per rank)
+    torch.cuda.set_device(0 if shared else local_rank)
     backend = None
-    if world > 1:
+    if shared:
+        backend = "gloo"
+        dist.init_process_group(backend)
+    elif world > 1:
         backend = "nccl"  # RCCL on ROCm
         dist.init_process_group(backend, device_id=torch.device("cuda", local_rank))
 
@@ -268,7 +275,7 @@ def main():
     st = dev.render_region(cam, args.seed, reg, shard.data_ptr(), stream, counters=True, timed=True).as_dict()
     my_rows = rtx.region_rows(reg)
     keys = ["samples", "segments", "node_visits", "prim_tests", "hits", "texel_fetches", "rng_draws"]
-    counts = torch.tensor([st[k] for k in keys], dtype=torch.float64, device="cuda")
+    counts = torch.tensor([st[k] for k in keys], dtype=torch.float64, device="cpu" if shared else "cuda")
     if world > 1:
         dist.all_reduce(counts)
     tot = dict(zip(keys, counts.tolist()))
@@ -276,7 +283,7 @@ def main():
     def step(times):
         s = dev.render_region(cam, args.seed, reg, shard.data_ptr(), stream, counters=False, timed=True)
         times.append(s.kernel_ms)
-        return gather_image(shard, H, rank, world)
+        return gather_image(shard.cpu() if shared else shard, H, rank, world)
 
     for _ in range(args.warmup):
         step([])
@@ -287,7 +294,7 @@ def main():
         img = step(kms)
     barrier()
     elapsed = time.perf_counter() - t0
-    t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if shared else "cuda")
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
@@ -303,6 +310,8 @@ def main():
         metric = ("Mray/s on 1920x1080x500spp random-spheres; achieved HBM GB/s vs peak" if headline else
                   f"Mray/s on {W}x{H}x{S}spp {args.scene}" + (" (configs[2])" if c3 else " (not the headline config)"))
         tag = " (configs[1])" if headline else (" (configs[2])" if c3 else "")
+        if shared:
+            metric = f"rehearsal: {world} ranks sharing one GPU, gloo gather (not a scaling number); " + metric
         profile_workload = f"{args.scene}:{W}x{H}x{S}"
         out = {
             "metric": metric,
@@ -322,7 +331,8 @@ def main():
                 "workload": f"{args.scene} {W}x{H}x{S}spp depth {cam.max_depth}{tag}",
                 "scene_seed": args.scene_seed,
                 "render_seed": args.seed,
-                "parallelism": f"row-interleave x{world}" + (" + RCCL gather" if world > 1 else ""),
+                "parallelism": f"row-interleave x{world}" + (" + gloo gather on one GPU" if shared else
+                                                               (" + RCCL gather" if world > 1 else "")),
                 "world_size": dist.get_world_size() if world > 1 else 1,
                 "backend": backend,
             },

@@ -45,3 +45,27 @@ def test_failed_rank_fails_the_launch():
     res = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--selftest-gloo", "--selftest-fail-rank", "1"],
                          cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
     assert res.returncode != 0
+
+
+def _bench_line(args):
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
+    res = subprocess.run([sys.executable, "-u", "bench.py"] + args, cwd=ROOT, env=env, capture_output=True, text=True,
+                         timeout=240)
+    assert res.returncode == 0, res.stderr[-3000:]
+    lines = [ln for ln in res.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, res.stdout  # only rank 0 prints
+    return json.loads(lines[0])
+
+
+@pytest.mark.gpu
+def test_rank_processes_render_the_same_image_on_one_gpu():
+    """The real multi-rank path on a one-GPU box: `bench.py --gpus 3 --rehearse-one-gpu` starts three
+    rank processes on cuda:0, each renders its row-interleaved shard with the megakernel, and the
+    shards are gathered (gloo, host copies: RCCL needs a GPU per rank) and de-interleaved on rank 0.
+    The framebuffer hash must equal the one-rank render's bit for bit."""
+    common = ["--width", "192", "--spp", "8", "--steps", "1", "--warmup", "0", "--no-cpu"]
+    one = _bench_line(["--gpus", "1"] + common)
+    three = _bench_line(["--gpus", "3", "--rehearse-one-gpu"] + common)
+    assert three["n_gpus"] == 3 and three["config"]["world_size"] == 3 and three["config"]["backend"] == "gloo"
+    assert three["metric"].startswith("rehearsal")
+    assert one["framebuffer_sha256_16"] == three["framebuffer_sha256_16"]
