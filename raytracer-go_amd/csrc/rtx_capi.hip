@@ -120,6 +120,8 @@ hipError_t copy_to_host(void* dst, const void* src, size_t bytes, hipStream_t st
                 std::memcpy(static_cast<char*>(dst) + (k - 1) * kStageBytes, g_stage.buf[(k - 1) % 2], len(k - 1));
         }
     }
+    // on a failure no copy into a stage may still be in flight when the lock is released
+    if (e != hipSuccess) (void)hipStreamSynchronize(st);
     return e;
 }
 
