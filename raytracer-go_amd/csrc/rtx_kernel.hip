@@ -24,6 +24,9 @@
 #ifndef RTX_WALK_STEPS  // walk steps per lane between two wave votes
 #define RTX_WALK_STEPS 6
 #endif
+#ifndef RTX_SUB_MAX  // samples per unit of a render with >= 128 units of 8 samples per resident wave
+#define RTX_SUB_MAX 16
+#endif
 #ifndef RTX_ASM_STEP  // 1: the timed kernel's walk step in assembly (trav_step_asm); 0 for A/B
 #define RTX_ASM_STEP 1
 #endif
@@ -432,8 +435,11 @@ hipError_t launch_items(Params p, bool use_lds, hipStream_t stream) {
             // Samples per unit: 8, or fewer when that leaves under 8 units per resident wave
             // (a small image's last units would run on a near-empty GPU).  Measured at 100 spp:
             // 1920x1080 8 -1.6 % vs 16; 400x225 2 -42 % vs 16; Cornell 600x600 8 -3 % vs 16.
+            // 16 when that still leaves >= 64 units per wave (the drain stays short): 1920x1080x500
+            // -0.9 % vs 8 (142.5 vs 143.8 ms).
             const uint64_t per_wave = tiles * p.kn / (8ull * WAVES * (uint64_t)per_cu * cus);
-            p.sub = per_wave >= 8 ? 8u : (per_wave >= 4 ? 4u : (per_wave >= 2 ? 2u : 1u));
+            p.sub = per_wave >= 128 ? RTX_SUB_MAX
+                                    : (per_wave >= 8 ? 8u : (per_wave >= 4 ? 4u : (per_wave >= 2 ? 2u : 1u)));
         }
         const uint64_t units = tiles * ((p.kn + p.sub - 1) / p.sub);
         uint64_t blocks = (uint64_t)per_cu * cus;
