@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define RTX_ABI_VERSION 5
+#define RTX_ABI_VERSION 6
 
 /* ---- status codes ------------------------------------------------------------ */
 enum {
@@ -241,7 +241,10 @@ typedef struct rtx_stats {
                                 did not run, likewise                                        */
     uint64_t shade_split_cycles[4]; /* shade_cycles split: scatter sampling, shading, item claims +
                                        camera rays, segment starts (1/dir)                    */
+    uint64_t walk_layout;   /* ABI 6: the layout walked: 0-7 = the camera octant of a rebuilt tree
+                               (rtx_scene_topology), RTX_LAYOUT_REFERENCE = the caller's tree  */
 } rtx_stats;
+#define RTX_LAYOUT_REFERENCE 8u
 
 #define RTX_FLAG_COUNTERS 1u /* count work units (separate kernel instantiation) */
 #define RTX_FLAG_NO_LDS 4u   /* A/B: read the scene from global memory even if it fits LDS */
@@ -269,6 +272,36 @@ int rtx_device_count(void);
  * the current HIP device (replicated to further devices lazily by rtx_render).
  * Replaces the tree walk the reference does on every ray (bvh.go:220).           */
 int rtx_scene_create(const rtx_scene_desc* desc, rtx_scene** out);
+
+/* ABI 6.  rtx_scene_create with build flags.  By default a scene whose world is one BVH over
+ * spheres (NewBVHFromWorld of a World of spheres, main.go:287) is walked over the library's
+ * own tree of the same spheres: a binned surface-area-heuristic split, each node's near child
+ * (along the camera's viewing direction) first.  The closest hit bvh.go:220-249 returns is
+ * the nearest sphere root among the spheres whose boxes the ray passes, whichever tree the
+ * boxes come from; the reference's tree (median splits on a random axis, bvh.go:142-185)
+ * costs 1.8x the box tests and 4x the sphere tests on randSpheres (DESIGN.md §12 states the
+ * floating-point caveat and how the tests check it).  RTX_SCENE_REFERENCE_BVH keeps the
+ * caller's tree and the reference's visit order (left, then right) as they are; so do the
+ * environment variable RTX_BVH=reference and every scene with quads, nested Worlds or a
+ * World root.  rtx_scene_create(d, out) = rtx_scene_create_ex(d, 0, out).              */
+#define RTX_SCENE_REFERENCE_BVH 1u
+int rtx_scene_create_ex(const rtx_scene_desc* desc, uint32_t flags, rtx_scene** out);
+
+/* The tree a rebuilt scene walks for camera octant `octant` (rtx_camera_octant): *n_nodes
+ * nodes with `left` the child visited first; sphere refs index the caller's sphere table;
+ * *root is the root ref.  nodes is filled when cap >= *n_nodes.  A scene that keeps the
+ * caller's tree reports *n_nodes = 0, *root = -1.  For tests and tools.                */
+int rtx_scene_topology(const rtx_scene* scene, uint32_t octant, rtx_bvh_node* nodes, uint32_t cap, uint32_t* n_nodes,
+                       int32_t* root);
+
+/* The same without a scene or a device: the tree rtx_scene_create_ex(desc, flags) walks for
+ * `octant` (*n_nodes = 0, *root = -1 when it would keep the caller's).  Host only.       */
+int rtx_walk_tree(const rtx_scene_desc* desc, uint32_t flags, uint32_t octant, rtx_bvh_node* nodes, uint32_t cap,
+                  uint32_t* n_nodes, int32_t* root);
+
+/* Octant of the camera's viewing direction (pixel00 + du W/2 + dv H/2 - center): bit k set
+ * when it points to negative axis k. */
+uint32_t rtx_camera_octant(const rtx_camera* cam);
 
 /* Release device memory owned by the scene (NULL is a no-op). */
 void rtx_scene_destroy(rtx_scene* scene);

@@ -26,6 +26,7 @@
 #include "rtx_layout.h"
 #include "rtx_ppm.h"
 #include "rtx_bvh.h"
+#include "rtx_topology.h"
 
 namespace {
 
@@ -49,18 +50,24 @@ int fail(int code, const char* fmt, ...) {
                         #expr, hipGetErrorString(e_), __FILE__, __LINE__);                        \
     } while (0)
 
+// One threaded layout of the walk on a device (rtx_layout.h): a scene keeping the caller's
+// topology has one; a rebuilt one (rtx_topology.h) one per camera octant, uploaded on first use.
+struct DeviceLayout {
+    rtx_entry* entries = nullptr;
+    uint32_t hot = 0;       // entries stored first and cached in LDS by v3 (scenes too big for the LDS copy)
+    uint32_t start = 0;     // walk position of the first entry of the walk (the root)
+    uint32_t prim_end = 0;  // scenes in the LDS copy: primitives stored first, below this position
+};
+
 struct DeviceCopy {
     int device = -1;
-    rtx_entry* entries = nullptr;
+    DeviceLayout lay[8];
     rtx_material* materials = nullptr;
     rtx_texture* textures = nullptr;
     uint32_t* texels = nullptr;
     unsigned long long* counters = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
-    uint32_t hot = 0;  // entries stored first and cached in LDS by v3 (scenes too big for the LDS copy)
     uint32_t n_textures = 0;  // device textures: those materials read (checkered, image, noise)
-    uint32_t start = 0;     // walk position of the first entry of the walk (the root)
-    uint32_t prim_end = 0;  // scenes in the LDS copy: primitives stored first, below this position
 };
 
 // Sample-colour scratch, one per device, shared by all scenes (grown on demand).  `last`
@@ -202,7 +209,12 @@ void release_comms_locked() {  // g_rccl_mu held
 }  // namespace
 
 struct rtx_scene {
-    std::vector<rtx_entry> entries;
+    // The walk as threaded entries: layouts[0] for a scene that keeps the caller's topology (the
+    // reference's visit order, bvh.go:220-249); a rebuilt scene (topo) has one per camera octant,
+    // emitted on first use — all of the same size.
+    std::vector<rtx_entry> layouts[8];
+    bool rebuilt = false;
+    rtxd::Topology topo;
     std::vector<float> quadtab;  // 16 floats per quad (rtx_layout.h)
     std::vector<rtx_material> materials;
     std::vector<rtx_texture> textures;
@@ -347,8 +359,9 @@ void free_copy(DeviceCopy& c);
 
 int upload_copy(rtx_scene* s, DeviceCopy& c);
 
-// The scene's copy on `device`, uploaded on first use; a failed upload frees what it had
-// allocated.  Every copy is counted in the device's Scratch::scenes.
+// The scene's copy on `device` (materials, textures, texels, counters), uploaded on first
+// use; a failed upload frees what it had allocated.  Every copy is counted in the device's
+// Scratch::scenes.  Walk layouts are uploaded separately (ensure_layout).
 int ensure_device(rtx_scene* s, int device, DeviceCopy** out) {
     auto it = s->copies.find(device);
     if (it != s->copies.end()) {
@@ -371,15 +384,31 @@ int ensure_device(rtx_scene* s, int device, DeviceCopy** out) {
     return RTX_OK;
 }
 
-int upload_copy(rtx_scene* s, DeviceCopy& c) {
-    HIP_TRY(hipMalloc(&c.entries, (s->entries.size() + 1) * sizeof(rtx_entry) + s->quadtab.size() * sizeof(float)));
+// The walk of camera octant `oct` as threaded entries (s->mu held): a rebuilt scene emits the
+// octant's orientation of its tree on first use; a scene keeping the caller's topology has one.
+int scene_layout(rtx_scene* s, uint32_t oct, const std::vector<rtx_entry>** out) {
+    if (!s->rebuilt) oct = 0;
+    std::vector<rtx_entry>& L = s->layouts[oct];
+    if (s->rebuilt && L.empty()) rtxd::emit_topology(s->topo, oct, L);
+    *out = &L;
+    return RTX_OK;
+}
+
+// Upload the walk layout of octant `oct` to copy c (current device = c's; s->mu held).
+int ensure_layout(rtx_scene* s, DeviceCopy* c, uint32_t oct) {
+    if (!s->rebuilt) oct = 0;
+    if (c->lay[oct].entries) return RTX_OK;
+    const std::vector<rtx_entry>* E = nullptr;
+    if (int rc = scene_layout(s, oct, &E)) return rc;
+    DeviceLayout& lay = c->lay[oct];
+    HIP_TRY(hipMalloc(&lay.entries, (E->size() + 1) * sizeof(rtx_entry) + s->quadtab.size() * sizeof(float)));
     {  // device layout: all 'a' halves, then all 'b' halves (rtxd::SceneRef), each ending
        // with the sentinel entry (rtx_layout.h).  Every entry names its successor (node: next
        // and escape, primitive: next), so the storage order is free: a scene too big for the
-       // LDS copy stores its top levels first (c.hot entries), which v3 caches in LDS; a scene
-       // in the LDS copy stores its primitives first (below c.prim_end), so the asm walk knows
+       // LDS copy stores its top levels first (lay.hot entries), which v3 caches in LDS; a scene
+       // in the LDS copy stores its primitives first (below lay.prim_end), so the asm walk knows
        // an entry's kind from its position before the entry's read returns (walk_phase_asm).
-        const size_t n = s->entries.size(), m = n + 1;
+        const size_t n = E->size(), m = n + 1;
         std::vector<uint32_t> pos(m);  // storage index of entry i; the sentinel stays last
         for (size_t i = 0; i <= n; ++i) pos[i] = (uint32_t)i;
         if (m * 16 > rtxd::LDS_B) {
@@ -390,9 +419,9 @@ int upload_copy(rtx_scene* s, DeviceCopy& c) {
                 if (per_depth.size() <= depth[i]) per_depth.resize(depth[i] + 1, 0);
                 ++per_depth[depth[i]];
                 int32_t tag, esc;
-                std::memcpy(&tag, &s->entries[i].b[3], 4);
+                std::memcpy(&tag, &(*E)[i].b[3], 4);
                 if (tag == RTX_E_NODE) {
-                    std::memcpy(&esc, &s->entries[i].a[3], 4);
+                    std::memcpy(&esc, &(*E)[i].a[3], 4);
                     ends.push_back((uint32_t)esc);
                 }
             }
@@ -404,32 +433,32 @@ int upload_copy(rtx_scene* s, DeviceCopy& c) {
                 if (depth[i] < levels) pos[i] = k++;
             for (size_t i = 0; i < n; ++i)
                 if (depth[i] >= levels) pos[i] = k++;
-            c.hot = hot;
+            lay.hot = hot;
         } else {
             uint32_t k = 0;
             for (int pass = 0; pass < 2; ++pass)
                 for (size_t i = 0; i < n; ++i) {
                     int32_t tag;
-                    std::memcpy(&tag, &s->entries[i].b[3], 4);
+                    std::memcpy(&tag, &(*E)[i].b[3], 4);
                     if ((tag != RTX_E_NODE) == (pass == 0)) pos[i] = k++;
                 }
             for (size_t i = 0; i < n; ++i) {
                 int32_t tag;
-                std::memcpy(&tag, &s->entries[i].b[3], 4);
-                if (tag != RTX_E_NODE) c.prim_end = 16 * (pos[i] + 1) > c.prim_end ? 16 * (pos[i] + 1) : c.prim_end;
+                std::memcpy(&tag, &(*E)[i].b[3], 4);
+                if (tag != RTX_E_NODE) lay.prim_end = 16 * (pos[i] + 1) > lay.prim_end ? 16 * (pos[i] + 1) : lay.prim_end;
             }
         }
-        c.start = 16 * pos[0];
+        lay.start = 16 * pos[0];
         std::vector<float> soa(m * 8 + s->quadtab.size(), 0.0f);
         for (size_t i = 0; i < n; ++i) {
             const size_t j = pos[i];
-            std::memcpy(&soa[4 * j], s->entries[i].a, 16);
-            std::memcpy(&soa[4 * (m + j)], s->entries[i].b, 16);
+            std::memcpy(&soa[4 * j], (*E)[i].a, 16);
+            std::memcpy(&soa[4 * (m + j)], (*E)[i].b, 16);
             int32_t tag, esc;  // the device recoding, rtx_layout.h
-            std::memcpy(&tag, &s->entries[i].b[3], 4);
+            std::memcpy(&tag, &(*E)[i].b[3], 4);
             const int32_t next = (int32_t)(16 * pos[i + 1]);
             if (tag == RTX_E_NODE) {
-                std::memcpy(&esc, &s->entries[i].a[3], 4);
+                std::memcpy(&esc, &(*E)[i].a[3], 4);
                 esc = (int32_t)(16 * pos[esc]);
                 std::memcpy(&soa[4 * j + 3], &esc, 4);
                 std::memcpy(&soa[4 * (m + j) + 3], &next, 4);
@@ -451,8 +480,12 @@ int upload_copy(rtx_scene* s, DeviceCopy& c) {
         std::memcpy(&soa[4 * n + 3], &self, 4);
         std::memcpy(&soa[4 * (m + n) + 3], &self, 4);
         if (!s->quadtab.empty()) std::memcpy(&soa[8 * m], s->quadtab.data(), s->quadtab.size() * sizeof(float));
-        HIP_TRY(hipMemcpy(c.entries, soa.data(), soa.size() * sizeof(float), hipMemcpyHostToDevice));
+        HIP_TRY(hipMemcpy(lay.entries, soa.data(), soa.size() * sizeof(float), hipMemcpyHostToDevice));
     }
+    return RTX_OK;
+}
+
+int upload_copy(rtx_scene* s, DeviceCopy& c) {
     // device materials: a Lambertian or DiffuseLight with a SolidColor texture carries the
     // colour itself (rtxd::RTX_DEV_TEX_INLINE), so shading reads no texture record; the other
     // textures they read are numbered anew in the device texture table, which holds only those
@@ -506,7 +539,7 @@ int upload_copy(rtx_scene* s, DeviceCopy& c) {
 void free_copy(DeviceCopy& c) {
     if (hipSetDevice(c.device) != hipSuccess) return;
     (void)hipDeviceSynchronize();  // no render of this copy still running
-    (void)hipFree(c.entries);
+    for (DeviceLayout& l : c.lay) (void)hipFree(l.entries);
     (void)hipFree(c.materials);
     (void)hipFree(c.textures);
     (void)hipFree(c.texels);
@@ -521,6 +554,32 @@ void drop_copy(DeviceCopy& c) {
     std::lock_guard<std::mutex> lk(g_scratch_mu);
     Scratch& sc = g_scratch[c.device];
     if (sc.scenes > 0 && --sc.scenes == 0) release_scratch_locked(c.device);
+}
+
+// The walk's tree (rtx_topology.h): 0 = the caller's, 1 = guarded, 2 = unguarded.  Default:
+// guarded when the spheres pass rtxd::precise_enough, else the caller's.  RTX_SCENE_REFERENCE_BVH
+// or the environment variable RTX_BVH=reference (read per scene) keep the caller's;
+// RTX_BVH=guarded / sah force the guarded / unguarded tree (A/B).
+int topology_mode(uint32_t flags, const std::vector<rtx_entry>& ref) {
+    if (flags & RTX_SCENE_REFERENCE_BVH) return 0;
+    const char* e = std::getenv("RTX_BVH");
+    if (e && std::strcmp(e, "reference") == 0) return 0;
+    if (e && std::strcmp(e, "sah") == 0) return 2;
+    if (e && std::strcmp(e, "guarded") == 0) return 1;
+    return rtxd::precise_enough(ref) ? 1 : 0;
+}
+
+// A scene whose layouts[0] holds the reference's walk of one tree: take the walk's own tree when
+// it qualifies (spheres only; rtxd::build_topology) and re-emit layouts[0] for octant 0.
+void adopt_topology(rtx_scene* s, uint32_t flags) {
+    const int mode = topology_mode(flags, s->layouts[0]);
+    if (mode == 0 || !rtxd::build_topology(s->layouts[0], mode == 1, s->topo)) return;
+    s->rebuilt = true;
+    rtxd::emit_topology(s->topo, 0, s->layouts[0]);
+}
+
+uint64_t walk_layout(const rtx_scene* s, const rtx_camera* cam) {
+    return s->rebuilt ? rtxd::camera_octant(*cam) : RTX_LAYOUT_REFERENCE;
 }
 
 int check_camera(const rtx_camera* cam) {
@@ -577,12 +636,13 @@ uint64_t watchdog_ticks() {
     return v;
 }
 
-rtxd::Params make_params(const rtx_scene* s, const DeviceCopy* c, const rtx_camera* cam, uint64_t seed,
+rtxd::Params make_params(const rtx_scene* s, const DeviceCopy* c, uint32_t oct, const rtx_camera* cam, uint64_t seed,
                          const rtx_region* r, float* d_out) {
     rtxd::Params p;
     std::memset(&p, 0, sizeof(p));
-    p.entries = reinterpret_cast<const float4*>(c->entries);
-    p.n_entries = (uint32_t)s->entries.size();
+    const DeviceLayout& lay = c->lay[oct];
+    p.entries = reinterpret_cast<const float4*>(lay.entries);
+    p.n_entries = (uint32_t)s->layouts[oct].size();
     p.n_quads = (uint32_t)(s->quadtab.size() / 16);
     p.n_materials = (uint32_t)s->materials.size();
     p.materials = c->materials;
@@ -605,9 +665,9 @@ rtxd::Params make_params(const rtx_scene* s, const DeviceCopy* c, const rtx_came
     p.shade_thresh = shade_thresh();
     p.has_uv = s->has_image ? 1u : 0u;
     p.has_noise = s->has_noise ? 1u : 0u;
-    p.n_hot = c->hot;
-    p.start = c->start;
-    p.prim_end = c->prim_end;
+    p.n_hot = lay.hot;
+    p.start = lay.start;
+    p.prim_end = lay.prim_end;
     return p;
 }
 
@@ -615,7 +675,9 @@ rtxd::Params make_params(const rtx_scene* s, const DeviceCopy* c, const rtx_came
 // *chunks receives the number of sample chunks (render kernel launches).
 int enqueue_on(rtx_scene* s, DeviceCopy* c, const rtx_camera* cam, uint64_t seed, const rtx_region* r, float* d_out,
                hipStream_t stream, uint32_t flags, bool timed, uint32_t* chunks) {
-    rtxd::Params p = make_params(s, c, cam, seed, r, d_out);
+    const uint32_t oct = s->rebuilt ? rtxd::camera_octant(*cam) : 0u;  // the walk's layout (rtx_topology.h)
+    if (int rc = ensure_layout(s, c, oct)) return rc;
+    rtxd::Params p = make_params(s, c, oct, cam, seed, r, d_out);
     const uint32_t th = (flags >> 8) & 0x7Fu;  // RTX_FLAG_SHADE_THRESH(n) override
     if (th) p.shade_thresh = th > 64 ? 64 : th;
     *chunks = 0;
@@ -806,8 +868,9 @@ extern "C" {
 int rtx_version(void) { return RTX_ABI_VERSION; }
 
 const char* rtx_build_info(void) {
-    return "librtx gfx950 megakernel (ABI 5: persistent (pixel, sample) item waves, LDS scene, threaded pre-order BVH, "
-           "RGBA16 image texels, RCCL band gather); built " __DATE__ " " __TIME__;
+    return "librtx gfx950 megakernel (ABI 6: persistent (pixel, sample) item waves, LDS scene, threaded pre-order BVH "
+           "(binned-SAH walk tree per camera octant, or the caller's), RGBA16 image texels, RCCL band gather); built "
+           __DATE__ " " __TIME__;
 }
 
 const char* rtx_last_error(void) { return g_last_error.c_str(); }
@@ -820,7 +883,9 @@ int rtx_device_count(void) {
 
 uint32_t rtx_region_rows(const rtx_region* region) { return region ? region_rows(region) : 0; }
 
-int rtx_scene_create(const rtx_scene_desc* d, rtx_scene** out) {
+int rtx_scene_create(const rtx_scene_desc* d, rtx_scene** out) { return rtx_scene_create_ex(d, 0u, out); }
+
+int rtx_scene_create_ex(const rtx_scene_desc* d, uint32_t flags, rtx_scene** out) {
     g_last_error.clear();
     if (!d || !out) return fail(RTX_ERR_INVALID_ARG, "NULL argument");
     *out = nullptr;
@@ -832,11 +897,12 @@ int rtx_scene_create(const rtx_scene_desc* d, rtx_scene** out) {
     if (int rc = check_acyclic(d)) return rc;
     rtx_scene* s = new rtx_scene();
     for (uint32_t i = 0; i < d->n_roots; ++i) {
-        if (int rc = emit(d, d->roots[i], s->entries)) {
+        if (int rc = emit(d, d->roots[i], s->layouts[0])) {
             delete s;
             return rc;
         }
     }
+    if (d->n_roots == 1) adopt_topology(s, flags);
     return finish_scene(s, d, out);
 }
 
@@ -863,20 +929,66 @@ int rtx_scene_create_spheres(const rtx_sphere* spheres, uint32_t n_spheres, cons
     if (hipGetDevice(&cur) != hipSuccess) return fail(RTX_ERR_NO_DEVICE, "no HIP device");
     rtx_scene* s = new rtx_scene();
     double ms = 0;
-    hipError_t e = rtxd::build_sphere_bvh(spheres, n_spheres, bvh_seed, bvh_draw0, s->entries, &ms);
+    hipError_t e = rtxd::build_sphere_bvh(spheres, n_spheres, bvh_seed, bvh_draw0, s->layouts[0], &ms);
     if (e != hipSuccess) {
         delete s;
         return fail(e == hipErrorOutOfMemory ? RTX_ERR_OOM : RTX_ERR_HIP, "GPU BVH build: %s", hipGetErrorString(e));
     }
     if (build_ms) *build_ms = ms;
+    adopt_topology(s, 0u);
     return finish_scene(s, &d, out);
 }
 
 uint64_t rtx_scene_export(const rtx_scene* s, void* out, uint64_t cap) {
     if (!s) return 0;
-    const uint64_t bytes = s->entries.size() * sizeof(rtx_entry);
-    if (out && cap >= bytes) std::memcpy(out, s->entries.data(), bytes);
+    const uint64_t bytes = s->layouts[0].size() * sizeof(rtx_entry);
+    if (out && cap >= bytes) std::memcpy(out, s->layouts[0].data(), bytes);
     return bytes;
+}
+
+int rtx_scene_topology(const rtx_scene* s, uint32_t octant, rtx_bvh_node* nodes, uint32_t cap, uint32_t* n_nodes,
+                       int32_t* root) {
+    g_last_error.clear();
+    if (!s || !n_nodes || !root || octant > 7) return fail(RTX_ERR_INVALID_ARG, "bad argument");
+    if (!s->rebuilt) {
+        *n_nodes = 0;
+        *root = -1;
+        return RTX_OK;
+    }
+    std::vector<rtx_bvh_node> v;
+    rtxd::orient_topology(s->topo, octant, v);
+    *n_nodes = (uint32_t)v.size();
+    *root = s->topo.root;
+    if (nodes && cap >= v.size()) std::memcpy(nodes, v.data(), v.size() * sizeof(rtx_bvh_node));
+    return RTX_OK;
+}
+
+uint32_t rtx_camera_octant(const rtx_camera* cam) { return cam ? rtxd::camera_octant(*cam) : 0u; }
+
+int rtx_walk_tree(const rtx_scene_desc* d, uint32_t flags, uint32_t octant, rtx_bvh_node* nodes, uint32_t cap,
+                  uint32_t* n_nodes, int32_t* root) {
+    g_last_error.clear();
+    if (!d || !n_nodes || !root || octant > 7) return fail(RTX_ERR_INVALID_ARG, "bad argument");
+    if (d->n_roots == 0 || !d->roots) return fail(RTX_ERR_INVALID_ARG, "scene has no root");
+    if (d->n_nodes && !d->nodes) return fail(RTX_ERR_INVALID_ARG, "nodes is NULL");
+    if (int rc = validate_tables(d)) return rc;
+    if (int rc = check_acyclic(d)) return rc;
+    std::vector<rtx_entry> ref;
+    for (uint32_t i = 0; i < d->n_roots; ++i)
+        if (int rc = emit(d, d->roots[i], ref)) return rc;
+    rtxd::Topology t;
+    const int mode = topology_mode(flags, ref);
+    if (d->n_roots != 1 || mode == 0 || !rtxd::build_topology(ref, mode == 1, t)) {
+        *n_nodes = 0;
+        *root = -1;
+        return RTX_OK;
+    }
+    std::vector<rtx_bvh_node> v;
+    rtxd::orient_topology(t, octant, v);
+    *n_nodes = (uint32_t)v.size();
+    *root = t.root;
+    if (nodes && cap >= v.size()) std::memcpy(nodes, v.data(), v.size() * sizeof(rtx_bvh_node));
+    return RTX_OK;
 }
 
 void rtx_scene_destroy(rtx_scene* s) {
@@ -890,7 +1002,7 @@ void rtx_scene_destroy(rtx_scene* s) {
 
 uint64_t rtx_scene_device_bytes(const rtx_scene* s) {
     if (!s) return 0;
-    return s->entries.size() * sizeof(rtx_entry) + s->quadtab.size() * sizeof(float) +
+    return s->layouts[0].size() * sizeof(rtx_entry) + s->quadtab.size() * sizeof(float) +
            s->materials.size() * sizeof(rtx_material) +
            s->textures.size() * sizeof(rtx_texture) + s->texels.size() * sizeof(uint32_t);
 }
@@ -912,7 +1024,9 @@ int rtx_render_region_device(rtx_scene* s, const rtx_camera* cam, uint64_t seed,
     if (int rc = enqueue_on(s, c, cam, seed, region, d_out, (hipStream_t)hip_stream, flags, stats != nullptr, &chunks))
         return rc;
     if (!stats) return RTX_OK;
-    return collect_on(c, count, (uint64_t)region_rows(region) * region->width * cam->samples_per_pixel, chunks, stats);
+    const int rc = collect_on(c, count, (uint64_t)region_rows(region) * region->width * cam->samples_per_pixel, chunks, stats);
+    stats->walk_layout = walk_layout(s, cam);
+    return rc;
 }
 
 int rtx_render(rtx_scene* s, const rtx_camera* cam, uint64_t seed, int n_gpus, float* out_rgb, rtx_stats* stats) {
@@ -1030,6 +1144,7 @@ int rtx_render(rtx_scene* s, const rtx_camera* cam, uint64_t seed, int n_gpus, f
         if (streams[d]) (void)hipStreamDestroy(streams[d]);
     }
     (void)hipSetDevice(cur);
+    total.walk_layout = walk_layout(s, cam);
     if (rc == RTX_OK && stats) *stats = total;
     return rc;
 }

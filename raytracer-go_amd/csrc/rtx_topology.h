@@ -1,0 +1,67 @@
+// rtx_topology.h — the walk's own tree over a sphere scene (rtx_topology.hip; host code).
+//
+// The reference's tree (NewBVH, bvh.go:142-185) splits at the median of a random axis, so its
+// boxes overlap heavily: 38 box and 6 sphere tests per segment on randSpheres, 97 box tests on
+// config 4.  Its closest hit (bvh.go:220-249) is the nearest root among the spheres the ray
+// reaches — those whose boxes, all the way down, the ray passes — so another tree over the same
+// spheres gives the same answer when every sphere is reachable by the same rays.
+//
+// GUARDED (the default): the units of the rebuilt tree are the reference tree's leaves, the
+// nodes NewBVH makes for one or two spheres (bvh.go:162-174), with their boxes and their spheres
+// in their order.  Above them sits a binned surface-area-heuristic tree whose boxes are unions of
+// unit boxes.  Every sphere keeps the reference's innermost box as its innermost box and every
+// box above it contains that box, so (slab tests being monotone in the box) a ray reaches a
+// sphere here exactly when it reaches it in the reference's tree, with the same running bound
+// semantics; only the order of the units changes.
+// UNGUARDED (RTX_BVH=sah, A/B): the units are the spheres themselves (own boxes).  The reachable
+// set can then differ where the float32 sphere test reports hits outside a sphere's box
+// (DESIGN.md §12 measures where).
+//
+// Either tree is walked near child first along the camera's viewing direction: one threaded
+// layout per camera octant, made on first use.
+#pragma once
+#include <cstdint>
+#include <vector>
+
+#include "../../include/rtx.h"
+#include "rtx_layout.h"
+
+namespace rtxd {
+
+struct Topology {
+    bool guarded = true;
+    uint32_t n_internal = 0;          // SAH nodes: nodes[0 .. n_internal)
+    // nodes: the SAH nodes (children in canonical order: left = the low side of the split), then
+    // (guarded) one copy of each unit's node with its sphere refs
+    std::vector<rtx_bvh_node> nodes;
+    std::vector<uint8_t> axis;        // split axis of each SAH node
+    std::vector<int32_t> child_unit;  // 2 per SAH node: the unit its left / right child is, or -1
+    int32_t root = 0;
+    // per unit: its entries in the reference's layout (guarded: the node, then its spheres;
+    // unguarded: the sphere), concatenated; unit u = unit_entries[unit_first[u] .. unit_first[u+1])
+    std::vector<rtx_entry> unit_entries;
+    std::vector<uint32_t> unit_first;
+};
+
+// The tree over the spheres of `ref`, the threaded entries emitted from the caller's tree
+// (rtx_layout.h, reference order).  Returns false (out untouched) when the tree does not qualify:
+// anything but spheres, a sphere outside a leaf node of one or two spheres (guarded), or fewer
+// than two units.
+bool build_topology(const std::vector<rtx_entry>& ref, bool guarded, Topology& out);
+
+// Whether the scene's spheres are small against the float32 sphere test's error (see the .hip):
+// the gate of the default (guarded) rebuild.
+bool precise_enough(const std::vector<rtx_entry>& ref);
+
+// The node table of `t` as walked for camera octant `oct` (bit k: the viewing direction is
+// negative along axis k): at every SAH node the child on the near side of its split along the
+// viewing direction is `left`, the one visited first.  Unit nodes keep the reference's order.
+void orient_topology(const Topology& t, uint32_t oct, std::vector<rtx_bvh_node>& out);
+
+// The threaded entries (rtx_layout.h) of `t` walked for octant `oct`.
+void emit_topology(const Topology& t, uint32_t oct, std::vector<rtx_entry>& out);
+
+// Octant of a camera's viewing direction (pixel00 + du W/2 + dv H/2 - center).
+uint32_t camera_octant(const rtx_camera& c);
+
+}  // namespace rtxd

@@ -1,0 +1,357 @@
+// rtx_topology.hip — the walk's own tree over a sphere scene (host code; see rtx_topology.h).
+#include "rtx_topology.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+
+namespace rtxd {
+namespace {
+
+// Go's math.Min / math.Max on float32 operands (bvh.go:28-50 via math.go:38-44): NaN wins,
+// -0 below +0.
+float go_min(float a, float b) {
+    if (a != a || b != b) return NAN;
+    if (a == 0.0f && b == 0.0f) return std::signbit(a) ? a : b;
+    return a < b ? a : b;
+}
+float go_max(float a, float b) {
+    if (a != a || b != b) return NAN;
+    if (a == 0.0f && b == 0.0f) return std::signbit(a) ? b : a;
+    return a > b ? a : b;
+}
+
+struct Box {
+    float mn[3], mx[3];
+};
+
+Box unite(const Box& a, const Box& b) {  // NewAabbFromBoxes, bvh.go:44-50
+    Box r;
+    for (int k = 0; k < 3; ++k) {
+        r.mn[k] = go_min(a.mn[k], b.mn[k]);
+        r.mx[k] = go_max(a.mx[k], b.mx[k]);
+    }
+    return r;
+}
+
+double half_area(const double lo[3], const double hi[3]) {
+    const double dx = hi[0] - lo[0], dy = hi[1] - lo[1], dz = hi[2] - lo[2];
+    return dx * dy + dy * dz + dz * dx;
+}
+
+int32_t tag_of(const rtx_entry& e) {
+    int32_t t;
+    std::memcpy(&t, &e.b[3], 4);
+    return t;
+}
+int32_t word(const float* f) {
+    int32_t t;
+    std::memcpy(&t, f, 4);
+    return t;
+}
+
+// Binned-SAH tree over `boxes` (one leaf per item): appends the SAH nodes to out.nodes /
+// out.axis / out.child_unit, item j becoming child ref item_ref[j].
+void build_sah(const std::vector<Box>& boxes, const std::vector<int32_t>& item_ref, Topology& out,
+               std::vector<int32_t>& child_unit) {
+    const uint32_t n = (uint32_t)boxes.size();
+    std::vector<uint32_t> ids(n);
+    for (uint32_t i = 0; i < n; ++i) ids[i] = i;
+    std::vector<double> cen(3 * (size_t)n);  // box centres (binning only)
+    for (uint32_t i = 0; i < n; ++i)
+        for (int k = 0; k < 3; ++k) cen[3 * i + k] = 0.5 * ((double)boxes[i].mn[k] + (double)boxes[i].mx[k]);
+    struct Task {
+        int32_t node;
+        uint32_t first, count;
+    };
+    std::vector<Task> stack;
+    auto new_node = [&]() {
+        out.nodes.push_back(rtx_bvh_node{});
+        out.axis.push_back(0);
+        child_unit.push_back(-1);
+        child_unit.push_back(-1);
+        return (int32_t)(out.nodes.size() - 1);
+    };
+    out.root = new_node();
+    stack.push_back({out.root, 0, n});
+    constexpr int NB = 32;
+    auto bin_of = [](double c, double lo, double ext) {  // NaN centres go to bin 0
+        const double v = (c - lo) * (NB / ext);
+        return v >= 0.0 ? (v < NB ? (int)v : NB - 1) : 0;
+    };
+    while (!stack.empty()) {
+        const Task t = stack.back();
+        stack.pop_back();
+        uint32_t* I = ids.data() + t.first;
+        Box b = boxes[I[0]];
+        double clo[3], chi[3];
+        for (int k = 0; k < 3; ++k) clo[k] = chi[k] = cen[3 * I[0] + k];
+        for (uint32_t i = 1; i < t.count; ++i) {
+            b = unite(b, boxes[I[i]]);
+            for (int k = 0; k < 3; ++k) {
+                clo[k] = std::min(clo[k], cen[3 * I[i] + k]);
+                chi[k] = std::max(chi[k], cen[3 * I[i] + k]);
+            }
+        }
+        std::memcpy(out.nodes[t.node].bmin, b.mn, sizeof(b.mn));
+        std::memcpy(out.nodes[t.node].bmax, b.mx, sizeof(b.mx));
+        // cost of a split: A(left) N(left) + A(right) N(right), over NB centre bins per axis
+        double best = INFINITY;
+        int bax = -1, bsplit = -1;
+        for (int ax = 0; ax < 3; ++ax) {
+            const double ext = chi[ax] - clo[ax];
+            if (!(ext > 0.0) || !std::isfinite(ext)) continue;
+            double blo[NB][3], bhi[NB][3];
+            uint32_t bc[NB] = {0};
+            for (int q = 0; q < NB; ++q)
+                for (int k = 0; k < 3; ++k) {
+                    blo[q][k] = INFINITY;
+                    bhi[q][k] = -INFINITY;
+                }
+            for (uint32_t i = 0; i < t.count; ++i) {
+                const int q = bin_of(cen[3 * I[i] + ax], clo[ax], ext);
+                ++bc[q];
+                for (int k = 0; k < 3; ++k) {
+                    blo[q][k] = std::min(blo[q][k], (double)boxes[I[i]].mn[k]);
+                    bhi[q][k] = std::max(bhi[q][k], (double)boxes[I[i]].mx[k]);
+                }
+            }
+            double ra[NB], lo[3], hi[3];
+            uint32_t rc[NB], cnt = 0;
+            for (int k = 0; k < 3; ++k) {
+                lo[k] = INFINITY;
+                hi[k] = -INFINITY;
+            }
+            for (int q = NB - 1; q > 0; --q) {
+                for (int k = 0; k < 3; ++k) {
+                    lo[k] = std::min(lo[k], blo[q][k]);
+                    hi[k] = std::max(hi[k], bhi[q][k]);
+                }
+                cnt += bc[q];
+                ra[q] = cnt ? half_area(lo, hi) : 0.0;
+                rc[q] = cnt;
+            }
+            for (int k = 0; k < 3; ++k) {
+                lo[k] = INFINITY;
+                hi[k] = -INFINITY;
+            }
+            cnt = 0;
+            for (int q = 0; q < NB - 1; ++q) {
+                for (int k = 0; k < 3; ++k) {
+                    lo[k] = std::min(lo[k], blo[q][k]);
+                    hi[k] = std::max(hi[k], bhi[q][k]);
+                }
+                cnt += bc[q];
+                if (cnt == 0 || rc[q + 1] == 0) continue;
+                const double c = half_area(lo, hi) * cnt + ra[q + 1] * rc[q + 1];
+                if (c < best) {
+                    best = c;
+                    bax = ax;
+                    bsplit = q;
+                }
+            }
+        }
+        uint32_t mid = t.count / 2;  // every centre equal (or not finite): split the list in the middle
+        if (bax >= 0) {
+            const double ext = chi[bax] - clo[bax];
+            auto low = [&](uint32_t id) { return bin_of(cen[3 * id + bax], clo[bax], ext) <= bsplit; };
+            mid = (uint32_t)(std::stable_partition(I, I + t.count, low) - I);
+            if (mid == 0 || mid == t.count) mid = t.count / 2;
+        } else {
+            bax = 0;
+        }
+        out.axis[t.node] = (uint8_t)bax;
+        const uint32_t cnt[2] = {mid, t.count - mid}, first[2] = {t.first, t.first + mid};
+        int32_t child[2];
+        for (int c = 0; c < 2; ++c) {
+            if (cnt[c] == 1) {
+                child[c] = item_ref[ids[first[c]]];
+                child_unit[2 * t.node + c] = (int32_t)ids[first[c]];
+            } else {
+                child[c] = new_node();
+                stack.push_back({child[c], first[c], cnt[c]});
+            }
+        }
+        out.nodes[t.node].left = child[0];
+        out.nodes[t.node].right = child[1];
+    }
+}
+
+}  // namespace
+
+// The float32 sphere test (hittables.go:96-116) forms c = |oc|^2 - r^2 from squares of order D^2
+// (D: the ray origin's distance to the centre), so it reports hits up to about eps D^2 / r outside a
+// sphere's silhouette.  Where such hits can reach past the innermost box, the order in which two
+// units are tried can decide which of two nearby spheres is the closest hit, so the
+// tree is rebuilt only where that zone is a small fraction of the spheres: eps D^2 / r_min^2 < 2^-7,
+// D the diagonal of the scene without its huge spheres (a sphere is huge when its radius exceeds the
+// extent of all smaller ones: main.go's ground, r = 1000).  randSpheres and the config-5 scene pass
+// (1.4e-3); config 4's 316-unit slab of r = 0.2 spheres fails (0.3).
+bool precise_enough(const std::vector<rtx_entry>& ref) {
+    std::vector<std::pair<float, uint32_t>> rad;  // (radius, entry), spheres only
+    for (uint32_t i = 0; i < ref.size(); ++i)
+        if (tag_of(ref[i]) >= 0) rad.push_back({std::fabs(ref[i].a[3]), i});
+    if (rad.empty()) return false;
+    std::sort(rad.begin(), rad.end());
+    std::vector<Box> pre(rad.size());  // union of the boxes of the k + 1 smallest spheres
+    for (size_t k = 0; k < rad.size(); ++k) {
+        const rtx_entry& e = ref[rad[k].second];
+        Box b;
+        for (int q = 0; q < 3; ++q) {
+            b.mn[q] = e.a[q] - rad[k].first;
+            b.mx[q] = e.a[q] + rad[k].first;
+        }
+        pre[k] = k ? unite(pre[k - 1], b) : b;
+    }
+    size_t keep = rad.size();  // drop the huge spheres, largest first
+    while (keep > 1) {
+        const Box& b = pre[keep - 2];
+        const double ext = std::max({(double)b.mx[0] - b.mn[0], (double)b.mx[1] - b.mn[1], (double)b.mx[2] - b.mn[2]});
+        if (!(rad[keep - 1].first > ext)) break;
+        --keep;
+    }
+    const Box& b = pre[keep - 1];
+    double d2 = 0.0;
+    for (int q = 0; q < 3; ++q) d2 += ((double)b.mx[q] - b.mn[q]) * ((double)b.mx[q] - b.mn[q]);
+    const double rmin = rad[0].first;
+    return rmin > 0.0 && std::ldexp(d2, -24) / (rmin * rmin) < std::ldexp(1.0, -7);
+}
+
+bool build_topology(const std::vector<rtx_entry>& ref, bool guarded, Topology& out) {
+    // the units, in the reference's walk order: [first entry, end) of each
+    std::vector<std::pair<uint32_t, uint32_t>> units;
+    const uint32_t n = (uint32_t)ref.size();
+    for (uint32_t i = 0; i < n;) {
+        const int32_t tag = tag_of(ref[i]);
+        if (tag == RTX_E_NODE) {
+            const uint32_t e = (uint32_t)word(&ref[i].a[3]);  // escape (host layout: an entry index)
+            bool leaf = guarded && e > i + 1 && e <= i + 3 && e <= n;
+            for (uint32_t k = i + 1; leaf && k < e; ++k) leaf = tag_of(ref[k]) >= 0;
+            if (leaf) {
+                units.push_back({i, e});
+                i = e;
+            } else {
+                ++i;
+            }
+        } else if (tag >= 0 && !guarded) {  // a sphere
+            units.push_back({i, i + 1});
+            ++i;
+        } else {
+            return false;  // a quad, or (guarded) a sphere outside a leaf node
+        }
+    }
+    if (units.size() < 2) return false;
+    Topology t;
+    t.guarded = guarded;
+    const uint32_t U = (uint32_t)units.size();
+    t.n_internal = U - 1;
+    std::vector<Box> boxes(U);
+    std::vector<int32_t> item_ref(U);
+    t.unit_first.push_back(0);
+    for (uint32_t u = 0; u < U; ++u) {
+        const rtx_entry& h = ref[units[u].first];
+        for (uint32_t k = units[u].first; k < units[u].second; ++k) t.unit_entries.push_back(ref[k]);
+        t.unit_first.push_back((uint32_t)t.unit_entries.size());
+        if (guarded) {  // the leaf node's own box
+            for (int k = 0; k < 3; ++k) {
+                boxes[u].mn[k] = h.a[k];
+                boxes[u].mx[k] = h.b[k];
+            }
+            item_ref[u] = (int32_t)(t.n_internal + u);
+        } else {  // the sphere's box: NewSphere's NewAabb(center - r, center + r), hittables.go:85-94
+            for (int k = 0; k < 3; ++k) {
+                const float p1 = h.a[k] + (h.a[3] * -1.0f), p2 = h.a[k] + h.a[3];
+                boxes[u].mn[k] = go_min(p1, p2);
+                boxes[u].mx[k] = go_max(p1, p2);
+            }
+            item_ref[u] = RTX_REF_PRIM(RTX_PRIM_SPHERE, word(&h.b[1]));
+        }
+    }
+    std::vector<int32_t> child_unit;
+    build_sah(boxes, item_ref, t, child_unit);
+    if (t.nodes.size() != t.n_internal) return false;  // (a binary tree over U leaves has U - 1 nodes)
+    if (guarded) {  // the units' nodes, as the reference built them
+        for (uint32_t u = 0; u < U; ++u) {
+            const uint32_t f = t.unit_first[u], e = t.unit_first[u + 1];
+            const rtx_entry& h = t.unit_entries[f];
+            rtx_bvh_node nd{};
+            for (int k = 0; k < 3; ++k) {
+                nd.bmin[k] = h.a[k];
+                nd.bmax[k] = h.b[k];
+            }
+            nd.left = RTX_REF_PRIM(RTX_PRIM_SPHERE, word(&t.unit_entries[f + 1].b[1]));
+            nd.right = e - f == 3 ? RTX_REF_PRIM(RTX_PRIM_SPHERE, word(&t.unit_entries[f + 2].b[1])) : nd.left;
+            t.nodes.push_back(nd);
+        }
+    }
+    t.child_unit = std::move(child_unit);
+    out = std::move(t);
+    return true;
+}
+
+void orient_topology(const Topology& t, uint32_t oct, std::vector<rtx_bvh_node>& out) {
+    out = t.nodes;
+    for (uint32_t i = 0; i < t.n_internal; ++i)
+        if ((oct >> t.axis[i]) & 1u) std::swap(out[i].left, out[i].right);
+}
+
+void emit_topology(const Topology& t, uint32_t oct, std::vector<rtx_entry>& out) {
+    out.clear();
+    out.reserve(t.n_internal + t.unit_entries.size());
+    struct Frame {
+        int32_t node;   // SAH node, or -1 - unit
+        int64_t close;  // >= 0: the entry whose escape this frame closes
+    };
+    std::vector<Frame> st{{t.root, -1}};
+    while (!st.empty()) {
+        const Frame f = st.back();
+        st.pop_back();
+        if (f.close >= 0) {
+            const int32_t esc = (int32_t)out.size();
+            std::memcpy(&out[(size_t)f.close].a[3], &esc, 4);
+            continue;
+        }
+        if (f.node < 0) {  // a unit: its entries, the leaf node's escape moved with it
+            const uint32_t u = (uint32_t)(-1 - f.node);
+            const uint32_t base = (uint32_t)out.size();
+            for (uint32_t k = t.unit_first[u]; k < t.unit_first[u + 1]; ++k) out.push_back(t.unit_entries[k]);
+            if (t.guarded) {
+                const int32_t esc = (int32_t)out.size();
+                std::memcpy(&out[base].a[3], &esc, 4);
+            }
+            continue;
+        }
+        const rtx_bvh_node& n = t.nodes[f.node];
+        rtx_entry e;
+        std::memset(&e, 0, sizeof(e));
+        for (int k = 0; k < 3; ++k) {
+            e.a[k] = n.bmin[k];
+            e.b[k] = n.bmax[k];
+        }
+        const int32_t tag = RTX_E_NODE;
+        std::memcpy(&e.b[3], &tag, 4);
+        const int64_t me = (int64_t)out.size();
+        out.push_back(e);
+        int32_t kid[2];
+        for (int c = 0; c < 2; ++c) {
+            const int32_t cu = t.child_unit[2 * f.node + c];
+            kid[c] = cu >= 0 ? -1 - cu : (c == 0 ? n.left : n.right);
+        }
+        const bool flip = (oct >> t.axis[f.node]) & 1u;  // the near child first
+        st.push_back({0, me});
+        st.push_back({kid[flip ? 0 : 1], -1});
+        st.push_back({kid[flip ? 1 : 0], -1});
+    }
+}
+
+uint32_t camera_octant(const rtx_camera& c) {
+    uint32_t o = 0;
+    for (int k = 0; k < 3; ++k) {
+        const double f = (double)c.pixel00[k] + (double)c.pixel_du[k] * (0.5 * c.image_width) +
+                         (double)c.pixel_dv[k] * (0.5 * c.image_height) - (double)c.center[k];
+        if (f < 0.0) o |= 1u << k;
+    }
+    return o;
+}
+
+}  // namespace rtxd

@@ -28,6 +28,8 @@ RTX_MAT_LAMBERTIAN, RTX_MAT_METAL, RTX_MAT_DIELECTRIC, RTX_MAT_DIFFUSE_LIGHT = 0
 RTX_TEX_SOLID, RTX_TEX_CHECKERED, RTX_TEX_IMAGE, RTX_TEX_NOISE = 0, 1, 2, 3
 RTX_FLAG_COUNTERS = 1
 RTX_FLAG_NO_LDS = 4
+RTX_SCENE_REFERENCE_BVH = 1  # rtx_scene_create_ex: keep the caller's tree and the reference's visit order
+RTX_LAYOUT_REFERENCE = 8  # Stats.walk_layout of a scene walking the caller's tree
 RTX_IMAGE_TEXEL_WORDS = 2  # RGBA16 image texels: two uint32 words each (rtx.h)
 
 
@@ -99,7 +101,8 @@ class Stats(ctypes.Structure):
                 ("wave_iters", c_uint64), ("lane_steps", c_uint64), ("shade_phases", c_uint64),
                 ("shade_lanes", c_uint64), ("trav_cycles", c_uint64), ("shade_cycles", c_uint64),
                 ("idle_lanes", c_uint64), ("cache_hits", c_uint64), ("sample_chunks", c_uint64),
-                ("parked_lanes", c_uint64), ("deferred_lanes", c_uint64), ("shade_split_cycles", c_uint64 * 4)]
+                ("parked_lanes", c_uint64), ("deferred_lanes", c_uint64), ("shade_split_cycles", c_uint64 * 4),
+                ("walk_layout", c_uint64)]
 
     def as_dict(self) -> dict:
         return {name: (list(v) if not isinstance(v := getattr(self, name), (int, float)) else v)
@@ -110,7 +113,8 @@ RTX_SYMBOLS = [
     "rtx_version", "rtx_build_info", "rtx_last_error", "rtx_device_count", "rtx_scene_create",
     "rtx_scene_destroy", "rtx_scene_device_bytes", "rtx_render", "rtx_render_region_device", "rtx_region_rows",
     "rtx_ppm_max_bytes", "rtx_encode_ppm_device", "rtx_render_ppm", "rtx_scene_create_spheres", "rtx_scene_export",
-    "rtx_release_device_memory", "rtx_device_scratch_bytes",
+    "rtx_release_device_memory", "rtx_device_scratch_bytes", "rtx_scene_create_ex", "rtx_scene_topology",
+    "rtx_camera_octant", "rtx_walk_tree",
 ]
 RTXHOST_SYMBOLS = [
     "rtxhost_build_scene", "rtxhost_scene_free", "rtxhost_scene_desc", "rtxhost_scene_camera",
@@ -148,6 +152,16 @@ def load() -> ctypes.CDLL:
     L.rtx_device_count.restype = c_int
     L.rtx_scene_create.argtypes = [POINTER(SceneDesc), POINTER(c_void_p)]
     L.rtx_scene_create.restype = c_int
+    L.rtx_scene_create_ex.argtypes = [POINTER(SceneDesc), c_uint32, POINTER(c_void_p)]
+    L.rtx_scene_create_ex.restype = c_int
+    L.rtx_scene_topology.argtypes = [c_void_p, c_uint32, POINTER(BvhNode), c_uint32, POINTER(c_uint32),
+                                     POINTER(c_int32)]
+    L.rtx_scene_topology.restype = c_int
+    L.rtx_walk_tree.argtypes = [POINTER(SceneDesc), c_uint32, c_uint32, POINTER(BvhNode), c_uint32,
+                                POINTER(c_uint32), POINTER(c_int32)]
+    L.rtx_walk_tree.restype = c_int
+    L.rtx_camera_octant.argtypes = [POINTER(Camera)]
+    L.rtx_camera_octant.restype = c_uint32
     L.rtx_scene_destroy.argtypes = [c_void_p]
     L.rtx_scene_destroy.restype = None
     L.rtx_scene_device_bytes.argtypes = [c_void_p]
@@ -276,14 +290,15 @@ class HostScene:
 class DeviceScene:
     """rtx_scene_create: the tables uploaded once to the current HIP device."""
 
-    def __init__(self, desc_ptr=None, handle=None):
+    def __init__(self, desc_ptr=None, handle=None, reference_bvh: bool = False):
         L = load()
         self.build_ms = None
         if handle is not None:
             self._h = handle
             return
         h = c_void_p()
-        check(L.rtx_scene_create(desc_ptr, ctypes.byref(h)), "rtx_scene_create")
+        check(L.rtx_scene_create_ex(desc_ptr, RTX_SCENE_REFERENCE_BVH if reference_bvh else 0, ctypes.byref(h)),
+              "rtx_scene_create_ex")
         self._h = h
 
     @classmethod
@@ -314,6 +329,29 @@ class DeviceScene:
 
     def device_bytes(self) -> int:
         return load().rtx_scene_device_bytes(self._h)
+
+    def topology(self, octant: int):
+        """(nodes ctypes array, root) of the tree the scene walks for a camera octant, or None when
+        the scene walks the caller's tree (rtx_scene_topology)."""
+        L = load()
+        n, root = c_uint32(), c_int32()
+        check(L.rtx_scene_topology(self._h, octant, None, 0, ctypes.byref(n), ctypes.byref(root)), "rtx_scene_topology")
+        if n.value == 0 and root.value == -1:
+            return None
+        arr = (BvhNode * max(n.value, 1))()
+        check(L.rtx_scene_topology(self._h, octant, arr, n.value, ctypes.byref(n), ctypes.byref(root)),
+              "rtx_scene_topology")
+        return arr, int(n.value), int(root.value)
+
+    def walk_desc(self, desc_ptr, cam: Camera):
+        """The scene description of the tree the scene walks for `cam` (the caller's own when the
+        scene keeps it): same spheres, materials and textures, the walk's nodes and root.  The
+        oracle rendering this description takes the kernel's box and primitive tests one for one."""
+        t = self.topology(camera_octant(cam))
+        if t is None:
+            return desc_ptr
+        arr, n, root = t
+        return desc_with_tree(desc_ptr, arr, n, root)
 
     def render_region(self, cam: Camera, seed: int, region: Region, out_ptr: int, stream: int = 0,
                       counters: bool = False, timed: bool = False, flags: int = 0):
@@ -385,6 +423,40 @@ def host_ycbcr_rgba(y: int, cb: int, cr: int):
     o = (c_uint32 * 4)()
     load_host().rtxhost_ycbcr_rgba(y, cb, cr, o)
     return tuple(o)
+
+
+def desc_with_tree(desc_ptr, arr, n: int, root: int):
+    """A copy of a scene description with another node table and root (same primitives and materials)."""
+    d = desc_ptr.contents
+    w = SceneDesc()
+    for f, _ in SceneDesc._fields_:
+        setattr(w, f, getattr(d, f))
+    roots = (c_int32 * 1)(root)
+    w.nodes = ctypes.cast(arr, POINTER(BvhNode))
+    w.n_nodes = n
+    w.n_roots = 1
+    w.roots = ctypes.cast(roots, POINTER(c_int32))
+    p = ctypes.pointer(w)
+    p._keep = (arr, roots, desc_ptr)  # the arrays live as long as the pointer
+    return p
+
+
+def walk_tree_desc(desc_ptr, cam: Camera, flags: int = 0):
+    """rtx_walk_tree (host only): the description of the tree a scene made from desc_ptr walks
+    for cam's octant — desc_ptr itself when the scene would keep the caller's tree."""
+    L = load()
+    n, root = c_uint32(), c_int32()
+    oc = camera_octant(cam)
+    check(L.rtx_walk_tree(desc_ptr, flags, oc, None, 0, ctypes.byref(n), ctypes.byref(root)), "rtx_walk_tree")
+    if n.value == 0 and root.value == -1:
+        return desc_ptr
+    arr = (BvhNode * max(n.value, 1))()
+    check(L.rtx_walk_tree(desc_ptr, flags, oc, arr, n.value, ctypes.byref(n), ctypes.byref(root)), "rtx_walk_tree")
+    return desc_with_tree(desc_ptr, arr, int(n.value), int(root.value))
+
+
+def camera_octant(cam: Camera) -> int:
+    return int(load().rtx_camera_octant(ctypes.byref(cam)))
 
 
 def region_rows(region: Region) -> int:

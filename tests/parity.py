@@ -1,0 +1,76 @@
+"""Shared GPU-vs-oracle checks (test infrastructure, imported by the -m gpu tests).
+
+Every GPU check renders its region TWICE through the C-ABI (rtx_render_region_device):
+  - with the timed kernel (counters off: the instantiation bench.py measures, with the
+    assembly walk), and
+  - with the counting kernel (RTX_FLAG_COUNTERS: the C++ walk plus work counters),
+and holds both to the oracle (oracle/oracle.c):
+  1. bit-identical to the oracle's iterative colour order walking the tree the scene walks
+     (rtx_scene_topology: the library's rebuilt tree, or the caller's), and the counting
+     kernel's counters equal to the oracle's on that tree — every box test, sphere test, hit,
+     texel fetch and RNG draw;
+  2. when the scene walks a rebuilt tree: the oracle on the rebuilt tree bit-identical to the
+     oracle on the caller's (the reference's) tree, with the same segments, hits, texel fetches
+     and draws — the tree changes the work, not a single path;
+  3. within the north-star bar, |delta| <= 1e-4 per channel, of the oracle in the reference's
+     own (recursive) colour order on the caller's tree.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+import oracle_binding as ob
+import rtx
+
+TOL = 1e-4  # north_star: per-channel RGB |delta| <= 1e-4 vs the seeded reference
+PATH_KEYS = ("samples", "segments", "hits", "texel_fetches", "rng_draws")
+WORK_KEYS = PATH_KEYS + ("node_visits", "prim_tests")
+
+
+def gpu_region(torch, dev, cam, seed, reg, counters=True, flags=0):
+    """One region render on cuda:0 (NaN-filled output), waited for; (image, stats)."""
+    rows = rtx.region_rows(reg)
+    out = torch.full((max(rows, 1), max(reg.width, 1), 3), float("nan"), dtype=torch.float32, device="cuda")
+    st = dev.render_region(cam, seed, reg, out.data_ptr(), torch.cuda.current_stream().cuda_stream,
+                           counters=counters, timed=True, flags=flags)
+    torch.cuda.synchronize()
+    return out[:rows, : reg.width].cpu().numpy(), st
+
+
+def assert_counters_equal(st, cnt, keys=WORK_KEYS):
+    for k in keys:
+        assert getattr(st, k) == cnt[k], (k, getattr(st, k), cnt[k])
+
+
+def oracle_checks(desc, walk, cam, seed, reg):
+    """(iterative image on the walked tree, its counters, reference-order image on the caller's
+    tree); asserts check 2 when the walked tree is a rebuilt one."""
+    it, cnt = ob.render(walk, cam, seed, reg, ob.ORDER_ITERATIVE)
+    if walk is not desc:
+        it0, cnt0 = ob.render(desc, cam, seed, reg, ob.ORDER_ITERATIVE)
+        assert np.array_equal(it, it0), f"rebuilt tree changes the image: max {np.abs(it - it0).max()}"
+        for k in PATH_KEYS:
+            assert cnt[k] == cnt0[k], (k, cnt[k], cnt0[k])
+    ref, _ = ob.render(desc, cam, seed, reg, ob.ORDER_REFERENCE)
+    return it, cnt, ref
+
+
+def check_scene(torch, dev, desc, cam, seed, reg, flags=0, kernels=("timed", "counting")):
+    """Checks 1-3 for both kernels on one region; returns (timed image, counting stats, oracle counters)."""
+    walk = dev.walk_desc(desc, cam)
+    it, cnt, ref = oracle_checks(desc, walk, cam, seed, reg)
+    img = st = None
+    for k in kernels:
+        gpu, s = gpu_region(torch, dev, cam, seed, reg, counters=(k == "counting"), flags=flags)
+        assert np.isfinite(gpu).all(), k
+        assert np.array_equal(gpu, it), f"{k} kernel not bit-identical to the oracle: max {np.abs(gpu - it).max()}"
+        d = float(np.abs(gpu - ref).max()) if gpu.size else 0.0
+        assert d <= TOL, f"{k} kernel: max |delta| = {d} > {TOL} vs the reference-order oracle"
+        want = rtx.camera_octant(cam) if walk is not desc else rtx.RTX_LAYOUT_REFERENCE
+        assert s.walk_layout == want, (k, s.walk_layout, want)
+        if k == "counting":
+            assert_counters_equal(s, cnt)
+            st = s
+        else:
+            img = gpu
+    return (img if img is not None else it), st, cnt

@@ -1,0 +1,28 @@
+"""Build hygiene (CPU): a kernel source that does not compile fails `make`, even where the
+Makefile filters hipcc's output through grep, and leaves no stale object behind."""
+import os
+import shutil
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.parametrize("src", ["rtx_kernel", "rtx_ppm"])
+def test_broken_source_fails_make(built, tmp_path, src):
+    pkg = tmp_path / "raytracer-go_amd"
+    shutil.copytree(os.path.join(ROOT, "raytracer-go_amd", "csrc"), pkg / "csrc")
+    shutil.copy(os.path.join(ROOT, "raytracer-go_amd", "Makefile"), pkg / "Makefile")
+    shutil.copytree(os.path.join(ROOT, "include"), tmp_path / "include")
+    # a stale object from an earlier good build must not survive the failed one
+    (pkg / "build").mkdir()
+    stale = pkg / "build" / f"{src}.o"
+    shutil.copy(os.path.join(ROOT, "raytracer-go_amd", "build", f"{src}.o"), stale)
+    path = pkg / "csrc" / f"{src}.hip"
+    path.write_text("#error deliberately broken source (tests/test_build_hygiene.py)\n" + path.read_text())
+    os.utime(path, None)
+    r = subprocess.run(["make", "-C", str(pkg), f"build/{src}.o"], capture_output=True, text=True, timeout=600)
+    assert r.returncode != 0, r.stdout + r.stderr
+    assert "deliberately broken" in r.stdout + r.stderr
+    assert not stale.exists()

@@ -31,8 +31,13 @@ def torch_cuda():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("bvh", ["reference", "default"])
 @pytest.mark.parametrize("scene", ["random_spheres", "earth_dielectric", "simple_light_demo", "stress_100k"])
-def test_gpu_build_equals_host_build(torch_cuda, built, scene):
+def test_gpu_build_equals_host_build(torch_cuda, built, monkeypatch, scene, bvh):
+    """RTX_BVH=reference: the reference's own layout from both builds; default: the walk's tree
+    (rtx_topology.h) over them, the same again."""
+    if bvh == "reference":
+        monkeypatch.setenv("RTX_BVH", "reference")
     host = rtx.HostScene(scene, 1)
     ref = rtx.DeviceScene(host.desc)
     gpu = rtx.DeviceScene.from_spheres(host)

@@ -17,6 +17,7 @@ import pytest
 
 import oracle_binding as ob
 import rtx
+from parity import check_scene
 
 BORDER = (0, 34678, 0)  # color.YCbCr{}.RGBA()
 
@@ -127,27 +128,13 @@ def torch_cuda():
     return torch
 
 
-def gpu_region(torch, dev, cam, seed, reg):
-    rows = rtx.region_rows(reg)
-    out = torch.full((rows, reg.width, 3), float("nan"), dtype=torch.float32, device="cuda")
-    st = dev.render_region(cam, seed, reg, out.data_ptr(), torch.cuda.current_stream().cuda_stream,
-                           counters=True, timed=True)
-    torch.cuda.synchronize()
-    return out.cpu().numpy(), st
-
-
 def parity(torch, scene, width, spp, depth, seed, reg=None):
+    """Both kernels vs the oracle (tests/parity.py); (timed image, oracle counters)."""
     s = rtx.HostScene(scene, 1)
     dev = rtx.DeviceScene(s.desc)
     cam = s.camera(width=width, spp=spp, depth=depth)
     reg = reg or rtx.Region(0, 0, cam.image_width, cam.image_height, 0, 1)
-    gpu, st = gpu_region(torch, dev, cam, seed, reg)
-    it, cnt = ob.render(s.desc, cam, seed, reg, ob.ORDER_ITERATIVE)
-    ref, _ = ob.render(s.desc, cam, seed, reg, ob.ORDER_REFERENCE)
-    assert np.array_equal(gpu, it), f"max {np.abs(gpu - it).max()}"
-    assert np.abs(gpu - ref).max() <= 1e-4
-    assert (st.segments, st.node_visits, st.prim_tests, st.hits, st.texel_fetches, st.rng_draws) == (
-        cnt["segments"], cnt["node_visits"], cnt["prim_tests"], cnt["hits"], cnt["texel_fetches"], cnt["rng_draws"])
+    gpu, _, cnt = check_scene(torch, dev, s.desc, cam, seed, reg)
     return gpu, cnt
 
 

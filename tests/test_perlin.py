@@ -14,6 +14,7 @@ import pytest
 
 import oracle_binding as ob
 import rtx
+from parity import check_scene
 
 f32 = np.float32
 
@@ -159,19 +160,9 @@ def torch_cuda():
 
 
 def gpu_check(torch, scene, cam, seed, reg, flags=0):
-    dev = rtx.DeviceScene(scene.desc)
-    rows = rtx.region_rows(reg)
-    out = torch.full((max(rows, 1), max(reg.width, 1), 3), float("nan"), dtype=torch.float32, device="cuda")
-    st = dev.render_region(cam, seed, reg, out.data_ptr(), torch.cuda.current_stream().cuda_stream,
-                           counters=True, timed=True, flags=flags)
-    torch.cuda.synchronize()
-    gpu = out[:rows, : reg.width].cpu().numpy()
-    it, cnt = ob.render(scene.desc, cam, seed, reg, ob.ORDER_ITERATIVE)
-    ref, _ = ob.render(scene.desc, cam, seed, reg, ob.ORDER_REFERENCE)
-    assert np.array_equal(gpu, it), f"max {np.abs(gpu - it).max()}"
-    assert float(np.abs(gpu - ref).max()) <= 1e-4
-    for k in ("samples", "segments", "node_visits", "prim_tests", "hits", "rng_draws"):
-        assert getattr(st, k) == cnt[k], k
+    """Both kernels (timed and counting) vs the oracle (tests/parity.py)."""
+    desc = scene.desc
+    check_scene(torch, rtx.DeviceScene(desc), desc, cam, seed, reg, flags=flags)
 
 
 @pytest.mark.gpu

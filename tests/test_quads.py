@@ -11,6 +11,7 @@ import pytest
 
 import oracle_binding as ob
 import rtx
+from parity import check_scene, gpu_region
 
 f32 = np.float32
 
@@ -172,25 +173,11 @@ def torch_cuda():
     return torch
 
 
-def gpu_render(torch, desc, cam, seed, reg, flags=0):
+def gpu_check(torch, desc, cam, seed, reg, flags=0):
+    """Both kernels (timed and counting) vs the oracle (tests/parity.py); (timed image, stats)."""
     dev = rtx.DeviceScene(desc)
-    rows = rtx.region_rows(reg)
-    out = torch.full((max(rows, 1), max(reg.width, 1), 3), float("nan"), dtype=torch.float32, device="cuda")
-    st = dev.render_region(cam, seed, reg, out.data_ptr(), torch.cuda.current_stream().cuda_stream,
-                           counters=True, timed=True, flags=flags)
-    torch.cuda.synchronize()
-    return out[:rows, : reg.width].cpu().numpy(), st
-
-
-def check(gpu, st, desc, cam, seed, reg):
-    it, cnt = ob.render(desc, cam, seed, reg, ob.ORDER_ITERATIVE)
-    ref, _ = ob.render(desc, cam, seed, reg, ob.ORDER_REFERENCE)
-    assert np.isfinite(gpu).all()
-    assert np.array_equal(gpu, it), f"not bit-identical to the iterative oracle: max {np.abs(gpu - it).max()}"
-    assert float(np.abs(gpu - ref).max()) <= TOL
-    for k in ("samples", "segments", "node_visits", "prim_tests", "hits", "texel_fetches"):
-        assert getattr(st, k) == cnt[k], k
-    assert st.rng_draws == cnt["rng_draws"]
+    gpu, st, _ = check_scene(torch, dev, desc, cam, seed, reg, flags=flags)
+    return gpu, st
 
 
 @pytest.mark.gpu
@@ -198,8 +185,7 @@ def test_gpu_light_panel(torch_cuda, built):
     desc, keep = light_panel()
     cam = light_panel_camera(spp=4)
     reg = rtx.Region(0, 0, cam.image_width, cam.image_height, 0, 1)
-    gpu, st = gpu_render(torch_cuda, desc, cam, 3, reg)
-    check(gpu, st, desc, cam, 3, reg)
+    gpu, st = gpu_check(torch_cuda, desc, cam, 3, reg)
 
 
 @pytest.mark.gpu
@@ -208,8 +194,7 @@ def test_gpu_quad_demo_full(torch_cuda, built, flags):
     s = rtx.HostScene("quad_demo", 1)
     cam = s.camera(spp=8)
     reg = rtx.Region(0, 0, cam.image_width, cam.image_height, 0, 1)
-    gpu, st = gpu_render(torch_cuda, s.desc, cam, 7, reg, flags)
-    check(gpu, st, s.desc, cam, 7, reg)
+    gpu, st = gpu_check(torch_cuda, s.desc, cam, 7, reg, flags)
 
 
 @pytest.mark.gpu
@@ -219,8 +204,7 @@ def test_gpu_cornell_box_crop_full_spp(torch_cuda, built):
     cam = s.camera()
     assert cam.samples_per_pixel == 200
     reg = rtx.Region(250, 60, 48, 32, 0, 1)
-    gpu, st = gpu_render(torch_cuda, s.desc, cam, 11, reg)
-    check(gpu, st, s.desc, cam, 11, reg)
+    gpu, st = gpu_check(torch_cuda, s.desc, cam, 11, reg)
 
 
 @pytest.mark.gpu
@@ -228,10 +212,10 @@ def test_gpu_cornell_box_full_low_spp_and_shards(torch_cuda, built):
     s = rtx.HostScene("cornell_box", 1)
     cam = s.camera(spp=2)
     reg = rtx.Region(0, 0, 600, 600, 0, 1)
-    gpu, st = gpu_render(torch_cuda, s.desc, cam, 13, reg)
-    check(gpu, st, s.desc, cam, 13, reg)
+    gpu, st = gpu_check(torch_cuda, s.desc, cam, 13, reg)
+    dev = rtx.DeviceScene(s.desc)
     got = np.full_like(gpu, np.nan)
     for rank in range(3):
-        part, _ = gpu_render(torch_cuda, s.desc, cam, 13, rtx.Region(0, 0, 600, 600, rank, 3))
+        part, _ = gpu_region(torch_cuda, dev, cam, 13, rtx.Region(0, 0, 600, 600, rank, 3), counters=False)
         got[rank::3] = part
     assert np.array_equal(got, gpu)

@@ -161,9 +161,15 @@ def test_random_scene_bitexact(built, seed, n_spheres, n_quads, axis_aligned):
     torch.cuda.set_device(0)
     d = build_scene(seed, n_spheres, n_quads)
     cam = camera(seed, 64, 36, 6, axis_aligned)
-    dev = rtx.DeviceScene(ctypes.byref(d))
+    pd = ctypes.pointer(d)
+    dev = rtx.DeviceScene(pd)
+    walk = dev.walk_desc(pd, cam)  # the tree the scene walks (sphere-only trees may be rebuilt)
     reg = rtx.Region(0, 0, cam.image_width, cam.image_height, 0, 1)
-    it, cnt = ob.render(ctypes.byref(d), cam, seed, reg, ob.ORDER_ITERATIVE)
+    it, cnt = ob.render(walk, cam, seed, reg, ob.ORDER_ITERATIVE)
+    if walk is not pd:  # the rebuilt tree: same image and paths as the caller's tree on the oracle
+        it0, cnt0 = ob.render(pd, cam, seed, reg, ob.ORDER_ITERATIVE)
+        assert np.array_equal(it, it0, equal_nan=True)
+        assert all(cnt[k] == cnt0[k] for k in ("segments", "hits", "rng_draws"))
     out = torch.full((cam.image_height, cam.image_width, 3), float("nan"), device="cuda")
     for counters in (True, False):
         st = dev.render_region(cam, seed, reg, out.data_ptr(), torch.cuda.current_stream().cuda_stream,
