@@ -243,8 +243,14 @@ typedef struct rtx_stats {
                                        camera rays, segment starts (1/dir)                    */
     uint64_t walk_layout;   /* ABI 6: the layout walked: 0-7 = the camera octant of a rebuilt tree
                                (rtx_scene_topology), RTX_LAYOUT_REFERENCE = the caller's tree  */
+    uint64_t gather_kind;   /* ABI 6, rtx_render: how the bands were assembled (RTX_GATHER_*)    */
 } rtx_stats;
 #define RTX_LAYOUT_REFERENCE 8u
+#define RTX_GATHER_NONE 0u   /* one band: it is the image                                        */
+#define RTX_GATHER_RCCL 1u   /* ncclGather of the padded bands to device 0, de-interleave kernel  */
+#define RTX_GATHER_DEVICE 2u /* RTX_SIM_BANDS (tests): bands on device 0, device copies, kernel   */
+#define RTX_GATHER_HOST 3u   /* RCCL unavailable or failed (or RTX_NO_RCCL=1): each band's rows
+                                copied into the caller's buffer                                 */
 
 #define RTX_FLAG_COUNTERS 1u /* count work units (separate kernel instantiation) */
 #define RTX_FLAG_NO_LDS 4u   /* A/B: read the scene from global memory even if it fits LDS */
@@ -316,9 +322,21 @@ uint64_t rtx_scene_device_bytes(const rtx_scene* scene);
  * (rank d renders rows y = d, d + n, ...), gathers the equal-sized bands to device 0
  * with one RCCL ncclGather over xGMI (communicators from ncclCommInitAll, cached per
  * device set; librccl is loaded on first use), de-interleaves them on device 0 and
- * copies the image to the host.  RTX_ERR_RCCL if RCCL cannot be loaded or fails.    */
+ * copies the image to the host.  Without RCCL (not loadable, or a failing
+ * CommInitAll / Gather) each band's rows are copied into out_rgb instead: slower,
+ * same bits (stats->gather_kind says which).  The band, gather and image buffers are
+ * kept per device between calls (rtx_release_device_memory frees them).
+ * stats (optional) receives the time (kernel_ms, gather_ms), samples, sample_chunks,
+ * walk_layout and gather_kind of the call; its work counters stay 0: rtx_render runs the
+ * timed kernel.  rtx_render = rtx_render_ex(..., flags = 0, ...).                     */
 int rtx_render(rtx_scene* scene, const rtx_camera* cam, uint64_t seed, int n_gpus, float* out_rgb,
                rtx_stats* stats);
+
+/* ABI 6: rtx_render with flags: RTX_FLAG_COUNTERS runs the counting kernel instead (same
+ * image; every work counter of stats filled; about twice the kernel time of the timed
+ * kernel on the headline config).                                                     */
+int rtx_render_ex(rtx_scene* scene, const rtx_camera* cam, uint64_t seed, int n_gpus, uint32_t flags,
+                  float* out_rgb, rtx_stats* stats);
 
 /* Free the device memory the library keeps between renders on `device` (-1: every
  * device): the per-device sample-colour scratch (up to RTX_SCRATCH_MB, 12 B per

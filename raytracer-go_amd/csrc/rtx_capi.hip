@@ -206,6 +206,70 @@ void release_comms_locked() {  // g_rccl_mu held
     g_comms.clear();
 }
 
+// rtx_render's per-device buffers (bands, the gathered bands, the assembled image), stream and
+// gather events, kept between calls and freed by rtx_release_device_memory; g_render_mu is held
+// for a whole rtx_render.  Keyed by (device, slot): slot d >= 0 is band d, -1 the gather, -2 the
+// image.
+struct RenderBuf {
+    void* ptr = nullptr;
+    size_t bytes = 0;
+};
+std::mutex g_render_mu;
+std::map<std::pair<int, int>, RenderBuf> g_render_bufs;
+std::map<int, hipStream_t> g_render_streams;
+std::map<std::pair<int, int>, hipEvent_t> g_render_events;
+
+void* render_buffer(int device, int slot, size_t bytes) {  // current device = device
+    RenderBuf& b = g_render_bufs[{device, slot}];
+    if (b.bytes < bytes) {
+        if (b.ptr) (void)hipFree(b.ptr);
+        b = RenderBuf{};
+        if (hipMalloc(&b.ptr, bytes) != hipSuccess) return b.ptr = nullptr;
+        b.bytes = bytes;
+    }
+    return b.ptr;
+}
+hipStream_t render_stream(int device) {  // current device = device
+    hipStream_t& st = g_render_streams[device];
+    if (!st && hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) st = nullptr;
+    return st;
+}
+hipEvent_t render_event(int device, int k) {  // current device = device
+    hipEvent_t& ev = g_render_events[{device, k}];
+    if (!ev && hipEventCreate(&ev) != hipSuccess) ev = nullptr;
+    return ev;
+}
+void release_render_locked(int device) {  // g_render_mu held; device -1: all
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    for (auto it = g_render_bufs.begin(); it != g_render_bufs.end();) {
+        if ((device < 0 || it->first.first == device) && hipSetDevice(it->first.first) == hipSuccess) {
+            (void)hipDeviceSynchronize();
+            if (it->second.ptr) (void)hipFree(it->second.ptr);
+            it = g_render_bufs.erase(it);
+        } else {
+            ++it;
+        }
+    }
+    for (auto it = g_render_streams.begin(); it != g_render_streams.end();) {
+        if ((device < 0 || it->first == device) && hipSetDevice(it->first) == hipSuccess) {
+            if (it->second) (void)hipStreamDestroy(it->second);
+            it = g_render_streams.erase(it);
+        } else {
+            ++it;
+        }
+    }
+    for (auto it = g_render_events.begin(); it != g_render_events.end();) {
+        if ((device < 0 || it->first.first == device) && hipSetDevice(it->first.first) == hipSuccess) {
+            if (it->second) (void)hipEventDestroy(it->second);
+            it = g_render_events.erase(it);
+        } else {
+            ++it;
+        }
+    }
+    (void)hipSetDevice(cur);
+}
+
 }  // namespace
 
 struct rtx_scene {
@@ -245,8 +309,8 @@ int check_ref(const rtx_scene_desc* d, int32_t ref) {
     if (type == RTX_PRIM_LIST) {  // a nested World (ABI 5)
         if (idx >= d->n_lists || !d->lists) return fail(RTX_ERR_INVALID_ARG, "list ref %u out of range (%u lists)", idx, d->n_lists);
         const rtx_list& l = d->lists[idx];
-        if (l.count == 0) return fail(RTX_ERR_INVALID_ARG, "list %u is empty (a World with nothing added)", idx);
-        if (!d->list_refs || (uint64_t)l.first + l.count > d->n_list_refs)
+        // (an empty World is a well-defined miss, hittables.go:55-72: it emits no entries)
+        if (l.count && (!d->list_refs || (uint64_t)l.first + l.count > d->n_list_refs))
             return fail(RTX_ERR_INVALID_ARG, "list %u items out of range (%u list refs)", idx, d->n_list_refs);
         return RTX_OK;
     }
@@ -1030,6 +1094,11 @@ int rtx_render_region_device(rtx_scene* s, const rtx_camera* cam, uint64_t seed,
 }
 
 int rtx_render(rtx_scene* s, const rtx_camera* cam, uint64_t seed, int n_gpus, float* out_rgb, rtx_stats* stats) {
+    return rtx_render_ex(s, cam, seed, n_gpus, 0u, out_rgb, stats);
+}
+
+int rtx_render_ex(rtx_scene* s, const rtx_camera* cam, uint64_t seed, int n_gpus, uint32_t flags, float* out_rgb,
+                  rtx_stats* stats) {
     g_last_error.clear();
     if (!s || !out_rgb) return fail(RTX_ERR_INVALID_ARG, "NULL argument");
     if (int rc = check_camera(cam)) return rc;
@@ -1037,114 +1106,153 @@ int rtx_render(rtx_scene* s, const rtx_camera* cam, uint64_t seed, int n_gpus, f
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(RTX_ERR_NO_DEVICE, "no HIP device");
     if (n_gpus <= 0) n_gpus = 1;
     if (n_gpus > ndev) return fail(RTX_ERR_INVALID_ARG, "n_gpus=%d but %d devices visible", n_gpus, ndev);
-    if ((uint32_t)n_gpus > cam->image_height) n_gpus = (int)cam->image_height;
-    // RCCL for more than one device (RTX_FORCE_RCCL=1: also for one, a 1-rank gather)
-    const bool use_rccl = n_gpus > 1 || env_knob("RTX_FORCE_RCCL", 0, 0, 1) == 1;
+    // RTX_SIM_BANDS=k (tests, one device): k bands, all on device 0, gathered by device copies
+    const uint32_t sim = n_gpus == 1 ? env_knob("RTX_SIM_BANDS", 1, 1, 64) : 1u;
+    int n = sim > 1 ? (int)sim : n_gpus;
+    if ((uint32_t)n > cam->image_height) n = (int)cam->image_height;
+    auto dev_of = [&](int d) { return sim > 1 ? 0 : d; };
+    // the gather: RCCL for more than one device (RTX_FORCE_RCCL=1: also for one, a 1-rank gather);
+    // per-band copies into the caller's rows when RCCL is unavailable or fails (RTX_NO_RCCL=1: always)
+    const bool want_rccl = sim == 1 && (n > 1 || env_knob("RTX_FORCE_RCCL", 0, 0, 1) == 1);
+    const bool no_rccl = env_knob("RTX_NO_RCCL", 0, 0, 1) == 1;
+    const uint32_t kflags = flags & RTX_FLAG_COUNTERS;
     std::lock_guard<std::mutex> lk(s->mu);
+    std::lock_guard<std::mutex> bl(g_render_mu);  // the cached band / gather / image buffers
     int cur = 0;
     HIP_TRY(hipGetDevice(&cur));
-    const int n = n_gpus;
     const uint32_t W = cam->image_width, H = cam->image_height;
     const uint32_t R = (H + n - 1) / n;  // rows of band 0, the longest: every band is sent padded to R
-    const size_t band_floats = (size_t)R * W * 3;
+    const size_t band_floats = (size_t)R * W * 3, band_bytes = std::max<size_t>(band_floats, 1) * sizeof(float);
+    const size_t img_bytes = (size_t)H * W * 3 * sizeof(float);
     std::vector<float*> bufs(n, nullptr);
     std::vector<hipStream_t> streams(n, nullptr);
     std::vector<rtx_region> regs(n);
     std::vector<uint32_t> chunks(n, 0);
-    float *gathered = nullptr, *img = nullptr;
-    hipEvent_t g0 = nullptr, g1 = nullptr;
     rtx_stats total;
     std::memset(&total, 0, sizeof(total));
     int rc = RTX_OK;
-    // 1. Each device renders its row-interleaved band (rows y % n == d) concurrently.
+    // 1. Each band (rows y % n == d) renders on its device, the devices concurrently.
     for (int d = 0; d < n && rc == RTX_OK; ++d) {
+        const int dv = dev_of(d);
         DeviceCopy* c = nullptr;
-        if ((rc = ensure_device(s, d, &c))) break;
-        if (hipSetDevice(d) != hipSuccess) { rc = fail(RTX_ERR_HIP, "hipSetDevice(%d)", d); break; }
+        if ((rc = ensure_device(s, dv, &c))) break;
+        if (hipSetDevice(dv) != hipSuccess) { rc = fail(RTX_ERR_HIP, "hipSetDevice(%d)", dv); break; }
         regs[d] = rtx_region{0, 0, W, H, (uint32_t)d, (uint32_t)n};
-        if (hipStreamCreateWithFlags(&streams[d], hipStreamNonBlocking) != hipSuccess) { rc = fail(RTX_ERR_HIP, "stream"); break; }
-        if (hipMalloc(&bufs[d], std::max<size_t>(band_floats, 1) * sizeof(float)) != hipSuccess) {
-            rc = fail(RTX_ERR_OOM, "hipMalloc band %zu B", band_floats * sizeof(float));
+        if (!(streams[d] = render_stream(dv))) { rc = fail(RTX_ERR_HIP, "stream on device %d", dv); break; }
+        if (!(bufs[d] = static_cast<float*>(render_buffer(dv, d, band_bytes)))) {
+            rc = fail(RTX_ERR_OOM, "hipMalloc band %zu B", band_bytes);
             break;
         }
-        rc = enqueue_on(s, c, cam, seed, &regs[d], bufs[d], streams[d], stats ? RTX_FLAG_COUNTERS : 0u, true, &chunks[d]);
+        rc = enqueue_on(s, c, cam, seed, &regs[d], bufs[d], streams[d], kflags, true, &chunks[d]);
     }
     // 2. Wait for every band (and read its counters), so gather_ms times only the gather.
     for (int d = 0; d < n && rc == RTX_OK; ++d) {
-        if (hipSetDevice(d) != hipSuccess) { rc = fail(RTX_ERR_HIP, "hipSetDevice(%d)", d); break; }
+        if (hipSetDevice(dev_of(d)) != hipSuccess) { rc = fail(RTX_ERR_HIP, "hipSetDevice(%d)", dev_of(d)); break; }
         rtx_stats st;
         uint64_t samples = (uint64_t)region_rows(&regs[d]) * W * cam->samples_per_pixel;
-        if ((rc = collect_on(&s->copies[d], stats != nullptr, samples, chunks[d], &st))) break;
+        if ((rc = collect_on(&s->copies[dev_of(d)], kflags != 0, samples, chunks[d], &st))) break;
         add_stats(&total, st);
     }
-    // 3. Assemble: one ncclGather of the padded bands to device 0 over xGMI, the
-    //    de-interleave on device 0, then the copy into the caller's buffer.
-    if (rc == RTX_OK && use_rccl) {
-        std::lock_guard<std::mutex> rl(g_rccl_mu);
-        const RcclApi* api = rccl_api();
-        if (!api) rc = fail(RTX_ERR_RCCL, "%s", g_rccl.err.c_str());
-        std::vector<ncclComm_t>* comms = nullptr;
-        if (rc == RTX_OK) {
+    // 3. Assemble on device 0: the padded bands gathered (one ncclGather over xGMI, or device
+    //    copies of simulated bands), de-interleaved by a kernel, copied into the caller's buffer;
+    //    or, without RCCL, each band's rows copied straight into the caller's rows.
+    uint32_t kind = n == 1 && !want_rccl ? RTX_GATHER_NONE : (sim > 1 ? RTX_GATHER_DEVICE : RTX_GATHER_RCCL);
+    std::vector<ncclComm_t>* comms = nullptr;
+    const RcclApi* api = nullptr;
+    std::unique_lock<std::mutex> rl(g_rccl_mu, std::defer_lock);
+    if (rc == RTX_OK && kind == RTX_GATHER_RCCL) {
+        rl.lock();
+        api = no_rccl ? nullptr : rccl_api();
+        if (api) {
             auto it = g_comms.find(n);
             if (it == g_comms.end()) {
                 std::vector<ncclComm_t> cs(n, nullptr);
                 std::vector<int> devs(n);
                 for (int d = 0; d < n; ++d) devs[d] = d;
-                const ncclResult_t e = api->CommInitAll(cs.data(), n, devs.data());
-                if (e != ncclSuccess) rc = fail(RTX_ERR_RCCL, "ncclCommInitAll(%d): %s", n, api->GetErrorString(e));
-                else it = g_comms.emplace(n, cs).first;
+                if (api->CommInitAll(cs.data(), n, devs.data()) == ncclSuccess) it = g_comms.emplace(n, cs).first;
             }
-            if (rc == RTX_OK) comms = &it->second;
+            if (it != g_comms.end()) comms = &it->second;
         }
-        if (rc == RTX_OK) {
-            if (hipSetDevice(0) != hipSuccess || hipMalloc(&gathered, (size_t)n * band_floats * sizeof(float)) != hipSuccess ||
-                hipMalloc(&img, (size_t)H * W * 3 * sizeof(float)) != hipSuccess ||
-                hipEventCreate(&g0) != hipSuccess || hipEventCreate(&g1) != hipSuccess ||
-                hipEventRecord(g0, streams[0]) != hipSuccess)
-                rc = fail(RTX_ERR_OOM, "device-0 buffers for the gather of %d bands", n);
-        }
-        if (rc == RTX_OK) {
-            ncclResult_t e = api->GroupStart();
-            for (int d = 0; d < n && e == ncclSuccess; ++d)
-                e = api->Gather(bufs[d], d == 0 ? gathered : nullptr, band_floats, ncclFloat, 0, (*comms)[d], streams[d]);
-            const ncclResult_t e2 = api->GroupEnd();
-            if (e == ncclSuccess) e = e2;
-            if (e != ncclSuccess) rc = fail(RTX_ERR_RCCL, "ncclGather: %s", api->GetErrorString(e));
-        }
-        if (rc == RTX_OK) {
-            (void)hipSetDevice(0);
-            const uint64_t total_floats = (uint64_t)H * W * 3;
-            hipLaunchKernelGGL(deinterleave_bands, dim3((uint32_t)((total_floats + 255) / 256)), dim3(256), 0, streams[0],
-                               gathered, img, (uint32_t)n, R, H, W * 3);
-            hipError_t e = hipGetLastError();
-            if (e == hipSuccess) e = hipEventRecord(g1, streams[0]);
-            if (e == hipSuccess) e = copy_to_host(out_rgb, img, total_floats * sizeof(float), streams[0]);
-            for (int d = 1; d < n && e == hipSuccess; ++d)
-                if ((e = hipSetDevice(d)) == hipSuccess) e = hipStreamSynchronize(streams[d]);
-            float ms = 0.0f;
-            if (e == hipSuccess && hipSetDevice(0) == hipSuccess) e = hipEventElapsedTime(&ms, g0, g1);
-            if (e != hipSuccess) rc = fail(RTX_ERR_HIP, "band assembly: %s", hipGetErrorString(e));
-            total.gather_ms = ms;
-        }
-    } else if (rc == RTX_OK) {  // one device, no RCCL: the band is the image
+        if (!comms) kind = RTX_GATHER_HOST;  // RCCL unavailable: per-band copies
+    }
+    if (rc == RTX_OK && sim > 1 && no_rccl) kind = RTX_GATHER_HOST;
+    hipEvent_t g0 = nullptr, g1 = nullptr;
+    if (rc == RTX_OK && kind != RTX_GATHER_NONE) {
         (void)hipSetDevice(0);
-        hipError_t e = copy_to_host(out_rgb, bufs[0], (size_t)H * W * 3 * sizeof(float), streams[0]);
+        g0 = render_event(0, 0);
+        g1 = render_event(0, 1);
+        if (!g0 || !g1 || hipEventRecord(g0, streams[0]) != hipSuccess) rc = fail(RTX_ERR_HIP, "gather events");
+    }
+    float* gathered = nullptr;
+    float* img = nullptr;
+    if (rc == RTX_OK && (kind == RTX_GATHER_RCCL || kind == RTX_GATHER_DEVICE)) {
+        (void)hipSetDevice(0);
+        gathered = static_cast<float*>(render_buffer(0, -1, (size_t)n * band_bytes));
+        img = static_cast<float*>(render_buffer(0, -2, img_bytes));
+        if (!gathered || !img) rc = fail(RTX_ERR_OOM, "device-0 buffers for the gather of %d bands", n);
+    }
+    if (rc == RTX_OK && kind == RTX_GATHER_RCCL) {
+        ncclResult_t e = api->GroupStart();
+        for (int d = 0; d < n && e == ncclSuccess; ++d)
+            e = api->Gather(bufs[d], d == 0 ? gathered : nullptr, band_floats, ncclFloat, 0, (*comms)[d], streams[d]);
+        const ncclResult_t e2 = api->GroupEnd();
+        if (e == ncclSuccess) e = e2;
+        if (e != ncclSuccess) {  // degrade to per-band copies (the bands are intact)
+            for (int d = 0; d < n; ++d)
+                if (hipSetDevice(d) == hipSuccess) (void)hipStreamSynchronize(streams[d]);
+            (void)hipSetDevice(0);
+            (void)hipEventRecord(g0, streams[0]);
+            kind = RTX_GATHER_HOST;
+        }
+    }
+    if (rc == RTX_OK && kind == RTX_GATHER_DEVICE) {
+        for (int d = 0; d < n && rc == RTX_OK; ++d)
+            if (hipMemcpyAsync(gathered + (size_t)d * (band_bytes / sizeof(float)), bufs[d], band_bytes,
+                               hipMemcpyDeviceToDevice, streams[0]) != hipSuccess)
+                rc = fail(RTX_ERR_HIP, "band copy %d", d);
+    }
+    if (rc == RTX_OK && (kind == RTX_GATHER_RCCL || kind == RTX_GATHER_DEVICE)) {
+        (void)hipSetDevice(0);
+        const uint64_t total_floats = (uint64_t)H * W * 3;
+        hipLaunchKernelGGL(deinterleave_bands, dim3((uint32_t)((total_floats + 255) / 256)), dim3(256), 0, streams[0],
+                           gathered, img, (uint32_t)n, R, H, W * 3);
+        hipError_t e = hipGetLastError();
+        if (e == hipSuccess) e = hipEventRecord(g1, streams[0]);
+        if (e == hipSuccess) e = copy_to_host(out_rgb, img, total_floats * sizeof(float), streams[0]);
+        for (int d = 1; d < n && e == hipSuccess; ++d)
+            if ((e = hipSetDevice(dev_of(d))) == hipSuccess) e = hipStreamSynchronize(streams[d]);
+        if (e != hipSuccess) rc = fail(RTX_ERR_HIP, "band assembly: %s", hipGetErrorString(e));
+    } else if (rc == RTX_OK && kind == RTX_GATHER_HOST) {
+        // band d holds image rows y = d + r n: one strided copy per band into the caller's rows
+        for (int d = 0; d < n && rc == RTX_OK; ++d) {
+            const uint32_t rows = region_rows(&regs[d]);
+            if (!rows) continue;
+            if (hipSetDevice(dev_of(d)) != hipSuccess ||
+                hipMemcpy2DAsync(out_rgb + (size_t)d * W * 3, (size_t)n * W * 3 * sizeof(float), bufs[d],
+                                 (size_t)W * 3 * sizeof(float), (size_t)W * 3 * sizeof(float), rows,
+                                 hipMemcpyDeviceToHost, streams[d]) != hipSuccess)
+                rc = fail(RTX_ERR_HIP, "band %d copy to the host", d);
+        }
+        for (int d = 0; d < n; ++d)
+            if (hipSetDevice(dev_of(d)) == hipSuccess && hipStreamSynchronize(streams[d]) != hipSuccess && rc == RTX_OK)
+                rc = fail(RTX_ERR_HIP, "band %d copy to the host", d);
+        if (rc == RTX_OK && (hipSetDevice(0) != hipSuccess || hipEventRecord(g1, streams[0]) != hipSuccess ||
+                             hipEventSynchronize(g1) != hipSuccess))
+            rc = fail(RTX_ERR_HIP, "gather event");
+    } else if (rc == RTX_OK) {  // one device, no gather: the band is the image
+        (void)hipSetDevice(0);
+        hipError_t e = copy_to_host(out_rgb, bufs[0], img_bytes, streams[0]);
         if (e != hipSuccess) rc = fail(RTX_ERR_HIP, "copy image: %s", hipGetErrorString(e));
     }
-    for (int d = 0; d < n; ++d) {
-        if (hipSetDevice(d) != hipSuccess) continue;
-        if (streams[d]) (void)hipStreamSynchronize(streams[d]);
-        if (bufs[d]) (void)hipFree(bufs[d]);
-        if (d == 0) {
-            if (gathered) (void)hipFree(gathered);
-            if (img) (void)hipFree(img);
-            if (g0) (void)hipEventDestroy(g0);
-            if (g1) (void)hipEventDestroy(g1);
-        }
-        if (streams[d]) (void)hipStreamDestroy(streams[d]);
+    if (rc == RTX_OK && kind != RTX_GATHER_NONE) {
+        float ms = 0.0f;
+        if (hipSetDevice(0) == hipSuccess && hipEventElapsedTime(&ms, g0, g1) == hipSuccess) total.gather_ms = ms;
     }
+    for (int d = 0; d < n; ++d)  // nothing of this call still in flight when the buffers are reused
+        if (streams[d] && hipSetDevice(dev_of(d)) == hipSuccess) (void)hipStreamSynchronize(streams[d]);
     (void)hipSetDevice(cur);
     total.walk_layout = walk_layout(s, cam);
+    total.gather_kind = kind;
     if (rc == RTX_OK && stats) *stats = total;
     return rc;
 }
@@ -1173,6 +1281,10 @@ int rtx_release_device_memory(int device) {
     if (device < 0) {
         std::lock_guard<std::mutex> lk(g_stage_mu);
         release_stage_locked();
+    }
+    {
+        std::lock_guard<std::mutex> lk(g_render_mu);
+        release_render_locked(device);
     }
     {  // communicators span devices 0..n-1: any release drops them all
         std::lock_guard<std::mutex> lk(g_rccl_mu);
@@ -1238,20 +1350,14 @@ int rtx_render_ppm(rtx_scene* s, const rtx_camera* cam, uint64_t seed, char* out
     if (int rc = check_camera(cam)) return rc;
     const uint32_t W = cam->image_width, H = cam->image_height;
     const uint64_t need = rtxd::ppm_max_bytes(W, H);
-    float* rgb = nullptr;
-    char* text = nullptr;
-    hipStream_t st = nullptr;
-    auto cleanup = [&]() {
-        if (st) (void)hipStreamDestroy(st);
-        (void)hipFree(rgb);
-        (void)hipFree(text);
-    };
-    HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
-    if (hipMalloc(&rgb, std::max<size_t>(1, (size_t)W * H * 3 * sizeof(float))) != hipSuccess ||
-        hipMalloc(&text, need) != hipSuccess) {
-        cleanup();
-        return fail(RTX_ERR_OOM, "device buffers for a %ux%u PPM", W, H);
-    }
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev));
+    std::lock_guard<std::mutex> bl(g_render_mu);  // the cached image / text buffers and stream
+    hipStream_t st = render_stream(dev);
+    float* rgb = static_cast<float*>(render_buffer(dev, -3, std::max<size_t>(1, (size_t)W * H * 3 * sizeof(float))));
+    char* text = static_cast<char*>(render_buffer(dev, -4, need));
+    if (!st) return fail(RTX_ERR_HIP, "stream on device %d", dev);
+    if (!rgb || !text) return fail(RTX_ERR_OOM, "device buffers for a %ux%u PPM", W, H);
     rtx_region reg{0, 0, W, H, 0, 1};
     rtx_stats local;
     int rc = rtx_render_region_device(s, cam, seed, &reg, rgb, st, 0, stats ? stats : &local);
@@ -1261,7 +1367,7 @@ int rtx_render_ppm(rtx_scene* s, const rtx_camera* cam, uint64_t seed, char* out
                                                   (unsigned long long)capacity, (unsigned long long)len);
     if (rc == RTX_OK && copy_to_host(out_text, text, len, st) != hipSuccess)
         rc = fail(RTX_ERR_HIP, "copying the PPM text to the host");
-    cleanup();
+    (void)hipStreamSynchronize(st);
     if (rc == RTX_OK) *out_len = len;
     return rc;
 }

@@ -1218,8 +1218,13 @@ __device__ __forceinline__ uint32_t trav_step_batched(Trav& t, const Ray& r, con
 // The whole traversal phase (traverse_loop's !COUNT body for this case): RTX_ASM_BLOCK asm steps
 // (RTX_ASM_BLOCK_Q with quads), then the
 // vote — at_end = pos >= end, walking lanes W, waiting lanes P0 — until no lane walks or at
-// least `thresh` wait; returns the final at_end mask.  Positions only increase along a walk, so
-// every lane reaches the sentinel and the loop ends.
+// least `thresh` wait; returns the final at_end mask.  Termination: storage positions do NOT
+// increase along a walk (a scene in the LDS copy stores its primitives first), but every step
+// moves a lane to a later entry of the threaded pre-order (a node's next is its first child, its
+// escape the entry after its subtree; a primitive's next the entry after it), the upload emits
+// that order from an acyclic tree (check_acyclic, rtx_capi.hip), and the sentinel ends it: every
+// lane reaches the sentinel within n_entries steps.  The watchdog (RTX_WATCHDOG_S) is checked
+// only between phases in render_items' loop and cannot interrupt this asm loop.
 #define RTX_WALK_VOTE                                                        \
         "v_cmp_ge_u32_e64 %[pm], %[pos], %[end]\n\t"                         \
         "s_andn2_b64 %[wk], %[W], %[pm]\n\t" /* still walking (scc: any) */  \

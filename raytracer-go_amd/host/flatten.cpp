@@ -171,7 +171,7 @@ struct Flattener {
                 fs.quads.push_back(qd);
                 refs[h] = r;
             } else if (auto w = dynamic_cast<const World*>(h)) {  // a nested World: a list ref (ABI 5)
-                if (w->hittables.empty()) return fail(RTX_ERR_INVALID_ARG, "empty World nested in the tree");
+                // (an empty World is a miss, hittables.go:55-72: a list of no items, which emits nothing)
                 rtx_list l{(uint32_t)fs.list_refs.size(), (uint32_t)w->hittables.size()};
                 r = RTX_REF_PRIM(RTX_PRIM_LIST, fs.lists.size());
                 fs.lists.push_back(l);

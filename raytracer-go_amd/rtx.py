@@ -30,6 +30,7 @@ RTX_FLAG_COUNTERS = 1
 RTX_FLAG_NO_LDS = 4
 RTX_SCENE_REFERENCE_BVH = 1  # rtx_scene_create_ex: keep the caller's tree and the reference's visit order
 RTX_LAYOUT_REFERENCE = 8  # Stats.walk_layout of a scene walking the caller's tree
+RTX_GATHER_NONE, RTX_GATHER_RCCL, RTX_GATHER_DEVICE, RTX_GATHER_HOST = 0, 1, 2, 3  # Stats.gather_kind
 RTX_IMAGE_TEXEL_WORDS = 2  # RGBA16 image texels: two uint32 words each (rtx.h)
 
 
@@ -102,7 +103,7 @@ class Stats(ctypes.Structure):
                 ("shade_lanes", c_uint64), ("trav_cycles", c_uint64), ("shade_cycles", c_uint64),
                 ("idle_lanes", c_uint64), ("cache_hits", c_uint64), ("sample_chunks", c_uint64),
                 ("parked_lanes", c_uint64), ("deferred_lanes", c_uint64), ("shade_split_cycles", c_uint64 * 4),
-                ("walk_layout", c_uint64)]
+                ("walk_layout", c_uint64), ("gather_kind", c_uint64)]
 
     def as_dict(self) -> dict:
         return {name: (list(v) if not isinstance(v := getattr(self, name), (int, float)) else v)
@@ -114,7 +115,7 @@ RTX_SYMBOLS = [
     "rtx_scene_destroy", "rtx_scene_device_bytes", "rtx_render", "rtx_render_region_device", "rtx_region_rows",
     "rtx_ppm_max_bytes", "rtx_encode_ppm_device", "rtx_render_ppm", "rtx_scene_create_spheres", "rtx_scene_export",
     "rtx_release_device_memory", "rtx_device_scratch_bytes", "rtx_scene_create_ex", "rtx_scene_topology",
-    "rtx_camera_octant", "rtx_walk_tree",
+    "rtx_camera_octant", "rtx_walk_tree", "rtx_render_ex",
 ]
 RTXHOST_SYMBOLS = [
     "rtxhost_build_scene", "rtxhost_scene_free", "rtxhost_scene_desc", "rtxhost_scene_camera",
@@ -168,6 +169,8 @@ def load() -> ctypes.CDLL:
     L.rtx_scene_device_bytes.restype = c_uint64
     L.rtx_render.argtypes = [c_void_p, POINTER(Camera), c_uint64, c_int, c_void_p, POINTER(Stats)]
     L.rtx_render.restype = c_int
+    L.rtx_render_ex.argtypes = [c_void_p, POINTER(Camera), c_uint64, c_int, c_uint32, c_void_p, POINTER(Stats)]
+    L.rtx_render_ex.restype = c_int
     L.rtx_render_region_device.argtypes = [c_void_p, POINTER(Camera), c_uint64, POINTER(Region), c_void_p,
                                            c_void_p, c_uint32, POINTER(Stats)]
     L.rtx_render_region_device.restype = c_int
@@ -364,12 +367,17 @@ class DeviceScene:
         check(rc, "rtx_render_region_device")
         return st
 
-    def render_host(self, cam: Camera, seed: int, n_gpus: int = 1, stats: bool = False):
+    def render_host(self, cam: Camera, seed: int, n_gpus: int = 1, stats: bool = False, counters: bool = False):
+        """rtx_render (counters=False: the timed kernel) or rtx_render_ex(RTX_FLAG_COUNTERS) into a host array."""
         import numpy as np
         out = np.zeros((cam.image_height, cam.image_width, 3), dtype=np.float32)
-        st = Stats() if stats else None
-        rc = load().rtx_render(self._h, ctypes.byref(cam), seed, n_gpus, out.ctypes.data_as(c_void_p),
-                               ctypes.byref(st) if st is not None else None)
+        st = Stats() if (stats or counters) else None
+        if counters:
+            rc = load().rtx_render_ex(self._h, ctypes.byref(cam), seed, n_gpus, RTX_FLAG_COUNTERS,
+                                      out.ctypes.data_as(c_void_p), ctypes.byref(st))
+        else:
+            rc = load().rtx_render(self._h, ctypes.byref(cam), seed, n_gpus, out.ctypes.data_as(c_void_p),
+                                   ctypes.byref(st) if st is not None else None)
         check(rc, "rtx_render")
         return out, st
 

@@ -44,7 +44,8 @@ def test_rccl_gather_path_one_device(built):
         "os.environ['RTX_FORCE_RCCL'] = '1'; b, sb = d.render_host(cam, 7, n_gpus=1, stats=True)\n"
         "assert np.array_equal(a, b), 'rccl path differs'\n"
         "assert sa.gather_ms == 0 and sb.gather_ms > 0, (sa.gather_ms, sb.gather_ms)\n"
-        "assert sa.segments == sb.segments and sb.samples == 320 * 180 * 4\n"
+        "assert (sa.gather_kind, sb.gather_kind) == (rtx.RTX_GATHER_NONE, rtx.RTX_GATHER_RCCL)\n"
+        "assert sa.segments == sb.segments == 0 and sb.samples == 320 * 180 * 4  # the timed kernel\n"
         "rtx.release_device_memory(-1)\n"
         "print('ok', sb.gather_ms)\n")
     assert out.startswith("ok")
@@ -60,8 +61,10 @@ def test_rtx_render_every_device(built):
         f"n = {n}\n"
         "s = rtx.HostScene('random_spheres', 1); d = rtx.DeviceScene(s.desc)\n"
         "cam = s.camera(width=400, spp=8)\n"
-        "a, sa = d.render_host(cam, 3, n_gpus=1, stats=True)\n"
-        "b, sb = d.render_host(cam, 3, n_gpus=n, stats=True)\n"
+        "a, sa = d.render_host(cam, 3, n_gpus=1, counters=True)\n"
+        "b, sb = d.render_host(cam, 3, n_gpus=n, counters=True)\n"
+        "c, sc = d.render_host(cam, 3, n_gpus=n, stats=True)\n"
+        "assert np.array_equal(a, c) and sc.gather_kind == rtx.RTX_GATHER_RCCL\n"
         "assert np.array_equal(a, b)\n"
         "for k in ('samples', 'segments', 'node_visits', 'prim_tests', 'hits', 'rng_draws'):\n"
         "    assert getattr(sa, k) == getattr(sb, k), k\n"
@@ -129,3 +132,59 @@ def test_watchdog_stops_v3(built):
         "print('next render ok')\n",
         env={"RTX_WATCHDOG_S": "0.02"})
     assert f"ERR {rtx.RTX_ERR_HIP}" in out and "next render ok" in out, out
+
+
+@pytest.mark.parametrize("bands", [2, 3, 5, 7])
+def test_band_assembly_index_math_one_gpu(built, bands):
+    """The n > 1 assembly on one GPU (RTX_SIM_BANDS=k: k row-interleaved bands rendered on device 0,
+    each padded to R = ceil(H / k) rows, placed at band offsets as the RCCL gather places them,
+    de-interleaved by the kernel; with RTX_NO_RCCL=1 each band's rows copied straight into the
+    caller's rows instead).  H = 112 is not a multiple of 3, 5 or 7: ragged last bands."""
+    out = child(
+        f"k = {bands}\n"
+        "import os\n"
+        "s = rtx.HostScene('random_spheres', 1); d = rtx.DeviceScene(s.desc)\n"
+        "cam = s.camera(width=200, spp=3)\n"
+        "assert cam.image_height == 112\n"
+        "a, sa = d.render_host(cam, 9, stats=True)\n"
+        "os.environ['RTX_SIM_BANDS'] = str(k)\n"
+        "b, sb = d.render_host(cam, 9, stats=True)\n"
+        "assert np.array_equal(a, b), 'device gather differs'\n"
+        "assert sb.gather_kind == rtx.RTX_GATHER_DEVICE and sb.samples == sa.samples, sb.gather_kind\n"
+        "os.environ['RTX_NO_RCCL'] = '1'\n"
+        "c, sc = d.render_host(cam, 9, stats=True)\n"
+        "assert np.array_equal(a, c), 'host band copies differ'\n"
+        "assert sc.gather_kind == rtx.RTX_GATHER_HOST\n"
+        "del os.environ['RTX_SIM_BANDS']\n"
+        "os.environ['RTX_FORCE_RCCL'] = '1'  # the RCCL path with RCCL unavailable: host copies\n"
+        "e, se = d.render_host(cam, 9, stats=True)\n"
+        "assert np.array_equal(a, e) and se.gather_kind == rtx.RTX_GATHER_HOST\n"
+        "rtx.release_device_memory(-1)\n"
+        "print('ok')\n")
+    assert out.strip().endswith("ok")
+
+
+def test_rtx_render_stats_run_the_timed_kernel(built):
+    """rtx_render(..., &stats) times the timed kernel (no work counters, about the kernel time of
+    rtx_render_region_device without counters); rtx_render_ex(RTX_FLAG_COUNTERS) runs the
+    counting kernel: same image, counters filled.  The buffers are reused across calls."""
+    out = child(
+        "s = rtx.HostScene('random_spheres', 1); d = rtx.DeviceScene(s.desc)\n"
+        "cam = s.camera(width=1920, spp=24)\n"
+        "reg = rtx.Region(0, 0, 1920, 1080, 0, 1)\n"
+        "o = torch.empty((1080, 1920, 3), device='cuda')\n"
+        "d.render_host(cam, 4, stats=True)  # warm-up\n"
+        "t = [d.render_region(cam, 4, reg, o.data_ptr(), 0, timed=True).kernel_ms for _ in range(3)]\n"
+        "free0 = torch.cuda.mem_get_info()[0]\n"
+        "runs = [d.render_host(cam, 4, stats=True) for _ in range(3)]\n"
+        "free1 = torch.cuda.mem_get_info()[0]\n"
+        "a, sa = runs[-1]\n"
+        "b, sb = d.render_host(cam, 4, counters=True)\n"
+        "assert np.array_equal(a, b) and np.array_equal(a, o.cpu().numpy())\n"
+        "assert sa.segments == 0 and sb.segments > 0 and sb.node_visits > 0\n"
+        "k = min(r[1].kernel_ms for r in runs)\n"
+        "assert abs(k - min(t)) < 0.1 * min(t), (k, t)\n"
+        "assert sb.kernel_ms > 1.2 * k, (sb.kernel_ms, k)\n"
+        "assert abs(free1 - free0) < (16 << 20), (free0, free1)  # no new buffers per call\n"
+        "print('ok', k, min(t), sb.kernel_ms)\n")
+    assert out.split()[0] == "ok"
