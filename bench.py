@@ -52,8 +52,8 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0, help="0: the host's CPU share per GPU")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-hash", action="store_true", help="skip the framebuffer hash")
-    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_r02.json"))
-    ap.add_argument("--valu", default=os.path.join(ROOT, "profiles", "valu_r02.json"))
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_r03.json"))
+    ap.add_argument("--valu", default=os.path.join(ROOT, "profiles", "valu_r03.json"))
     # launcher self-test on the CPU (tests/test_bench_launcher.py): gloo, no GPU, shards filled
     # with a known function of the global pixel instead of rendered
     ap.add_argument("--rehearse-one-gpu", action="store_true",
@@ -181,42 +181,77 @@ def schedule(st: dict) -> dict:
     return out
 
 
-def load_profile(path: str, workload: str):
+def lib_sha16() -> str:
+    """sha256 prefix of the librtx.so this process renders with (rtx.load(): RTX_LIB or the in-tree build)."""
+    import rtx
+
+    path = os.environ.get("RTX_LIB") or rtx.lib_path("librtx.so")
+    with open(path, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()[:16]
+
+
+def load_profile(path: str, workload: str, lib: str):
+    """A committed PMC summary, if it was measured on this workload with this very library
+    (pmc_valu.py / pmc_traffic.py record the library's hash); else (None, why)."""
     if not os.path.exists(path):
-        return None
+        return None, f"{os.path.relpath(path, ROOT)} missing"
     with open(path) as f:
         d = json.load(f)
-    return d if d.get("workload") == workload else None
+    if d.get("workload") != workload:
+        return None, f"{os.path.relpath(path, ROOT)} is for {d.get('workload')}, not {workload}"
+    if d.get("librtx_sha256_16") != lib:
+        return None, (f"{os.path.relpath(path, ROOT)} was measured on librtx {d.get('librtx_sha256_16')}, "
+                      f"this run loads {lib}: stale, frac not derived")
+    return d, None
 
 
-def roofline(st: dict, pixels: int, kernel_s: float, workload: str, traffic_path: str, valu_path: str) -> dict:
+def served_from(st: dict, lds_scene: bool) -> str:
+    """Where the walk's entry reads come from."""
+    reads = st.get("node_visits", 0) + st.get("prim_tests", 0)
+    if lds_scene:
+        return "LDS (whole scene + material table copied per workgroup)"
+    if st.get("cache_hits") and reads:
+        h = st["cache_hits"] / reads
+        return f"LDS cache of the top levels {h:.1%} of entry reads, the other {1 - h:.1%} L2/MALL/HBM"
+    return "L2/MALL/HBM (scene in HBM, no LDS cache)"
+
+
+def roofline(st: dict, pixels: int, kernel_s: float, workload: str, traffic_path: str, valu_path: str,
+             lds_scene: bool) -> dict:
     """The render kernel's roof is VALU issue: its scene and materials are
     LDS-resident, HBM carries only the sample scratch.  achieved = the committed PMC pass's VALU
-    wave-instructions per launch (same kernel, same workload) / this run's HIP-event time of
-    the launch; peak = 1024 SIMDs x 2.4 GHz / 2 cycles per wave64 instruction.  The SURVEY §8(d)
-    algorithmic bytes (LDS-served, not HBM) and the measured HBM bytes are reported beside it."""
+    wave-instructions per launch (same kernel, same workload, same librtx.so by hash) / this run's
+    HIP-event time of the launch; peak = 1024 SIMDs x 2.4 GHz / 2 cycles per wave64 instruction.
+    A profile of another library build leaves achieved / frac null (stale).  The SURVEY §8(d)
+    algorithmic bytes and the measured HBM bytes are reported beside it."""
     launch_bytes = alg_bytes(st, pixels)
-    tr = load_profile(traffic_path, workload)
-    vr = load_profile(valu_path, workload)
+    lib = lib_sha16()
+    tr, tr_why = load_profile(traffic_path, workload, lib)
+    vr, vr_why = load_profile(valu_path, workload, lib)
     out = {"bound": "valu", "achieved": None, "peak": round(VALU_PEAK_GINST, 1), "unit": "Gwave-inst/s",
-           "frac": None, "traffic": tr.get("hbm_bytes_per_launch") if tr else None}
+           "frac": None, "traffic": tr.get("hbm_bytes_per_launch") if tr else None, "librtx_sha256_16": lib}
     if vr:
         achieved = vr["valu_insts_per_launch"] / kernel_s / 1e9
         out.update(achieved=round(achieved, 1), frac=round(achieved / VALU_PEAK_GINST, 4),
                    lane_frac=vr["valu_lane_frac"], pmc_issue_frac=vr["valu_issue_frac"],
                    valu_insts_per_launch=vr["valu_insts_per_launch"], source=os.path.relpath(valu_path, ROOT))
+    else:
+        out["stale"] = vr_why
+    src = served_from(st, lds_scene)
     out["alg_bytes"] = {
         "per_launch": launch_bytes,
         "achieved_gbs": round(launch_bytes / kernel_s / 1e9, 1),
-        "served_from": "LDS (scene + material table copied per workgroup)",
-        "frac_of_lds_read_peak": round(launch_bytes / kernel_s / 1e9 / LDS_READ_PEAK_GBS, 4),
-        "frac_of_hbm_peak_if_it_were_hbm": round(launch_bytes / kernel_s / 1e9 / HBM_PEAK_GBS, 4),
+        "served_from": src,
     }
+    if lds_scene:
+        out["alg_bytes"]["frac_of_lds_read_peak"] = round(launch_bytes / kernel_s / 1e9 / LDS_READ_PEAK_GBS, 4)
     if tr:
         out["hbm"] = {"bytes_per_launch": tr["hbm_bytes_per_launch"],
                       "achieved_gbs": round(tr["hbm_bytes_per_launch"] / kernel_s / 1e9, 1),
                       "frac": round(tr["hbm_bytes_per_launch"] / kernel_s / 1e9 / HBM_PEAK_GBS, 4),
                       "source": os.path.relpath(traffic_path, ROOT)}
+    else:
+        out["hbm"] = {"stale": tr_why}
     return out
 
 
@@ -280,24 +315,36 @@ def main():
         dist.all_reduce(counts)
     tot = dict(zip(keys, counts.tolist()))
 
-    def step(times):
+    def step(times, gathers):
         s = dev.render_region(cam, args.seed, reg, shard.data_ptr(), stream, counters=False, timed=True)
         times.append(s.kernel_ms)
-        return gather_image(shard.cpu() if shared else shard, H, rank, world)
+        g0 = time.perf_counter()  # (render_region waited for this rank's kernel)
+        out = gather_image(shard.cpu() if shared else shard, H, rank, world)
+        if world > 1 and out is not None and not shared:
+            torch.cuda.synchronize()
+        gathers.append((time.perf_counter() - g0) * 1e3)
+        return out
 
     for _ in range(args.warmup):
-        step([])
+        step([], [])
     barrier()
-    kms = []
+    kms, gms = [], []
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        img = step(kms)
+        img = step(kms, gms)
     barrier()
     elapsed = time.perf_counter() - t0
     t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if shared else "cuda")
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
+    # per-rank kernel time (HIP events on this rank's stream), to tell imbalance from gather cost
+    mine = torch.tensor([sum(kms) / len(kms)], dtype=torch.float64, device="cpu" if shared else "cuda")
+    per_rank = [mine]
+    if world > 1:
+        per_rank = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(per_rank, mine)
+    rank_kms = [float(x.item()) for x in per_rank]
 
     if rank == 0:
         assert img is not None and tuple(img.shape) == (H, W, 3)
@@ -341,10 +388,16 @@ def main():
             "segments_per_sample": round(tot["segments"] / tot["samples"], 4),
             "node_visits_per_segment": round(tot["node_visits"] / tot["segments"], 3),
             "kernel_ms_avg": round(avg_kernel_s * 1e3, 3),
+            "walk_layout": ("reference tree" if st.get("walk_layout") == rtx.RTX_LAYOUT_REFERENCE else
+                            f"rebuilt tree, camera octant {st.get('walk_layout')}"),
             "schedule": schedule(st),
             "roofline": roofline(st, my_rows * W, avg_kernel_s, profile_workload if world == 1 else "-",
-                                 args.traffic, args.valu),
+                                 args.traffic, args.valu, dev.device_bytes() <= 64 * 1024),
         }
+        if world > 1:  # rank 0's wall time in the gather (incl. waiting for the slowest rank)
+            out["gather_ms_avg"] = round(sum(gms) / len(gms), 3)
+            out["kernel_ms_per_rank"] = {"min": round(min(rank_kms), 3), "max": round(max(rank_kms), 3),
+                                         "all": [round(x, 3) for x in rank_kms]}
         if not args.no_hash:
             out["framebuffer_sha256_16"] = framebuffer_hash(img)  # bitwise-comparable across N
         if world == 1 and not args.no_cpu:

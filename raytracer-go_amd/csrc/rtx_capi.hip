@@ -754,7 +754,8 @@ int enqueue_on(rtx_scene* s, DeviceCopy* c, const rtx_camera* cam, uint64_t seed
     if (p.width > 0 && p.rows > 0) {
         // Sample scratch: up to RTX_SCRATCH_MB (default 16 GiB of the 288 GB HBM) of sample
         // colours, 12 B each; the samples run in chunks that fit.
-        const uint64_t per_sample = (uint64_t)p.width * p.rows * 12;
+        // tile-major: every 8x8 tile whole (render_items / reduce_samples), 12 B per pixel
+        const uint64_t per_sample = (uint64_t)((p.width + 7) / 8) * ((p.rows + 7) / 8) * 64 * 12;
         const uint64_t budget = (uint64_t)env_knob("RTX_SCRATCH_MB", 16384, 1, 1 << 20) << 20;
         uint64_t chunk = budget / per_sample;
         if (chunk > cam->samples_per_pixel) chunk = cam->samples_per_pixel;

@@ -218,7 +218,7 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
     const uint32_t n_tiles = tiles_x * ((p.rows + 7u) / 8u);
     const uint32_t nsub = (p.kn + p.sub - 1u) / p.sub;
     const uint64_t n_units = (uint64_t)n_tiles * nsub;
-    const size_t npix = (size_t)p.width * p.rows;
+    const size_t tile_floats = (size_t)n_tiles * 64 * 3;  // one sample of every tile (tile-major scratch)
 
     // the wave's unit (uniform, kept in SGPRs: every value below is derived from readfirstlane):
     // tile origin (u_x8, u_r8), first sample, items, next item
@@ -226,7 +226,7 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
     bool exhausted = false;
 
     uint32_t mode = M_CLAIM, seg = 0, items_done = 0;
-    size_t pix = 0;  // region-linear pixel of the lane's item
+    size_t pix = 0;  // the lane's item in the tile-major scratch: 64 * tile + pixel within the tile
     V3 base = v3(0.0f, 0.0f, 0.0f);
     V3 thr = v3(1.0f, 1.0f, 1.0f), acc = v3(0.0f, 0.0f, 0.0f);
     Ray r{v3(0, 0, 0), v3(0, 0, 0)};
@@ -239,7 +239,7 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
     uint64_t split[4] = {0, 0, 0, 0};  // COUNT: shading-phase cycles: scatter, shade, claims + camera rays, trav_begin
 
     auto store = [&](V3 col) {  // the item's colour, GetColor's result for sample k
-        float* o = p.scratch + ((size_t)(rng.sample - p.k0) * npix + pix) * 3;
+        float* o = p.scratch + (size_t)(rng.sample - p.k0) * tile_floats + pix * 3;
         o[0] = col.x;
         o[1] = col.y;
         o[2] = col.z;
@@ -326,7 +326,7 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
                     base = pixel_base(c, x, y);
                     rng.pixel = y * c.image_width + x;
                     rng.sample = u_k0 + (j >> 6);
-                    pix = (size_t)lr * p.width + lx;
+                    pix = (size_t)((u_r8 >> 3) * tiles_x + (u_x8 >> 3)) * 64 + l;
                     got = true;
                 }
             }
@@ -372,12 +372,19 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
 
 // GetPixelColor's sum over the stored colours of samples [k0, k0 + kn), in k order
 // (camera.go:256-259), continued from the running sum in `out` when k0 > 0; the last
-// chunk applies Scale(1/spp) (camera.go:261).  One thread per pixel, coalesced reads.
+// chunk applies Scale(1/spp) (camera.go:261).  The scratch is tile-major — sample k of tile t
+// is one 768-B block of its 64 pixels' colours, so a wave's colour stores fill whole lines
+// (pixel-major rows of 96 B wrote 1.26x the colour bytes to HBM as partial lines).  Thread i
+// sums pixel i % 64 of tile i / 64: consecutive threads read consecutive colours.
 __global__ __launch_bounds__(256) void reduce_samples(Params p, uint32_t last) {
-    const size_t npix = (size_t)p.width * p.rows;
+    const uint32_t tiles_x = (p.width + 7u) / 8u;
+    const size_t n_tiles = (size_t)tiles_x * ((p.rows + 7u) / 8u);
     const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= npix) return;
-    float* o = p.out + i * 3;
+    if (i >= n_tiles * 64) return;
+    const uint32_t t = (uint32_t)(i >> 6), l = (uint32_t)(i & 63u);
+    const uint32_t lx = (t % tiles_x) * 8u + (l & 7u), lr = (t / tiles_x) * 8u + (l >> 3);
+    if (lx >= p.width || lr >= p.rows) return;  // outside a ragged tile
+    float* o = p.out + ((size_t)lr * p.width + lx) * 3;
     float sx = 0.0f, sy = 0.0f, sz = 0.0f;
     if (p.k0 > 0) {
         sx = o[0];
@@ -385,7 +392,7 @@ __global__ __launch_bounds__(256) void reduce_samples(Params p, uint32_t last) {
         sz = o[2];
     }
     const float* src = p.scratch + i * 3;
-    for (uint32_t k = 0; k < p.kn; ++k, src += npix * 3) {
+    for (uint32_t k = 0; k < p.kn; ++k, src += n_tiles * 64 * 3) {
         sx = sx + src[0];
         sy = sy + src[1];
         sz = sz + src[2];
@@ -427,7 +434,7 @@ hipError_t launch_items(Params p, bool use_lds, hipStream_t stream) {
     if (per_cu < 1) per_cu = 1;
     const uint32_t spp = p.cam.samples_per_pixel, chunk = p.kn, sub = p.sub;
     const uint64_t tiles = (uint64_t)((p.width + 7) / 8) * ((p.rows + 7) / 8);
-    const uint64_t npix = (uint64_t)p.width * p.rows;
+    const uint64_t slots = tiles * 64;  // pixels of the tile-major scratch (ragged tiles padded)
     for (uint32_t k0 = 0; k0 < spp; k0 += chunk) {
         p.k0 = k0;
         p.kn = spp - k0 < chunk ? spp - k0 : chunk;
@@ -450,7 +457,7 @@ hipError_t launch_items(Params p, bool use_lds, hipStream_t stream) {
         e = hipMemsetAsync(p.tile_counter, 0, sizeof(uint32_t), stream);  // (the watchdog flag: once per render)
         if (e != hipSuccess) return e;
         hipLaunchKernelGGL(kern, dim3((uint32_t)blocks), dim3(block), shmem, stream, p);
-        hipLaunchKernelGGL(reduce_samples, dim3((uint32_t)((npix + 255) / 256)), dim3(256), 0, stream, p,
+        hipLaunchKernelGGL(reduce_samples, dim3((uint32_t)((slots + 255) / 256)), dim3(256), 0, stream, p,
                            (uint32_t)(k0 + p.kn >= spp));
         e = hipGetLastError();
         if (e != hipSuccess) return e;

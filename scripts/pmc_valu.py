@@ -10,6 +10,7 @@ the launch (GRBM_GUI_ACTIVE is summed over the 8 XCDs: / 8 = shader clocks; x 10
 import argparse
 import csv
 import glob
+import hashlib
 import json
 import os
 
@@ -19,6 +20,9 @@ ap.add_argument("out")
 ap.add_argument("--workload", required=True)
 ap.add_argument("--kernel", default="render_items<false")
 ap.add_argument("--simds", type=int, default=1024)
+ap.add_argument("--lib", default=os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                              "raytracer-go_amd", "librtx.so"),
+                help="the library the profiled run loaded: its hash ties the profile to the code (bench.py checks it)")
 args = ap.parse_args()
 
 vals = {}
@@ -38,6 +42,7 @@ out = {
     "shader_cycles_per_launch": cycles,
     "valu_issue_frac": round(insts * 2.0 / (cycles * args.simds), 4),
     "valu_lane_frac": round(vals["SQ_THREAD_CYCLES_VALU"][0] / (64.0 * insts), 4),
+    "librtx_sha256_16": hashlib.sha256(open(args.lib, "rb").read()).hexdigest()[:16],
     "method": "rocprofv3 --kernel-trace --pmc SQ_INSTS_VALU SQ_THREAD_CYCLES_VALU GRBM_GUI_ACTIVE ...; "
               "issue frac = 2 cycles x SQ_INSTS_VALU / (GRBM_GUI_ACTIVE / 8 XCDs x 1024 SIMDs)",
 }
