@@ -3,8 +3,10 @@
 //
 // A maintainer copies this file into the reference's package `internal` (next to
 // internal/camera.go; the Hittable/Material/Texture fields it flattens are unexported, so it
-// must live in that package) and points the cgo flags at a build of this repository
-// (`make -C raytracer-go_amd`).  It replaces nothing: Render (internal/camera.go:180) stays as
+// must live in that package) and points cgo at a build of this repository (`make -C
+// raytracer-go_amd`) through the environment, wherever it is checked out:
+//   CGO_CFLAGS="-I$RTX/include" CGO_LDFLAGS="-L$RTX/raytracer-go_amd -Wl,-rpath,$RTX/raytracer-go_amd" go build
+// ($RTX = this repository's root).  It replaces nothing: Render (internal/camera.go:180) stays as
 // the CPU path, and RenderGPU falls back to it for anything the GPU path does not carry.
 //
 // Go is not installed in the image this repository is built in, so this file has not been
@@ -13,8 +15,7 @@
 package internal
 
 /*
-#cgo CFLAGS: -I${SRCDIR}/../../raytracer-mi355x/include
-#cgo LDFLAGS: -L${SRCDIR}/../../raytracer-mi355x/raytracer-go_amd -lrtx -Wl,-rpath,${SRCDIR}/../../raytracer-mi355x/raytracer-go_amd
+#cgo LDFLAGS: -lrtx
 #include <stdlib.h>
 #include "rtx.h"
 */
@@ -198,9 +199,7 @@ func (t *gpuTables) ref(h Hittable) (C.int32_t, error) {
 		})
 		return primRef(C.RTX_PRIM_QUAD, len(t.quads)-1), nil
 	case *World: // a World nested in the tree (hittables.go:55-72 as a BVH child): a list ref
-		if len(v.hittables) == 0 {
-			return 0, errUnsupported
-		}
+		// (an empty one is a miss: a list of no items, ABI 6)
 		refs := make([]C.int32_t, len(v.hittables))
 		for i, h := range v.hittables {
 			r, err := t.ref(h)
@@ -220,6 +219,13 @@ func (t *gpuTables) ref(h Hittable) (C.int32_t, error) {
 
 func rtxErr(rc C.int) error {
 	return fmt.Errorf("rtx error %d: %s", int(rc), C.GoString(C.rtx_last_error()))
+}
+
+// gpuMissing: the library cannot run this render at all (no device, a feature it reports as
+// unsupported): RenderGPU then renders on the CPU.  (RCCL trouble is not among them: rtx_render
+// assembles the bands with per-band copies when RCCL is unavailable or fails, rtx.h.)
+func gpuMissing(rc C.int) bool {
+	return rc == C.RTX_ERR_UNSUPPORTED || rc == C.RTX_ERR_NO_DEVICE || rc == C.RTX_ERR_RCCL
 }
 
 // flatten: the tree Render receives as rtx.h tables; a plain *World gives one root per item
@@ -286,12 +292,17 @@ func (c *Camera) RenderGPU(world Hittable, writer io.Writer, seed uint64, gpus i
 	}
 	if len(t.lists) > 0 {
 		pin.Pin(&t.lists[0])
-		pin.Pin(&t.listRefs[0])
 		desc.lists, desc.n_lists = &t.lists[0], C.uint32_t(len(t.lists))
+	}
+	if len(t.listRefs) > 0 {
+		pin.Pin(&t.listRefs[0])
 		desc.list_refs, desc.n_list_refs = &t.listRefs[0], C.uint32_t(len(t.listRefs))
 	}
 	var scene *C.rtx_scene
 	if rc := C.rtx_scene_create(&desc, &scene); rc != 0 {
+		if gpuMissing(rc) {
+			return c.Render(world, writer)
+		}
 		return rtxErr(rc)
 	}
 	// Destroying the last scene on a device also frees the library's sample scratch there, so
@@ -312,6 +323,9 @@ func (c *Camera) RenderGPU(world Hittable, writer io.Writer, seed uint64, gpus i
 		var n C.uint64_t
 		if rc := C.rtx_render_ppm(scene, &cam, C.uint64_t(seed), (*C.char)(unsafe.Pointer(&text[0])),
 			C.uint64_t(len(text)), &n, nil); rc != 0 {
+			if gpuMissing(rc) {
+				return c.Render(world, writer)
+			}
 			return rtxErr(rc)
 		}
 		_, err := writer.Write(text[:int(n)])
@@ -319,6 +333,9 @@ func (c *Camera) RenderGPU(world Hittable, writer io.Writer, seed uint64, gpus i
 	}
 	rgb := make([]float32, w*h*3) // several GPUs: float32 image gathered to device 0, text here
 	if rc := C.rtx_render(scene, &cam, C.uint64_t(seed), C.int(gpus), (*C.float)(unsafe.Pointer(&rgb[0])), nil); rc != 0 {
+		if gpuMissing(rc) {
+			return c.Render(world, writer)
+		}
 		return rtxErr(rc)
 	}
 	var sb strings.Builder
