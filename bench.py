@@ -205,19 +205,20 @@ def load_profile(path: str, workload: str, lib: str):
     return d, None
 
 
-def served_from(st: dict, lds_scene: bool) -> str:
-    """Where the walk's entry reads come from."""
+def served_from(st: dict) -> str:
+    """Where the walk's entry reads come from (rtx_stats.scene_placement)."""
+    import rtx
+
     reads = st.get("node_visits", 0) + st.get("prim_tests", 0)
-    if lds_scene:
+    if st.get("scene_placement") == rtx.RTX_SCENE_IN_LDS:
         return "LDS (whole scene + material table copied per workgroup)"
-    if st.get("cache_hits") and reads:
+    if st.get("scene_placement") == rtx.RTX_SCENE_LDS_CACHE and reads:
         h = st["cache_hits"] / reads
         return f"LDS cache of the top levels {h:.1%} of entry reads, the other {1 - h:.1%} L2/MALL/HBM"
     return "L2/MALL/HBM (scene in HBM, no LDS cache)"
 
 
-def roofline(st: dict, pixels: int, kernel_s: float, workload: str, traffic_path: str, valu_path: str,
-             lds_scene: bool) -> dict:
+def roofline(st: dict, pixels: int, kernel_s: float, workload: str, traffic_path: str, valu_path: str) -> dict:
     """The render kernel's roof is VALU issue: its scene and materials are
     LDS-resident, HBM carries only the sample scratch.  achieved = the committed PMC pass's VALU
     wave-instructions per launch (same kernel, same workload, same librtx.so by hash) / this run's
@@ -237,7 +238,8 @@ def roofline(st: dict, pixels: int, kernel_s: float, workload: str, traffic_path
                    valu_insts_per_launch=vr["valu_insts_per_launch"], source=os.path.relpath(valu_path, ROOT))
     else:
         out["stale"] = vr_why
-    src = served_from(st, lds_scene)
+    src = served_from(st)
+    lds_scene = src.startswith("LDS (whole")
     out["alg_bytes"] = {
         "per_launch": launch_bytes,
         "achieved_gbs": round(launch_bytes / kernel_s / 1e9, 1),
@@ -392,7 +394,7 @@ def main():
                             f"rebuilt tree, camera octant {st.get('walk_layout')}"),
             "schedule": schedule(st),
             "roofline": roofline(st, my_rows * W, avg_kernel_s, profile_workload if world == 1 else "-",
-                                 args.traffic, args.valu, dev.device_bytes() <= 64 * 1024),
+                                 args.traffic, args.valu),
         }
         if world > 1:  # rank 0's wall time in the gather (incl. waiting for the slowest rank)
             out["gather_ms_avg"] = round(sum(gms) / len(gms), 3)

@@ -244,7 +244,11 @@ typedef struct rtx_stats {
     uint64_t walk_layout;   /* ABI 6: the layout walked: 0-7 = the camera octant of a rebuilt tree
                                (rtx_scene_topology), RTX_LAYOUT_REFERENCE = the caller's tree  */
     uint64_t gather_kind;   /* ABI 6, rtx_render: how the bands were assembled (RTX_GATHER_*)    */
+    uint64_t scene_placement; /* ABI 6: where the walk read the scene (RTX_SCENE_IN_LDS / ...)    */
 } rtx_stats;
+#define RTX_SCENE_IN_HBM 0u    /* entries from HBM (through L2)                                   */
+#define RTX_SCENE_IN_LDS 1u    /* the whole scene and its materials copied into LDS per workgroup */
+#define RTX_SCENE_LDS_CACHE 2u /* top levels cached in LDS, the rest from HBM                     */
 #define RTX_LAYOUT_REFERENCE 8u
 #define RTX_GATHER_NONE 0u   /* one band: it is the image                                        */
 #define RTX_GATHER_RCCL 1u   /* ncclGather of the padded bands to device 0, de-interleave kernel  */

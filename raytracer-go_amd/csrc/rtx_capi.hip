@@ -68,6 +68,7 @@ struct DeviceCopy {
     unsigned long long* counters = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     uint32_t n_textures = 0;  // device textures: those materials read (checkered, image, noise)
+    uint32_t placement = 0;   // the last enqueued render's rtxd::scene_placement
 };
 
 // Sample-colour scratch, one per device, shared by all scenes (grown on demand).  `last`
@@ -778,6 +779,7 @@ int enqueue_on(rtx_scene* s, DeviceCopy* c, const rtx_camera* cam, uint64_t seed
         p.debug_launch = env_knob("RTX_DEBUG_LAUNCH", 0, 0, 1);
         p.prim_batch = env_knob("RTX_PRIM_BATCH", 16, 1, 65);  // 65: primitive tests only when no node is left
     }
+    c->placement = rtxd::scene_placement(p, flags);
     // every stats slot, the unit queue head and the watchdog flag start at 0 for every render
     HIP_TRY(hipMemsetAsync(c->counters, 0, rtxd::COUNTER_SLOTS * sizeof(unsigned long long), stream));
     if (timed) HIP_TRY(hipEventRecord(c->ev0, stream));
@@ -816,6 +818,7 @@ int collect_on(DeviceCopy* c, bool count, uint64_t samples, uint32_t chunks, rtx
     for (int q = 0; q < 4; ++q) st->shade_split_cycles[q] = h[18 + q];
     st->sample_chunks = chunks;
     st->kernel_ms = ms;
+    st->scene_placement = c->placement;
     return RTX_OK;
 }
 
@@ -924,6 +927,7 @@ void add_stats(rtx_stats* acc, const rtx_stats& s) {
     acc->deferred_lanes += s.deferred_lanes;
     for (int q = 0; q < 4; ++q) acc->shade_split_cycles[q] += s.shade_split_cycles[q];
     acc->sample_chunks = std::max(acc->sample_chunks, s.sample_chunks);
+    acc->scene_placement = s.scene_placement;
 }
 
 }  // namespace

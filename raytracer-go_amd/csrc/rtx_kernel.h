@@ -9,4 +9,6 @@ struct Params;
 // the instantiation that accumulates the work counters into p.counters; RTX_FLAG_NO_LDS
 // reads the scene from global memory (A/B, identical output).
 hipError_t launch_render(const Params& p, uint32_t flags, hipStream_t stream);
+// Where a launch reads the scene (RTX_SCENE_IN_LDS / LDS_CACHE / IN_HBM, rtx.h).
+uint32_t scene_placement(const Params& p, uint32_t flags);
 }  // namespace rtxd

@@ -489,14 +489,20 @@ hipError_t launch_items_for(const Params& p, bool use_lds, hipStream_t stream) {
                      : launch_items<COUNT, false, false, RTX_V3_WAVES, COUNT ? 0 : RTX_V3_MINW>(p, use_lds, stream);
 }
 
+uint32_t scene_placement(const Params& p, uint32_t flags) {
+    // the whole scene in LDS (fixed layout) when its 'a' halves fit below LDS_B and all of it
+    // in 64 KB; else from HBM, with the top levels cached in LDS when stored first (n_hot)
+    if (!(flags & RTX_FLAG_NO_LDS) && (p.n_entries + 1) * 16 <= LDS_B &&
+        lds_fixed_bytes(p.n_entries, p.n_quads, p.n_materials, p.n_textures) <= LDS_MAX_BYTES)
+        return RTX_SCENE_IN_LDS;
+    return p.n_hot > 0 && !p.has_noise ? RTX_SCENE_LDS_CACHE : RTX_SCENE_IN_HBM;
+}
+
 hipError_t launch_render(const Params& p, uint32_t flags, hipStream_t stream) {
     if (p.width == 0 || p.rows == 0) return hipSuccess;
     if (!p.scratch) return hipErrorInvalidValue;  // the caller sizes the sample scratch
     const bool count = (flags & RTX_FLAG_COUNTERS) != 0;
-    // the whole scene in LDS (fixed layout) when its 'a' halves fit below LDS_B and all of it
-    // in 64 KB; else from HBM, with the top levels cached in LDS when stored first (n_hot)
-    const bool use_lds = !(flags & RTX_FLAG_NO_LDS) && (p.n_entries + 1) * 16 <= LDS_B &&
-                         lds_fixed_bytes(p.n_entries, p.n_quads, p.n_materials, p.n_textures) <= LDS_MAX_BYTES;
+    const bool use_lds = scene_placement(p, flags) == RTX_SCENE_IN_LDS;
     return count ? launch_items_for<true>(p, use_lds, stream) : launch_items_for<false>(p, use_lds, stream);
 }
 

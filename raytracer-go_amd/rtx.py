@@ -31,6 +31,7 @@ RTX_FLAG_NO_LDS = 4
 RTX_SCENE_REFERENCE_BVH = 1  # rtx_scene_create_ex: keep the caller's tree and the reference's visit order
 RTX_LAYOUT_REFERENCE = 8  # Stats.walk_layout of a scene walking the caller's tree
 RTX_GATHER_NONE, RTX_GATHER_RCCL, RTX_GATHER_DEVICE, RTX_GATHER_HOST = 0, 1, 2, 3  # Stats.gather_kind
+RTX_SCENE_IN_HBM, RTX_SCENE_IN_LDS, RTX_SCENE_LDS_CACHE = 0, 1, 2  # Stats.scene_placement
 RTX_IMAGE_TEXEL_WORDS = 2  # RGBA16 image texels: two uint32 words each (rtx.h)
 
 
@@ -103,7 +104,7 @@ class Stats(ctypes.Structure):
                 ("shade_lanes", c_uint64), ("trav_cycles", c_uint64), ("shade_cycles", c_uint64),
                 ("idle_lanes", c_uint64), ("cache_hits", c_uint64), ("sample_chunks", c_uint64),
                 ("parked_lanes", c_uint64), ("deferred_lanes", c_uint64), ("shade_split_cycles", c_uint64 * 4),
-                ("walk_layout", c_uint64), ("gather_kind", c_uint64)]
+                ("walk_layout", c_uint64), ("gather_kind", c_uint64), ("scene_placement", c_uint64)]
 
     def as_dict(self) -> dict:
         return {name: (list(v) if not isinstance(v := getattr(self, name), (int, float)) else v)
