@@ -258,6 +258,8 @@ typedef struct rtx_stats {
 
 #define RTX_FLAG_COUNTERS 1u /* count work units (separate kernel instantiation) */
 #define RTX_FLAG_NO_LDS 4u   /* A/B: read the scene from global memory even if it fits LDS */
+#define RTX_FLAG_TIMING (1u << 20) /* diagnostics: the timed kernel with the wave-cycle split of
+                                      rtx_stats (trav_cycles, shade_cycles, shade_split_cycles) */
 /* Bits 2u, 8u, 16u, 32u, 64u and RTX_FLAG_WAVE_GEOM (bits 24-26) selected the A/B schedules
  * v0/v1/v2 of ABI 3; they were removed in ABI 4 and are ignored. */
 /* Tuning: lanes of a wave that must wait before it shades (1..64; 0 = default, or the

@@ -170,8 +170,12 @@ __device__ __forceinline__ void split_clk(uint64_t& acc, uint64_t& clk) {
 // Samples beyond the scratch budget run in chunks [k0, k0 + kn); the running sum of a
 // pixel is carried in the output between chunks.
 // ------------------------------------------------------------------------------------
-template <bool COUNT, bool USE_LDS, bool QUADS, bool NOISE, int WAVES = 8, int MINW = 0, bool HYB = false>
+// CLK (RTX_FLAG_TIMING, diagnostics): the timed kernel (asm walk, no work counters) with the
+// counting kernel's s_memtime split of wave cycles into walk and shading phases.
+template <bool COUNT, bool USE_LDS, bool QUADS, bool NOISE, int WAVES = 8, int MINW = 0, bool HYB = false,
+          bool CLK = false>
 __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
+    constexpr bool TIME = COUNT || CLK;
     // walk steps between two wave votes (A/B with primitive batching: 4 +0.7 %, 8 +0.8 %, 12 +1.3 %)
     constexpr uint32_t WAVE_BLOCK = 64 * WAVES, STEPS = RTX_WALK_STEPS;
     extern __shared__ float4 lds_entries[];
@@ -256,13 +260,13 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
             if (lane == 0) atomicOr(p.error_flag, 1u);
             break;
         }
-        if (COUNT) clk = __builtin_amdgcn_s_memtime();
+        if (TIME) clk = __builtin_amdgcn_s_memtime();
         // primitive batching only for a scene in LDS: a lane that waits re-reads its entry, which
         // from HBM cost config 4 +34 %
         traverse_phase<COUNT, STEPS, QUADS, USE_LDS, HYB, USE_LDS>(mode, t, r, E, n_entries, thresh, cnt, wave_iters,
                                                               lane_steps, shade_phases, shade_lanes, idle_lanes,
                                                               parked, deferred, p.prim_batch);
-        if (COUNT) {
+        if (TIME) {
             const uint64_t now = __builtin_amdgcn_s_memtime();
             trav_cycles += now - clk;
             clk = now;
@@ -273,7 +277,7 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
         U4 b0{0u, 0u, 0u, 0u};
         if (mode == M_SHADE && t.hit >= 0) b0 = rng.block(seg + 1, 0u);
         const Scatter sc = coop_scatter<QUADS>(p, E, rng, seg + 1, mode == M_SHADE ? t.hit : -1, b0);
-        if (COUNT) split_clk(split[0], clk);
+        if (TIME) split_clk(split[0], clk);
         bool ready = false;
         if (mode == M_SHADE) {
             V3 color;
@@ -290,7 +294,7 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
                 ready = true;
             }
         }
-        if (COUNT) split_clk(split[1], clk);
+        if (TIME) split_clk(split[1], clk);
         // Lanes without an item take the next ones of the wave's unit; new camera rays
         // at one program point.  Loops only for max depth 0 and ragged tiles.
         for (;;) {
@@ -345,28 +349,30 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
                 }
             }
         }
-        if (COUNT) split_clk(split[2], clk);
+        if (TIME) split_clk(split[2], clk);
         if (ready) {  // begin a segment: world.Hit (ray.go:36)
             if (COUNT) ++cnt.segments;
             trav_begin(t, r, p.start);
             mode = n_entries > 0 ? M_TRAV : M_SHADE;
         }
-        if (COUNT) split_clk(split[3], clk);
+        if (TIME) split_clk(split[3], clk);
     }
     if (COUNT) {
         flush_counters(p, items_done, cnt);
         if (lane == 0) {
             flush_sched(p, wave_iters, lane_steps / STEPS, shade_phases, shade_lanes);
-            atomicAdd(&p.counters[12], (unsigned long long)trav_cycles);
             atomicAdd(&p.counters[14], (unsigned long long)idle_lanes);
-            for (int q = 0; q < 4; ++q) {
-                shade_cycles += split[q];
-                atomicAdd(&p.counters[18 + q], (unsigned long long)split[q]);
-            }
-            atomicAdd(&p.counters[13], (unsigned long long)shade_cycles);
             atomicAdd(&p.counters[16], (unsigned long long)(parked / STEPS));
             atomicAdd(&p.counters[17], (unsigned long long)(deferred / STEPS));
         }
+    }
+    if (TIME && lane == 0) {
+        atomicAdd(&p.counters[12], (unsigned long long)trav_cycles);
+        for (int q = 0; q < 4; ++q) {
+            shade_cycles += split[q];
+            atomicAdd(&p.counters[18 + q], (unsigned long long)split[q]);
+        }
+        atomicAdd(&p.counters[13], (unsigned long long)shade_cycles);
     }
 }
 
@@ -415,16 +421,16 @@ constexpr uint32_t LDS_MAX_BYTES = 64 * 1024;
 
 // v3: chunks of p.kn samples (the scratch holds one chunk), each rendered by a
 // resident-capacity grid of render_items and summed into p.out by reduce_samples.
-template <bool COUNT, bool QUADS, bool NOISE, int WAVES = 8, int MINW = 0>
+template <bool COUNT, bool QUADS, bool NOISE, int WAVES = 8, int MINW = 0, bool CLK = false>
 hipError_t launch_items(Params p, bool use_lds, hipStream_t stream) {
     // a scene too big for LDS: its top levels (p.n_hot entries) cached in LDS when the
     // device layout stored them first (RTX_HOT_ENTRIES=0 turns that off)
     const bool hyb = !use_lds && p.n_hot > 0 && !NOISE;
     const size_t shmem = use_lds ? lds_fixed_bytes(p.n_entries, p.n_quads, p.n_materials, p.n_textures)
                                  : (hyb ? lds_hot_bytes(p.n_hot) : 0);
-    const auto kern = use_lds ? render_items<COUNT, true, QUADS, NOISE, WAVES, MINW>
-                              : (hyb ? render_items<COUNT, false, QUADS, NOISE, WAVES, MINW, !NOISE>
-                                     : render_items<COUNT, false, QUADS, NOISE, WAVES, MINW>);
+    const auto kern = use_lds ? render_items<COUNT, true, QUADS, NOISE, WAVES, MINW, false, CLK>
+                              : (hyb ? render_items<COUNT, false, QUADS, NOISE, WAVES, MINW, !NOISE, CLK>
+                                     : render_items<COUNT, false, QUADS, NOISE, WAVES, MINW, false, CLK>);
     constexpr int block = 64 * WAVES;
     int dev = 0, cus = 0, per_cu = 0;
     hipError_t e = hipGetDevice(&dev);
@@ -503,6 +509,9 @@ hipError_t launch_render(const Params& p, uint32_t flags, hipStream_t stream) {
     if (!p.scratch) return hipErrorInvalidValue;  // the caller sizes the sample scratch
     const bool count = (flags & RTX_FLAG_COUNTERS) != 0;
     const bool use_lds = scene_placement(p, flags) == RTX_SCENE_IN_LDS;
+    if (!count && (flags & RTX_FLAG_TIMING) && !p.has_noise && p.item_waves != 4)  // diagnostics: sphere scenes
+        return p.n_quads ? launch_items<false, true, false, RTX_V3_WAVES, RTX_V3_MINW, true>(p, use_lds, stream)
+                         : launch_items<false, false, false, RTX_V3_WAVES, RTX_V3_MINW, true>(p, use_lds, stream);
     return count ? launch_items_for<true>(p, use_lds, stream) : launch_items_for<false>(p, use_lds, stream);
 }
 

@@ -28,6 +28,7 @@ RTX_MAT_LAMBERTIAN, RTX_MAT_METAL, RTX_MAT_DIELECTRIC, RTX_MAT_DIFFUSE_LIGHT = 0
 RTX_TEX_SOLID, RTX_TEX_CHECKERED, RTX_TEX_IMAGE, RTX_TEX_NOISE = 0, 1, 2, 3
 RTX_FLAG_COUNTERS = 1
 RTX_FLAG_NO_LDS = 4
+RTX_FLAG_TIMING = 1 << 20  # diagnostics: timed kernel + wave-cycle split
 RTX_SCENE_REFERENCE_BVH = 1  # rtx_scene_create_ex: keep the caller's tree and the reference's visit order
 RTX_LAYOUT_REFERENCE = 8  # Stats.walk_layout of a scene walking the caller's tree
 RTX_GATHER_NONE, RTX_GATHER_RCCL, RTX_GATHER_DEVICE, RTX_GATHER_HOST = 0, 1, 2, 3  # Stats.gather_kind
