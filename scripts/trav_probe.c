@@ -117,6 +117,8 @@ typedef struct { float mn[3], mx[3]; int32_t l, r; int32_t first, count; } snode
 static snode_t* SN; static int n_sn; static int32_t* SP; /* prims (refs) in leaf order */
 static int sah_leaf = 1;
 static int guard = 0;
+static int32_t* GUARD_OF; /* guard 3: sphere -> its reference leaf node */
+static float INFL = 0.02f;
 static float c_isect = 1.5f;
 
 static aabb_t prim_box(const rtx_scene_desc* s, int32_t ref) {
@@ -197,7 +199,11 @@ static void sah_walk(const rtx_scene_desc* s, int ni, const ray_t* r, float* clo
         for (int i = n->first; i < n->first + n->count; ++i) {
             int32_t pr[2] = {SP[i], SP[i]};
             int np = 1;
-            if (guard) { const rtx_bvh_node* b = &s->nodes[SP[i]]; pr[0] = b->left; pr[1] = b->right; np = b->left == b->right ? 1 : 2; }
+            if (guard == 3) {  /* the sphere's reference leaf box, then the sphere */
+                const rtx_bvh_node* gb = &s->nodes[GUARD_OF[(~SP[i]) & 0x0FFFFFFF]];
+                p->box++;
+                if (!aabb_hit(gb, r, 0.001f, *closest)) continue;
+            } else if (guard) { const rtx_bvh_node* b = &s->nodes[SP[i]]; pr[0] = b->left; pr[1] = b->right; np = b->left == b->right ? 1 : 2; }
             for (int q = 0; q < np; ++q) {
                 p->prim++;
                 float t;
@@ -255,6 +261,21 @@ static void sah_probe(const rtx_scene_desc* s, const ray_t* r, float t_ref) {
 /* guard: 1: the SAH units are the reference tree's leaves (nodes of 1-2 primitives), with their boxes */
 static void sah_setup(const rtx_scene_desc* s) {
     int n = (int)s->n_spheres;
+    if (guard == 3) {  /* single spheres, navigation boxes = own boxes inflated by INFL */
+        GUARD_OF = malloc(n * 4);
+        for (uint32_t i = 0; i < s->n_nodes; ++i) {
+            const rtx_bvh_node* b = &s->nodes[i];
+            if (b->left < 0) GUARD_OF[(~b->left) & 0x0FFFFFFF] = (int32_t)i;
+            if (b->right < 0) GUARD_OF[(~b->right) & 0x0FFFFFFF] = (int32_t)i;
+        }
+        SN = calloc(2 * n + 1, sizeof(snode_t)); SP = malloc(n * 4); PB = malloc(n * sizeof(aabb_t)); PC = malloc(12 * n);
+        for (int i = 0; i < n; ++i) {
+            SP[i] = RTX_REF_PRIM(RTX_PRIM_SPHERE, i); PB[i] = prim_box(s, SP[i]);
+            for (int k = 0; k < 3; ++k) { PB[i].mn[k] -= INFL; PB[i].mx[k] += INFL; PC[3*i+k] = s->spheres[i].center[k]; }
+        }
+        sah_build(s, 0, n);
+        return;
+    }
     if (guard) {
         int m = 0;
         SN = calloc(2 * n + 1, sizeof(snode_t)); SP = malloc(n * 4); PB = malloc(n * sizeof(aabb_t)); PC = malloc(12 * n);
@@ -280,8 +301,17 @@ static void sah_setup(const rtx_scene_desc* s) {
 static probe_t P_oct, P_dist;
 static uint64_t probe_ref_box, probe_ref_prim, segs;
 
+static uint64_t far_hist[8]; /* segments whose origin lies > 0/5/10/20/40/80/160/inf units outside the core box */
+static float CORE_MN[3] = {-11.2f, 0.0f, -11.2f}, CORE_MX[3] = {11.2f, 2.0f, 11.2f};
 static void probe_segment(const ctx_t* cx, const ray_t* r, int hit_any, const hit_t* h) {
     const rtx_scene_desc* s = cx->s;
+    {
+        float o[3] = {r->origin.x, r->origin.y, r->origin.z}, dm = 0;
+        for (int k = 0; k < 3; ++k) { float e = o[k] < CORE_MN[k] ? CORE_MN[k] - o[k] : (o[k] > CORE_MX[k] ? o[k] - CORE_MX[k] : 0); if (e > dm) dm = e; }
+        const float lim[7] = {0, 5, 10, 20, 40, 80, 160};
+        int b = 7; for (int q = 0; q < 7; ++q) if (dm <= lim[q]) { b = q; break; }
+        far_hist[b]++;
+    }
     float t_ref = hit_any ? h->t : INFINITY;
     for (int m = 0; m < 2; ++m) {
         probe_t* p = m ? &P_dist : &P_oct;
@@ -332,6 +362,7 @@ int main(int argc, char** argv) {
     const rtx_scene_desc* s = rtxhost_scene_desc(hs);
     rtx_camera cam;
     if (getenv("GUARD")) guard = atoi(getenv("GUARD"));
+    if (getenv("INFL")) INFL = atof(getenv("INFL"));
     if (getenv("LEAF")) sah_leaf = atoi(getenv("LEAF"));
     if (getenv("CI")) c_isect = atof(getenv("CI"));
     sah_setup(s);
@@ -358,6 +389,9 @@ int main(int argc, char** argv) {
            (double)P_oct.prim / segs, (unsigned long long)P_oct.mism_t);
     printf("  dist: box %.2f prim %.2f per segment, t mismatches %llu\n", (double)P_dist.box / segs,
            (double)P_dist.prim / segs, (unsigned long long)P_dist.mism_t);
+    printf("  origin outside the core box by <=0/5/10/20/40/80/160/more:");
+    for (int q = 0; q < 8; ++q) printf(" %.2e", (double)far_hist[q] / segs);
+    printf("\n");
     printf("  sah : box %.2f prim %.2f per segment, t mismatches %llu (%d nodes, leaf <= %d)\n", (double)P_sah.box / segs,
            (double)P_sah.prim / segs, (unsigned long long)P_sah.mism_t, n_sn, sah_leaf);
     printf("  saho: box %.2f prim %.2f per segment, t mismatches %llu\n", (double)P_saho.box / segs,
