@@ -352,10 +352,10 @@ def test_every_camera_octant(torch_cuda, spheres, dev_spheres, octant):
     below): each render walks its octant's layout of the rebuilt tree (uploaded on first use, beside the
     layouts of earlier renders), both kernels bit-identical to the oracle."""
     sx, sy, sz = (-1 if octant & 1 else 1), (-1 if octant & 2 else 1), (-1 if octant & 4 else 1)
-    frm = (-13.0 * sx, -2.5 * sy, -9.0 * sz)  # look from the opposite side, at the origin
+    # from above the ground (y = 2.5), across the spheres, tilted up or down
+    frm, at = (-13.0 * sx, 2.5, -9.0 * sz), (0.0, 2.5 + 2.0 * sy, 0.0)
     cam = ob.camera(np.float32(16.0) / np.float32(9.0), 96, samples_per_pixel=4, max_depth=50, look_from=frm,
-                    look_at=(0, 0, 0), fov_degrees=30, defocus_degrees=0.6, focus_dist=10,
-                    background=(0.7, 0.8, 1.0))
+                    look_at=at, fov_degrees=30, defocus_degrees=0.6, focus_dist=10, background=(0.7, 0.8, 1.0))
     assert rtx.camera_octant(cam) == octant
     reg = rtx.Region(0, 0, cam.image_width, cam.image_height, 0, 1)
     _, st, _ = check_scene(torch_cuda, dev_spheres, spheres.desc, cam, 3 + octant, reg)
