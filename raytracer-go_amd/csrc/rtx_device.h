@@ -944,6 +944,24 @@ __device__ __forceinline__ uint32_t trav_step_batched(Trav& t, const Ray& r, con
         "s_cbranch_scc1 LB%=_" #KN "\n\t"                                    \
         "s_mov_b64 exec, %[save]\n\t"                                        \
         "s_branch LE%=_" #K "\n"
+// Primitive runs (sphere scenes): the lanes of a primitive step whose successor is a primitive
+// again (a reference leaf's second sphere, or a World's next item) test it at once, in the same step,
+// under the step's exec narrowed to them — as box runs do for nodes (no header, no count test, no
+// exec restore between the two sphere tests).  Each lane still tests its entries in its own order with
+// its own bound.  RTX_PRIM_RUN=0 for A/B.
+#ifndef RTX_PRIM_RUN
+#define RTX_PRIM_RUN 1
+#endif
+#if RTX_PRIM_RUN
+#define RTX_PRIM_RUN_TAIL(K, WAIT)                                           \
+        "v_cmp_gt_u32_e64 %[pm], %[pe], %[pos]\n\t" /* (exec: this step's lanes) on a primitive again */\
+        "s_and_b64 exec, exec, %[pm]\n\t"                                    \
+        "s_cbranch_scc0 LR%=_" #K "\n\t"                                     \
+        WAIT /* its read, issued in the test */                              \
+        "s_branch LU%=_" #K "\n"
+#else
+#define RTX_PRIM_RUN_TAIL(K, WAIT) ""
+#endif
 #define RTX_WALK_STEP_PF(K, LOAD, WAIT, BEND)                                      \
         "v_cmp_gt_u32_e64 %[pm], %[pe], %[pos]\n\t" /* primitive: pos < prim_end */\
         "s_bcnt1_i32_b64 %[cnt], %[pm]\n\t"                                  \
@@ -982,7 +1000,8 @@ __device__ __forceinline__ uint32_t trav_step_batched(Trav& t, const Ray& r, con
         "LP%=_" #K ":\n\t"                                                   \
         WAIT                                                                 \
         "s_and_saveexec_b64 %[save], %[pm]\n\t"                              \
-        "s_cbranch_execz LR%=_" #K "\n\t"                                    \
+        "s_cbranch_execz LR%=_" #K "\n"                                       \
+        "LU%=_" #K ":\n\t" /* a primitive run continues here, exec = its lanes */\
         "v_sub_f32 v10, %[ox], v0\n\t" /* oc = o - center */                 \
         "v_sub_f32 v11, %[oy], v1\n\t"                                       \
         "v_sub_f32 v12, %[oz], v2\n\t"                                       \
@@ -1030,7 +1049,8 @@ __device__ __forceinline__ uint32_t trav_step_batched(Trav& t, const Ray& r, con
         "v_cmp_lt_f32_e64 %[l2], v16, %[cl]\n\t"                             \
         "s_and_b64 %[l1], %[l1], %[l2]\n\t" /* (disc < 0: NaN roots fail) */ \
         "v_cndmask_b32_e64 %[cl], %[cl], v16, %[l1]\n\t"                     \
-        "v_cndmask_b32_e64 %[hit], %[hit], v14, %[l1]\n"                     \
+        "v_cndmask_b32_e64 %[hit], %[hit], v14, %[l1]\n\t"                   \
+        RTX_PRIM_RUN_TAIL(K, WAIT)                                           \
         "LR%=_" #K ":\n\t"                                                   \
         "s_mov_b64 exec, %[save]\n"                                          \
         "LE%=_" #K ":\n\t"
@@ -1322,6 +1342,7 @@ __device__ __forceinline__ uint64_t walk_phase_asm(Trav& t, const Ray& r, uint32
 }
 #undef RTX_WALK_STEP_PF
 #undef RTX_WALK_STEP_PFQ
+#undef RTX_PRIM_RUN_TAIL
 #undef RTX_WALK_4
 #undef RTX_WALK_5
 #undef RTX_WALK_6
