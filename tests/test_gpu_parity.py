@@ -360,3 +360,21 @@ def test_every_camera_octant(torch_cuda, spheres, dev_spheres, octant):
     reg = rtx.Region(0, 0, cam.image_width, cam.image_height, 0, 1)
     _, st, _ = check_scene(torch_cuda, dev_spheres, spheres.desc, cam, 3 + octant, reg)
     assert st.walk_layout == octant
+
+
+@pytest.mark.parametrize("name,stride", [("C2", 36), ("C4", 36)])
+def test_config_rows_vs_oracle(torch_cuda, built, name, stride):
+    """Every `stride`-th row of the whole BASELINE frame (C2: 1920x1080x500 on the rebuilt tree; C4:
+    1920x1080x100 on the reference's), rendered by the timed kernel as part of the full frame, against
+    the oracle walking the CALLER's tree (iterative colour order): bit-identical."""
+    scene, width, spp, _ = CONFIGS[name]
+    s = rtx.HostScene(scene, 1)
+    dev = rtx.DeviceScene(s.desc)
+    cam = s.camera(width=width, spp=spp)
+    H = cam.image_height
+    gpu, _ = gpu_region(torch_cuda, dev, cam, 2024, rtx.Region(0, 0, width, H, 0, 1), counters=False)
+    rows = rtx.Region(0, 0, width, H, 7 % stride, stride)  # rows 7, 7 + stride, ...
+    it, _ = ob.render(s.desc, cam, 2024, rows, ob.ORDER_ITERATIVE)
+    want = gpu[rows.rank::stride]
+    bad = np.argwhere((want != it).any(axis=2))
+    assert len(bad) == 0, (len(bad), bad[:8].tolist(), float(np.abs(want - it).max()))
