@@ -13,6 +13,7 @@ reads (the scene copy into LDS is exactly that), so it is doubled.
 import argparse
 import csv
 import glob
+import hashlib
 import json
 import os
 import statistics
@@ -22,6 +23,9 @@ ap.add_argument("pmc_dir")
 ap.add_argument("out")
 ap.add_argument("--workload", required=True)
 ap.add_argument("--kernel", default="render_items<false")
+ap.add_argument("--lib", default=os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                              "raytracer-go_amd", "librtx.so"),
+                help="the library the profiled run loaded: its hash ties the profile to the code (bench.py checks it)")
 args = ap.parse_args()
 
 vals = {"FETCH_SIZE": [], "WRITE_SIZE": []}
@@ -40,6 +44,7 @@ out = {
     "fetch_bytes_per_launch": fetch,
     "write_bytes_per_launch": write,
     "hbm_bytes_per_launch": fetch + write,
+    "librtx_sha256_16": hashlib.sha256(open(args.lib, "rb").read()).hexdigest()[:16],
     "method": "rocprofv3 --kernel-trace --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes); "
               "KiB units; FETCH_SIZE x2 (gfx950 16-B/lane read correction)",
 }

@@ -26,3 +26,18 @@ def test_broken_source_fails_make(built, tmp_path, src):
     assert r.returncode != 0, r.stdout + r.stderr
     assert "deliberately broken" in r.stdout + r.stderr
     assert not stale.exists()
+
+
+def test_committed_profiles_name_one_build():
+    """bench.py derives roofline.frac / roofline.hbm only from PMC summaries measured on the
+    library it loads (by hash): the committed VALU and traffic summaries must name the same one."""
+    import json
+
+    hashes = set()
+    for name in ("valu_r03.json", "traffic_r03.json"):
+        with open(os.path.join(ROOT, "profiles", name)) as f:
+            d = json.load(f)
+        assert d.get("librtx_sha256_16"), name
+        assert d["workload"] == "random_spheres:1920x1080x500"
+        hashes.add(d["librtx_sha256_16"])
+    assert len(hashes) == 1, hashes
