@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define RTX_ABI_VERSION 6
+#define RTX_ABI_VERSION 7
 
 /* ---- status codes ------------------------------------------------------------ */
 enum {
@@ -297,6 +297,13 @@ int rtx_scene_create(const rtx_scene_desc* desc, rtx_scene** out);
  * environment variable RTX_BVH=reference and every scene with quads, nested Worlds or a
  * World root.  rtx_scene_create(d, out) = rtx_scene_create_ex(d, 0, out).              */
 #define RTX_SCENE_REFERENCE_BVH 1u
+/* ABI 7.  The collapsed walk: a walk leaves out the box tests of tree nodes
+ * whose children are all nodes where that saves tests on sample paths from the first camera
+ * rendered with each layout.  A child's box lies inside its parent's and the slab test is
+ * monotone in the box, so no primitive test, hit, path or image bit changes — only
+ * rtx_stats.node_visits.  RTX_SCENE_EVERY_BOX (or RTX_COLLAPSE=0 in the environment) keeps
+ * every box test, as bvh.go:220-249 makes them. */
+#define RTX_SCENE_EVERY_BOX 2u
 int rtx_scene_create_ex(const rtx_scene_desc* desc, uint32_t flags, rtx_scene** out);
 
 /* The tree a rebuilt scene walks for camera octant `octant` (rtx_camera_octant): *n_nodes
@@ -310,6 +317,19 @@ int rtx_scene_topology(const rtx_scene* scene, uint32_t octant, rtx_bvh_node* no
  * `octant` (*n_nodes = 0, *root = -1 when it would keep the caller's).  Host only.       */
 int rtx_walk_tree(const rtx_scene_desc* desc, uint32_t flags, uint32_t octant, rtx_bvh_node* nodes, uint32_t cap,
                   uint32_t* n_nodes, int32_t* root);
+
+/* ABI 7.  The box tests the walk for `cam` leaves out: skip[k] = 1 for the k-th node entry of
+ * the uncollapsed walk (the walked tree — rtx_scene_topology's, or the caller's — in visit
+ * order: a node, then its first child's subtree, then its second's).  *n = the number of node
+ * entries; skip is filled when cap >= *n.  The walk for a layout is planned on that layout's
+ * first render (or on this call); later cameras of the same layout reuse it.  For tests and
+ * tools (the oracle walks the same skips: parity of node_visits).                        */
+int rtx_scene_walk_skip(rtx_scene* scene, const rtx_camera* cam, uint8_t* skip, uint32_t cap, uint32_t* n);
+
+/* The same without a scene or a device: the skips rtx_scene_create_ex(desc, flags) plans for
+ * a first render with `cam`.  Host only.                                                   */
+int rtx_walk_skip(const rtx_scene_desc* desc, uint32_t flags, const rtx_camera* cam, uint8_t* skip, uint32_t cap,
+                  uint32_t* n);
 
 /* Octant of the camera's viewing direction (pixel00 + du W/2 + dv H/2 - center): bit k set
  * when it points to negative axis k. */

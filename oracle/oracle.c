@@ -441,10 +441,29 @@ static int aabb_hit(const rtx_bvh_node* n, const ray_t* r, float tmin, float tma
 
 static int hit_ref(const ctx_t* cx, int32_t ref, const ray_t* r, float tmin, float tmax, hit_t* out, int dup);
 
+/* Walk hooks (set between renders, read by every render thread): per-node box tests and
+ * passes, and the nodes whose box test a collapsed walk leaves out.  Leaving a node's test
+ * out changes no result: a child's box lies inside its parent's (NewAabbFromBoxes' min/max)
+ * and InBoundary is monotone in the box, so a child passes only where its parent passes. */
+static uint64_t* g_node_tested;
+static uint64_t* g_node_passed;
+static const uint8_t* g_node_skip;
+
+void oracle_node_hooks(uint64_t* tested, uint64_t* passed, const uint8_t* skip) {
+    g_node_tested = tested;
+    g_node_passed = passed;
+    g_node_skip = skip;
+}
+
 /* (*BVH).Hit, bvh.go:220-249. */
 static int bvh_hit(const ctx_t* cx, const rtx_bvh_node* n, const ray_t* r, float tmin, float tmax, hit_t* out) {
-    cx->c->node_visits++;
-    if (!aabb_hit(n, r, tmin, tmax)) return 0;                              /* :221 */
+    const size_t id = (size_t)(n - cx->s->nodes);
+    if (!g_node_skip || !g_node_skip[id]) {
+        cx->c->node_visits++;
+        if (g_node_tested) __atomic_fetch_add(&g_node_tested[id], 1, __ATOMIC_RELAXED);
+        if (!aabb_hit(n, r, tmin, tmax)) return 0;                          /* :221 */
+        if (g_node_passed) __atomic_fetch_add(&g_node_passed[id], 1, __ATOMIC_RELAXED);
+    }
     hit_t hl, hr;
     int hit_left = hit_ref(cx, n->left, r, tmin, tmax, &hl, 0);             /* :225 */
     float rmax = tmax;                                                      /* :227 */

@@ -80,6 +80,10 @@ void oracle_camera_init(float aspect_ratio, int32_t image_width, const oracle_ca
 /* Render a region (rtx.h semantics).  threads <= 0 -> 1.  out holds
  * rtx_region_rows(region) * region->width * 3 floats.  counters may be NULL.
  * Returns 0, or -1 on bad arguments / unsupported scene features.                */
+/* Walk hooks for probes and collapsed-walk parity (NULL = off): per-node box tests and passes
+ * (indexed like desc->nodes, counted atomically), and nodes whose box test is left out. */
+void oracle_node_hooks(uint64_t* tested, uint64_t* passed, const uint8_t* skip);
+
 int oracle_render(const rtx_scene_desc* scene, const rtx_camera* cam, uint64_t seed, const rtx_region* region,
                   int order, int threads, float* out, oracle_counters* counters);
 

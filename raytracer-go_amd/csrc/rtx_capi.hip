@@ -26,6 +26,7 @@
 #include "rtx_layout.h"
 #include "rtx_ppm.h"
 #include "rtx_bvh.h"
+#include "rtx_collapse.h"
 #include "rtx_topology.h"
 
 namespace {
@@ -274,11 +275,17 @@ void release_render_locked(int device) {  // g_render_mu held; device -1: all
 }  // namespace
 
 struct rtx_scene {
-    // The walk as threaded entries: layouts[0] for a scene that keeps the caller's topology (the
-    // reference's visit order, bvh.go:220-249); a rebuilt scene (topo) has one per camera octant,
-    // emitted on first use — all of the same size.
+    // The caller's tree as threaded entries in the reference's visit order (bvh.go:220-249).
+    std::vector<rtx_entry> base;
+    // The walk as threaded entries: layouts[0] for a scene that keeps the caller's topology; a
+    // rebuilt scene (topo) has one per camera octant.  Each is planned on first use, for the
+    // camera of that render: the tree's entries less the box tests the collapsed walk leaves
+    // out (rtx_collapse.h; skips[k]: per node entry of the uncollapsed walk, 1 = left out).
     std::vector<rtx_entry> layouts[8];
+    std::vector<uint8_t> skips[8];
+    bool planned[8] = {};
     bool rebuilt = false;
+    bool every_box = false;  // RTX_SCENE_EVERY_BOX: no box test left out
     rtxd::Topology topo;
     std::vector<float> quadtab;  // 16 floats per quad (rtx_layout.h)
     std::vector<rtx_material> materials;
@@ -449,22 +456,59 @@ int ensure_device(rtx_scene* s, int device, DeviceCopy** out) {
     return RTX_OK;
 }
 
-// The walk of camera octant `oct` as threaded entries (s->mu held): a rebuilt scene emits the
-// octant's orientation of its tree on first use; a scene keeping the caller's topology has one.
-int scene_layout(rtx_scene* s, uint32_t oct, const std::vector<rtx_entry>** out) {
-    if (!s->rebuilt) oct = 0;
-    std::vector<rtx_entry>& L = s->layouts[oct];
-    if (s->rebuilt && L.empty()) rtxd::emit_topology(s->topo, oct, L);
-    *out = &L;
+// Whether walks leave box tests out (rtx_collapse.h): RTX_COLLAPSE=0 in the environment (read
+// per plan) or the scene flag RTX_SCENE_EVERY_BOX keep every test.
+bool collapse_enabled(bool every_box) {
+    if (every_box) return false;
+    const char* e = std::getenv("RTX_COLLAPSE");
+    return !(e && std::strcmp(e, "0") == 0);
+}
+
+// The walk of one tree for one camera: `base` (the caller's tree) or `topo` oriented for octant
+// `oct`, less the box tests the collapsed walk leaves out for paths from `cam`.
+void plan_walk(const std::vector<rtx_entry>& base, const rtxd::Topology* topo, uint32_t oct,
+               const std::vector<float>& quadtab, const rtx_camera& cam, bool collapse, std::vector<rtx_entry>& out,
+               std::vector<uint8_t>& skip) {
+    std::vector<rtx_entry> full;
+    if (topo) rtxd::emit_topology(*topo, oct, full);
+    const std::vector<rtx_entry>& E = topo ? full : base;
+    if (collapse) {
+        std::vector<double> pass;
+        double walks = 0.0;
+        rtxd::sample_node_passes(E, quadtab, cam, pass, &walks);
+        rtxd::collapse_layout(E, pass, walks, out, skip);
+        return;
+    }
+    out = E;
+    skip.clear();
+    for (const rtx_entry& e : E) {
+        int32_t tag;
+        std::memcpy(&tag, &e.b[3], 4);
+        if (tag == RTX_E_NODE) skip.push_back(0);
+    }
+}
+
+// Layout slot of a camera: its octant for a rebuilt scene, else 0.
+uint32_t layout_slot(const rtx_scene* s, const rtx_camera* cam) { return s->rebuilt ? rtxd::camera_octant(*cam) : 0u; }
+
+// The walk for `cam` as threaded entries (s->mu held), planned on the slot's first use.
+int scene_layout(rtx_scene* s, const rtx_camera* cam, const std::vector<rtx_entry>** out) {
+    const uint32_t k = layout_slot(s, cam);
+    if (!s->planned[k]) {
+        plan_walk(s->base, s->rebuilt ? &s->topo : nullptr, k, s->quadtab, *cam, collapse_enabled(s->every_box),
+                  s->layouts[k], s->skips[k]);
+        s->planned[k] = true;
+    }
+    *out = &s->layouts[k];
     return RTX_OK;
 }
 
-// Upload the walk layout of octant `oct` to copy c (current device = c's; s->mu held).
-int ensure_layout(rtx_scene* s, DeviceCopy* c, uint32_t oct) {
-    if (!s->rebuilt) oct = 0;
+// Upload the walk layout for `cam` to copy c (current device = c's; s->mu held).
+int ensure_layout(rtx_scene* s, DeviceCopy* c, const rtx_camera* cam) {
+    const uint32_t oct = layout_slot(s, cam);
     if (c->lay[oct].entries) return RTX_OK;
     const std::vector<rtx_entry>* E = nullptr;
-    if (int rc = scene_layout(s, oct, &E)) return rc;
+    if (int rc = scene_layout(s, cam, &E)) return rc;
     DeviceLayout& lay = c->lay[oct];
     HIP_TRY(hipMalloc(&lay.entries, (E->size() + 1) * sizeof(rtx_entry) + s->quadtab.size() * sizeof(float)));
     {  // device layout: all 'a' halves, then all 'b' halves (rtxd::SceneRef), each ending
@@ -634,13 +678,27 @@ int topology_mode(uint32_t flags, const std::vector<rtx_entry>& ref) {
     return rtxd::precise_enough(ref) ? 1 : 0;
 }
 
-// A scene whose layouts[0] holds the reference's walk of one tree: take the walk's own tree when
-// it qualifies (spheres only; rtxd::build_topology) and re-emit layouts[0] for octant 0.
+// A scene whose base holds the reference's walk of one tree: take the walk's own tree when it
+// qualifies (spheres only; rtxd::build_topology).
 void adopt_topology(rtx_scene* s, uint32_t flags) {
-    const int mode = topology_mode(flags, s->layouts[0]);
-    if (mode == 0 || !rtxd::build_topology(s->layouts[0], mode == 1, s->topo)) return;
+    s->every_box = (flags & RTX_SCENE_EVERY_BOX) != 0;
+    const int mode = topology_mode(flags, s->base);
+    if (mode == 0 || !rtxd::build_topology(s->base, mode == 1, s->topo)) return;
     s->rebuilt = true;
-    rtxd::emit_topology(s->topo, 0, s->layouts[0]);
+}
+
+// The quad table of a scene description (rtx_layout.h): (Q, material), (u, 0), (v, 0), (w, 0).
+void quad_table(const rtx_scene_desc* d, std::vector<float>& tab) {
+    tab.assign((size_t)d->n_quads * 16, 0.0f);
+    for (uint32_t i = 0; i < d->n_quads; ++i) {
+        const rtx_quad& q = d->quads[i];
+        float* o = &tab[(size_t)i * 16];
+        std::memcpy(o, q.q, 12);
+        std::memcpy(o + 3, &q.material, 4);
+        std::memcpy(o + 4, q.u, 12);
+        std::memcpy(o + 8, q.v, 12);
+        std::memcpy(o + 12, q.w, 12);
+    }
 }
 
 uint64_t walk_layout(const rtx_scene* s, const rtx_camera* cam) {
@@ -740,8 +798,8 @@ rtxd::Params make_params(const rtx_scene* s, const DeviceCopy* c, uint32_t oct, 
 // *chunks receives the number of sample chunks (render kernel launches).
 int enqueue_on(rtx_scene* s, DeviceCopy* c, const rtx_camera* cam, uint64_t seed, const rtx_region* r, float* d_out,
                hipStream_t stream, uint32_t flags, bool timed, uint32_t* chunks) {
-    const uint32_t oct = s->rebuilt ? rtxd::camera_octant(*cam) : 0u;  // the walk's layout (rtx_topology.h)
-    if (int rc = ensure_layout(s, c, oct)) return rc;
+    const uint32_t oct = layout_slot(s, cam);  // the walk's layout (rtx_topology.h, rtx_collapse.h)
+    if (int rc = ensure_layout(s, c, cam)) return rc;
     rtxd::Params p = make_params(s, c, oct, cam, seed, r, d_out);
     const uint32_t th = (flags >> 8) & 0x7Fu;  // RTX_FLAG_SHADE_THRESH(n) override
     if (th) p.shade_thresh = th > 64 ? 64 : th;
@@ -864,16 +922,7 @@ int validate_tables(const rtx_scene_desc* d) {
 // Quad table, materials, textures and texels of a scene whose entries are built; then
 // the copy on the current device.  Takes ownership of s (deleted on failure).
 int finish_scene(rtx_scene* s, const rtx_scene_desc* d, rtx_scene** out) {
-    s->quadtab.resize((size_t)d->n_quads * 16);
-    for (uint32_t i = 0; i < d->n_quads; ++i) {  // (Q, material), (u, 0), (v, 0), (w, 0)
-        const rtx_quad& q = d->quads[i];
-        float* o = &s->quadtab[(size_t)i * 16];
-        std::memcpy(o, q.q, 12);
-        std::memcpy(o + 3, &q.material, 4);
-        std::memcpy(o + 4, q.u, 12);
-        std::memcpy(o + 8, q.v, 12);
-        std::memcpy(o + 12, q.w, 12);
-    }
+    quad_table(d, s->quadtab);
     s->materials.assign(d->materials, d->materials + d->n_materials);
     s->textures.assign(d->textures, d->textures + d->n_textures);
     for (const rtx_texture& t : s->textures) {
@@ -966,12 +1015,13 @@ int rtx_scene_create_ex(const rtx_scene_desc* d, uint32_t flags, rtx_scene** out
     if (int rc = check_acyclic(d)) return rc;
     rtx_scene* s = new rtx_scene();
     for (uint32_t i = 0; i < d->n_roots; ++i) {
-        if (int rc = emit(d, d->roots[i], s->layouts[0])) {
+        if (int rc = emit(d, d->roots[i], s->base)) {
             delete s;
             return rc;
         }
     }
     if (d->n_roots == 1) adopt_topology(s, flags);
+    else s->every_box = (flags & RTX_SCENE_EVERY_BOX) != 0;
     return finish_scene(s, d, out);
 }
 
@@ -998,7 +1048,7 @@ int rtx_scene_create_spheres(const rtx_sphere* spheres, uint32_t n_spheres, cons
     if (hipGetDevice(&cur) != hipSuccess) return fail(RTX_ERR_NO_DEVICE, "no HIP device");
     rtx_scene* s = new rtx_scene();
     double ms = 0;
-    hipError_t e = rtxd::build_sphere_bvh(spheres, n_spheres, bvh_seed, bvh_draw0, s->layouts[0], &ms);
+    hipError_t e = rtxd::build_sphere_bvh(spheres, n_spheres, bvh_seed, bvh_draw0, s->base, &ms);
     if (e != hipSuccess) {
         delete s;
         return fail(e == hipErrorOutOfMemory ? RTX_ERR_OOM : RTX_ERR_HIP, "GPU BVH build: %s", hipGetErrorString(e));
@@ -1010,8 +1060,8 @@ int rtx_scene_create_spheres(const rtx_sphere* spheres, uint32_t n_spheres, cons
 
 uint64_t rtx_scene_export(const rtx_scene* s, void* out, uint64_t cap) {
     if (!s) return 0;
-    const uint64_t bytes = s->layouts[0].size() * sizeof(rtx_entry);
-    if (out && cap >= bytes) std::memcpy(out, s->layouts[0].data(), bytes);
+    const uint64_t bytes = s->base.size() * sizeof(rtx_entry);
+    if (out && cap >= bytes) std::memcpy(out, s->base.data(), bytes);
     return bytes;
 }
 
@@ -1033,6 +1083,48 @@ int rtx_scene_topology(const rtx_scene* s, uint32_t octant, rtx_bvh_node* nodes,
 }
 
 uint32_t rtx_camera_octant(const rtx_camera* cam) { return cam ? rtxd::camera_octant(*cam) : 0u; }
+
+namespace {
+int copy_skip(const std::vector<uint8_t>& v, uint8_t* skip, uint32_t cap, uint32_t* n) {
+    *n = (uint32_t)v.size();
+    if (skip && cap >= v.size() && !v.empty()) std::memcpy(skip, v.data(), v.size());
+    return RTX_OK;
+}
+}  // namespace
+
+int rtx_scene_walk_skip(rtx_scene* s, const rtx_camera* cam, uint8_t* skip, uint32_t cap, uint32_t* n) {
+    g_last_error.clear();
+    if (!s || !n) return fail(RTX_ERR_INVALID_ARG, "bad argument");
+    if (int rc = check_camera(cam)) return rc;
+    std::lock_guard<std::mutex> lk(s->mu);
+    const std::vector<rtx_entry>* E = nullptr;
+    if (int rc = scene_layout(s, cam, &E)) return rc;
+    return copy_skip(s->skips[layout_slot(s, cam)], skip, cap, n);
+}
+
+int rtx_walk_skip(const rtx_scene_desc* d, uint32_t flags, const rtx_camera* cam, uint8_t* skip, uint32_t cap,
+                  uint32_t* n) {
+    g_last_error.clear();
+    if (!d || !n) return fail(RTX_ERR_INVALID_ARG, "bad argument");
+    if (int rc = check_camera(cam)) return rc;
+    if (d->n_roots == 0 || !d->roots) return fail(RTX_ERR_INVALID_ARG, "scene has no root");
+    if (d->n_nodes && !d->nodes) return fail(RTX_ERR_INVALID_ARG, "nodes is NULL");
+    if (int rc = validate_tables(d)) return rc;
+    if (int rc = check_acyclic(d)) return rc;
+    std::vector<rtx_entry> base;
+    for (uint32_t i = 0; i < d->n_roots; ++i)
+        if (int rc = emit(d, d->roots[i], base)) return rc;
+    rtxd::Topology t;
+    const bool rebuilt = d->n_roots == 1 && topology_mode(flags, base) != 0 &&
+                         rtxd::build_topology(base, topology_mode(flags, base) == 1, t);
+    std::vector<float> quadtab;
+    quad_table(d, quadtab);
+    std::vector<rtx_entry> walk;
+    std::vector<uint8_t> v;
+    plan_walk(base, rebuilt ? &t : nullptr, rtxd::camera_octant(*cam), quadtab, *cam,
+              collapse_enabled((flags & RTX_SCENE_EVERY_BOX) != 0), walk, v);
+    return copy_skip(v, skip, cap, n);
+}
 
 int rtx_walk_tree(const rtx_scene_desc* d, uint32_t flags, uint32_t octant, rtx_bvh_node* nodes, uint32_t cap,
                   uint32_t* n_nodes, int32_t* root) {
@@ -1071,7 +1163,7 @@ void rtx_scene_destroy(rtx_scene* s) {
 
 uint64_t rtx_scene_device_bytes(const rtx_scene* s) {
     if (!s) return 0;
-    return s->layouts[0].size() * sizeof(rtx_entry) + s->quadtab.size() * sizeof(float) +
+    return s->base.size() * sizeof(rtx_entry) + s->quadtab.size() * sizeof(float) +
            s->materials.size() * sizeof(rtx_material) +
            s->textures.size() * sizeof(rtx_texture) + s->texels.size() * sizeof(uint32_t);
 }

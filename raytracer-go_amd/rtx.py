@@ -30,6 +30,7 @@ RTX_FLAG_COUNTERS = 1
 RTX_FLAG_NO_LDS = 4
 RTX_FLAG_TIMING = 1 << 20  # diagnostics: timed kernel + wave-cycle split
 RTX_SCENE_REFERENCE_BVH = 1  # rtx_scene_create_ex: keep the caller's tree and the reference's visit order
+RTX_SCENE_EVERY_BOX = 2  # rtx_scene_create_ex: the walk leaves no box test out (ABI 7, rtx_collapse.h)
 RTX_LAYOUT_REFERENCE = 8  # Stats.walk_layout of a scene walking the caller's tree
 RTX_GATHER_NONE, RTX_GATHER_RCCL, RTX_GATHER_DEVICE, RTX_GATHER_HOST = 0, 1, 2, 3  # Stats.gather_kind
 RTX_SCENE_IN_HBM, RTX_SCENE_IN_LDS, RTX_SCENE_LDS_CACHE = 0, 1, 2  # Stats.scene_placement
@@ -117,7 +118,7 @@ RTX_SYMBOLS = [
     "rtx_scene_destroy", "rtx_scene_device_bytes", "rtx_render", "rtx_render_region_device", "rtx_region_rows",
     "rtx_ppm_max_bytes", "rtx_encode_ppm_device", "rtx_render_ppm", "rtx_scene_create_spheres", "rtx_scene_export",
     "rtx_release_device_memory", "rtx_device_scratch_bytes", "rtx_scene_create_ex", "rtx_scene_topology",
-    "rtx_camera_octant", "rtx_walk_tree", "rtx_render_ex",
+    "rtx_camera_octant", "rtx_walk_tree", "rtx_render_ex", "rtx_scene_walk_skip", "rtx_walk_skip",
 ]
 RTXHOST_SYMBOLS = [
     "rtxhost_build_scene", "rtxhost_scene_free", "rtxhost_scene_desc", "rtxhost_scene_camera",
@@ -163,6 +164,10 @@ def load() -> ctypes.CDLL:
     L.rtx_walk_tree.argtypes = [POINTER(SceneDesc), c_uint32, c_uint32, POINTER(BvhNode), c_uint32,
                                 POINTER(c_uint32), POINTER(c_int32)]
     L.rtx_walk_tree.restype = c_int
+    L.rtx_scene_walk_skip.argtypes = [c_void_p, POINTER(Camera), c_void_p, c_uint32, POINTER(c_uint32)]
+    L.rtx_scene_walk_skip.restype = c_int
+    L.rtx_walk_skip.argtypes = [POINTER(SceneDesc), c_uint32, POINTER(Camera), c_void_p, c_uint32, POINTER(c_uint32)]
+    L.rtx_walk_skip.restype = c_int
     L.rtx_camera_octant.argtypes = [POINTER(Camera)]
     L.rtx_camera_octant.restype = c_uint32
     L.rtx_scene_destroy.argtypes = [c_void_p]
@@ -295,15 +300,15 @@ class HostScene:
 class DeviceScene:
     """rtx_scene_create: the tables uploaded once to the current HIP device."""
 
-    def __init__(self, desc_ptr=None, handle=None, reference_bvh: bool = False):
+    def __init__(self, desc_ptr=None, handle=None, reference_bvh: bool = False, every_box: bool = False):
         L = load()
         self.build_ms = None
         if handle is not None:
             self._h = handle
             return
         h = c_void_p()
-        check(L.rtx_scene_create_ex(desc_ptr, RTX_SCENE_REFERENCE_BVH if reference_bvh else 0, ctypes.byref(h)),
-              "rtx_scene_create_ex")
+        flags = (RTX_SCENE_REFERENCE_BVH if reference_bvh else 0) | (RTX_SCENE_EVERY_BOX if every_box else 0)
+        check(L.rtx_scene_create_ex(desc_ptr, flags, ctypes.byref(h)), "rtx_scene_create_ex")
         self._h = h
 
     @classmethod
@@ -357,6 +362,12 @@ class DeviceScene:
             return desc_ptr
         arr, n, root = t
         return desc_with_tree(desc_ptr, arr, n, root)
+
+    def walk_skip(self, cam: Camera):
+        """rtx_scene_walk_skip: per node entry of the uncollapsed walk for cam (visit order), 1 where
+        the collapsed walk leaves its box test out (numpy uint8)."""
+        return _skip_mask(lambda buf, cap, n: load().rtx_scene_walk_skip(self._h, ctypes.byref(cam), buf, cap, n),
+                          "rtx_scene_walk_skip")
 
     def render_region(self, cam: Camera, seed: int, region: Region, out_ptr: int, stream: int = 0,
                       counters: bool = False, timed: bool = False, flags: int = 0):
@@ -463,6 +474,53 @@ def walk_tree_desc(desc_ptr, cam: Camera, flags: int = 0):
     arr = (BvhNode * max(n.value, 1))()
     check(L.rtx_walk_tree(desc_ptr, flags, oc, arr, n.value, ctypes.byref(n), ctypes.byref(root)), "rtx_walk_tree")
     return desc_with_tree(desc_ptr, arr, int(n.value), int(root.value))
+
+
+def _skip_mask(call, where):
+    import numpy as np
+    n = c_uint32()
+    check(call(None, 0, ctypes.byref(n)), where)
+    m = np.zeros(max(n.value, 1), np.uint8)
+    check(call(m.ctypes.data_as(c_void_p), n.value, ctypes.byref(n)), where)
+    return m[: n.value]
+
+
+def walk_skip(desc_ptr, cam: Camera, flags: int = 0):
+    """rtx_walk_skip (host only): the skips a scene made from desc_ptr plans for a first render with cam."""
+    return _skip_mask(lambda buf, cap, n: load().rtx_walk_skip(desc_ptr, flags, ctypes.byref(cam), buf, cap, n),
+                      "rtx_walk_skip")
+
+
+def node_skip(desc_ptr, skip):
+    """Map a skip mask over node entries in visit order (emit's pre-order: a node, its left subtree,
+    then its right, a one-element split's child once, a nested World's items in order) onto the
+    description's node table, for the oracle's walk hooks.  A node met twice must agree."""
+    import numpy as np
+    d = desc_ptr.contents
+    out = np.zeros(max(d.n_nodes, 1), np.uint8)
+    seen = np.zeros(max(d.n_nodes, 1), np.uint8)
+    k = 0
+    for r in range(d.n_roots):
+        stack = [d.roots[r]]
+        while stack:
+            ref = stack.pop()
+            if ref >= 0:
+                nd = d.nodes[ref]
+                v = skip[k]
+                k += 1
+                if seen[ref] and out[ref] != v:
+                    raise ValueError(f"node {ref} is walked twice with different skips")
+                seen[ref], out[ref] = 1, v
+                if nd.right != nd.left:
+                    stack.append(nd.right)
+                stack.append(nd.left)
+            elif ((~ref) & 0xFFFFFFFF) >> 28 == RTX_PRIM_LIST:
+                lst = d.lists[(~ref) & 0x0FFFFFFF]
+                for i in reversed(range(lst.count)):
+                    stack.append(d.list_refs[lst.first + i])
+    if k != len(skip):
+        raise ValueError(f"skip mask has {len(skip)} node entries, the walk {k}")
+    return out[: d.n_nodes]
 
 
 def camera_octant(cam: Camera) -> int:

@@ -13,7 +13,7 @@ FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-ma
 cd raytracer-go_amd
 $HIPCC $FLAGS -Xclang -target-feature -Xclang -packed-fp32-ops -c csrc/rtx_kernel.hip -o ../$B/rtx_kernel.o 2>&1 |
     grep -v "packed-fp32-ops' is not a recognized feature" || true
-for f in rtx_capi rtx_ppm rtx_bvh rtx_topology; do
+for f in rtx_capi rtx_ppm rtx_bvh rtx_topology rtx_collapse; do
     $HIPCC $FLAGS -c csrc/$f.hip -o ../$B/$f.o &
 done
 wait

@@ -87,6 +87,8 @@ def load():
     L.oracle_ycbcr_texels.argtypes = [c_void_p, c_void_p, c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
                                       ctypes.c_int64, c_int, c_void_p]
     L.oracle_ycbcr_texels.restype = c_int
+    L.oracle_node_hooks.argtypes = [c_void_p, c_void_p, c_void_p]
+    L.oracle_node_hooks.restype = None
     _lib = L
     return L
 
@@ -131,16 +133,25 @@ def region_rows(reg: rtx.Region) -> int:
 
 
 def render(desc_ptr, cam: rtx.Camera, seed: int, region: rtx.Region, order: int = ORDER_REFERENCE,
-           threads: int = 0):
-    """Oracle render of a region -> (float32 array [rows, width, 3], counters dict)."""
+           threads: int = 0, skip=None):
+    """Oracle render of a region -> (float32 array [rows, width, 3], counters dict).  skip: per node
+    of desc_ptr's table, 1 = leave its box test out (a collapsed walk, rtx.node_skip)."""
     L = load()
     if threads <= 0:
         threads = min(16, os.cpu_count() or 1)
     rows = region_rows(region)
     out = np.zeros((rows, region.width, 3), dtype=np.float32)
     cnt = Counters()
-    rc = L.oracle_render(desc_ptr, ctypes.byref(cam), seed, ctypes.byref(region), order, threads,
-                         out.ctypes.data_as(c_void_p), ctypes.byref(cnt))
+    sk = None if skip is None else np.ascontiguousarray(skip, np.uint8)
+    if sk is not None:
+        assert len(sk) >= desc_ptr.contents.n_nodes
+        L.oracle_node_hooks(None, None, sk.ctypes.data_as(c_void_p))
+    try:
+        rc = L.oracle_render(desc_ptr, ctypes.byref(cam), seed, ctypes.byref(region), order, threads,
+                             out.ctypes.data_as(c_void_p), ctypes.byref(cnt))
+    finally:
+        if sk is not None:
+            L.oracle_node_hooks(None, None, None)
     if rc != 0:
         raise RuntimeError("oracle_render rejected its arguments")
     return out, cnt.as_dict()

@@ -6,9 +6,11 @@ Every GPU check renders its region TWICE through the C-ABI (rtx_render_region_de
   - with the counting kernel (RTX_FLAG_COUNTERS: the C++ walk plus work counters),
 and holds both to the oracle (oracle/oracle.c):
   1. bit-identical to the oracle's iterative colour order walking the tree the scene walks
-     (rtx_scene_topology: the library's rebuilt tree, or the caller's), and the counting
-     kernel's counters equal to the oracle's on that tree — every box test, sphere test, hit,
-     texel fetch and RNG draw;
+     (rtx_scene_topology: the library's rebuilt tree, or the caller's) with the box tests the
+     scene's collapsed walk leaves out left out too (rtx_scene_walk_skip), and the counting
+     kernel's counters equal to the oracle's on that walk — every box test, sphere test, hit,
+     texel fetch and RNG draw; the oracle's full walk of the same tree gives the same image and
+     paths (leaving a box test out changes nothing else: rtx_collapse.h);
   2. when the scene walks a rebuilt tree: the oracle on the rebuilt tree bit-identical to the
      oracle on the caller's (the reference's) tree, with the same segments, hits, texel fetches
      and draws — the tree changes the work, not a single path;
@@ -42,13 +44,20 @@ def assert_counters_equal(st, cnt, keys=WORK_KEYS):
         assert getattr(st, k) == cnt[k], (k, getattr(st, k), cnt[k])
 
 
-def oracle_checks(desc, walk, cam, seed, reg):
-    """(iterative image on the walked tree, its counters, reference-order image on the caller's
-    tree); asserts check 2 when the walked tree is a rebuilt one."""
-    it, cnt = ob.render(walk, cam, seed, reg, ob.ORDER_ITERATIVE)
-    if walk is not desc:
+def walk_of(dev, desc, cam):
+    """(the tree the scene walks for cam, its per-node skips for the oracle's walk hooks)."""
+    walk = dev.walk_desc(desc, cam)
+    return walk, rtx.node_skip(walk, dev.walk_skip(cam))
+
+
+def oracle_checks(desc, walk, cam, seed, reg, skip=None):
+    """(iterative image on the walked tree with its skips, its counters, reference-order image on
+    the caller's tree); asserts check 2 and the collapsed walk's own check."""
+    it, cnt = ob.render(walk, cam, seed, reg, ob.ORDER_ITERATIVE, skip=skip)
+    if walk is not desc or (skip is not None and skip.any()):
         it0, cnt0 = ob.render(desc, cam, seed, reg, ob.ORDER_ITERATIVE)
-        assert np.array_equal(it, it0), f"rebuilt tree changes the image: max {np.abs(it - it0).max()}"
+        assert np.array_equal(it, it0), f"walked tree changes the image: max {np.abs(it - it0).max()}"
+        assert cnt["prim_tests"] == cnt0["prim_tests"] or walk is not desc
         for k in PATH_KEYS:
             assert cnt[k] == cnt0[k], (k, cnt[k], cnt0[k])
     ref, _ = ob.render(desc, cam, seed, reg, ob.ORDER_REFERENCE)
@@ -57,8 +66,8 @@ def oracle_checks(desc, walk, cam, seed, reg):
 
 def check_scene(torch, dev, desc, cam, seed, reg, flags=0, kernels=("timed", "counting")):
     """Checks 1-3 for both kernels on one region; returns (timed image, counting stats, oracle counters)."""
-    walk = dev.walk_desc(desc, cam)
-    it, cnt, ref = oracle_checks(desc, walk, cam, seed, reg)
+    walk, skip = walk_of(dev, desc, cam)
+    it, cnt, ref = oracle_checks(desc, walk, cam, seed, reg, skip)
     img = st = None
     for k in kernels:
         gpu, s = gpu_region(torch, dev, cam, seed, reg, counters=(k == "counting"), flags=flags)

@@ -218,10 +218,11 @@ def test_full_frame_bitwise(torch_cuda, built, scene, width, spp):
     check_scene(torch_cuda, dev, s.desc, cam, 23, reg)
 
 
-@pytest.mark.parametrize("hot", ["0", "1", "1280", "2048"])
+@pytest.mark.parametrize("hot", ["0", "64", "1280", "2048"])
 def test_stress_100k_lds_cache(torch_cuda, built, monkeypatch, hot):
     """Config 4 with its top BVH levels stored first and cached in LDS (RTX_HOT_ENTRIES, read at
-    upload): none, the root only, 8-wave and 12-wave workgroups.  The timed kernel's image is
+    upload): none, the first levels (the collapsed walk leaves the top nodes' own tests out, so the
+    first level holds their descendants), 8-wave and 12-wave workgroups.  The timed kernel's image is
     the oracle's bit for bit, and the counting kernel reports the cache hits."""
     monkeypatch.setenv("RTX_HOT_ENTRIES", hot)
     scene = rtx.HostScene("stress_100k", 1)

@@ -14,6 +14,7 @@ import numpy as np
 import pytest
 
 import oracle_binding as ob
+import parity
 import rtx
 from test_capi import create, lambertian, make_desc, sphere, texture
 
@@ -115,12 +116,13 @@ def test_nested_worlds_gpu_bitexact(built):
     cam = sc.camera(width=192, spp=6, depth=50)
     reg = rtx.Region(0, 0, cam.image_width, cam.image_height, 0, 1)
     out = torch.full((cam.image_height, cam.image_width, 3), float("nan"), device="cuda")
+    walk, skip = parity.walk_of(dev, sc.desc, cam)  # (the caller's tree; its collapsed walk's skips)
+    it, cnt = ob.render(walk, cam, 11, reg, ob.ORDER_ITERATIVE, skip=skip)
     for counters in (True, False):  # the counting kernel (C++ walk) and the timed one (asm walk)
         st = dev.render_region(cam, 11, reg, out.data_ptr(), torch.cuda.current_stream().cuda_stream,
                                counters=counters, timed=True)
         torch.cuda.synchronize()
         gpu = out.cpu().numpy()
-        it, cnt = ob.render(sc.desc, cam, 11, reg, ob.ORDER_ITERATIVE)
         assert np.array_equal(gpu, it), float(np.nanmax(np.abs(gpu - it)))
         if counters:
             assert (st.segments, st.node_visits, st.prim_tests, st.hits, st.rng_draws) == (

@@ -13,6 +13,7 @@ import numpy as np
 import pytest
 
 import oracle_binding as ob
+import parity
 import rtx
 
 pytestmark = pytest.mark.gpu
@@ -163,9 +164,9 @@ def test_random_scene_bitexact(built, seed, n_spheres, n_quads, axis_aligned):
     cam = camera(seed, 64, 36, 6, axis_aligned)
     pd = ctypes.pointer(d)
     dev = rtx.DeviceScene(pd)
-    walk = dev.walk_desc(pd, cam)  # the tree the scene walks (sphere-only trees may be rebuilt)
+    walk, skip = parity.walk_of(dev, pd, cam)  # the tree the scene walks (sphere-only trees may be rebuilt)
     reg = rtx.Region(0, 0, cam.image_width, cam.image_height, 0, 1)
-    it, cnt = ob.render(walk, cam, seed, reg, ob.ORDER_ITERATIVE)
+    it, cnt = ob.render(walk, cam, seed, reg, ob.ORDER_ITERATIVE, skip=skip)
     if walk is not pd:  # the rebuilt tree: same image and paths as the caller's tree on the oracle
         it0, cnt0 = ob.render(pd, cam, seed, reg, ob.ORDER_ITERATIVE)
         assert np.array_equal(it, it0, equal_nan=True)
