@@ -298,6 +298,7 @@ def main():
     cam = scene.camera(width=args.width, spp=args.spp, depth=args.depth)
     W, H, S = cam.image_width, cam.image_height, cam.samples_per_pixel
     dev = rtx.DeviceScene(scene.desc)  # one-time upload to this rank's HBM
+    skips = dev.walk_skip(cam)  # the walk's plan for this camera (rtx_collapse.h), made before timing
     reg = rtx.Region(0, 0, W, H, rank, world)
     R = max_shard_rows(H, world)
     shard = torch.zeros((R, W, 3), dtype=torch.float32, device="cuda")
@@ -391,7 +392,9 @@ def main():
             "node_visits_per_segment": round(tot["node_visits"] / tot["segments"], 3),
             "kernel_ms_avg": round(avg_kernel_s * 1e3, 3),
             "walk_layout": ("reference tree" if st.get("walk_layout") == rtx.RTX_LAYOUT_REFERENCE else
-                            f"rebuilt tree, camera octant {st.get('walk_layout')}"),
+                            f"rebuilt tree, camera octant {st.get('walk_layout')}")
+                           + (f", collapsed: {int(skips.sum())} of {len(skips)} node tests left out" if skips.any()
+                              else ", every box test"),
             "schedule": schedule(st),
             "roofline": roofline(st, my_rows * W, avg_kernel_s, profile_workload if world == 1 else "-",
                                  args.traffic, args.valu),
