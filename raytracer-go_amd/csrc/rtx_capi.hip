@@ -283,6 +283,7 @@ struct rtx_scene {
     // out (rtx_collapse.h; skips[k]: per node entry of the uncollapsed walk, 1 = left out).
     std::vector<rtx_entry> layouts[8];
     std::vector<uint8_t> skips[8];
+    std::vector<double> reads[8];  // estimated reads per entry of layouts[k] (the hot set of a big scene)
     bool planned[8] = {};
     bool rebuilt = false;
     bool every_box = false;  // RTX_SCENE_EVERY_BOX: no box test left out
@@ -468,24 +469,14 @@ bool collapse_enabled(bool every_box) {
 // `oct`, less the box tests the collapsed walk leaves out for paths from `cam`.
 void plan_walk(const std::vector<rtx_entry>& base, const rtxd::Topology* topo, uint32_t oct,
                const std::vector<float>& quadtab, const rtx_camera& cam, bool collapse, std::vector<rtx_entry>& out,
-               std::vector<uint8_t>& skip) {
+               std::vector<uint8_t>& skip, std::vector<double>* reads) {
     std::vector<rtx_entry> full;
     if (topo) rtxd::emit_topology(*topo, oct, full);
     const std::vector<rtx_entry>& E = topo ? full : base;
-    if (collapse) {
-        std::vector<double> pass;
-        double walks = 0.0;
-        rtxd::sample_node_passes(E, quadtab, cam, pass, &walks);
-        rtxd::collapse_layout(E, pass, walks, out, skip);
-        return;
-    }
-    out = E;
-    skip.clear();
-    for (const rtx_entry& e : E) {
-        int32_t tag;
-        std::memcpy(&tag, &e.b[3], 4);
-        if (tag == RTX_E_NODE) skip.push_back(0);
-    }
+    std::vector<double> pass;
+    double walks = 0.0;
+    rtxd::sample_node_passes(E, quadtab, cam, pass, &walks);
+    rtxd::collapse_layout(E, pass, walks, collapse, out, skip, reads);
 }
 
 // Layout slot of a camera: its octant for a rebuilt scene, else 0.
@@ -496,7 +487,7 @@ int scene_layout(rtx_scene* s, const rtx_camera* cam, const std::vector<rtx_entr
     const uint32_t k = layout_slot(s, cam);
     if (!s->planned[k]) {
         plan_walk(s->base, s->rebuilt ? &s->topo : nullptr, k, s->quadtab, *cam, collapse_enabled(s->every_box),
-                  s->layouts[k], s->skips[k]);
+                  s->layouts[k], s->skips[k], &s->reads[k]);
         s->planned[k] = true;
     }
     *out = &s->layouts[k];
@@ -535,13 +526,29 @@ int ensure_layout(rtx_scene* s, DeviceCopy* c, const rtx_camera* cam) {
                 }
             }
             const uint32_t cap = env_knob("RTX_HOT_ENTRIES", rtxd::HOT_ENTRIES_MAX, 0, rtxd::HOT_ENTRIES_MAX);
-            uint32_t levels = 0, hot = 0;
-            while (levels < per_depth.size() && hot + per_depth[levels] <= cap) hot += per_depth[levels++];
+            const std::vector<double>& R = s->reads[oct];
+            std::vector<uint8_t> in_hot(n, 0);
+            uint32_t hot = 0;
+            if (R.size() == n && env_knob("RTX_HOT_BY_READS", 1, 0, 1)) {
+                // the entries the walk reads most (the plan's sample estimate), in walk order
+                std::vector<uint32_t> idx(n);
+                for (size_t i = 0; i < n; ++i) idx[i] = (uint32_t)i;
+                const size_t take = std::min<size_t>(cap, n);
+                std::partial_sort(idx.begin(), idx.begin() + take, idx.end(), [&](uint32_t a, uint32_t b) {
+                    return R[a] != R[b] ? R[a] > R[b] : depth[a] != depth[b] ? depth[a] < depth[b] : a < b;
+                });
+                for (size_t q = 0; q < take; ++q) in_hot[idx[q]] = 1;
+                hot = (uint32_t)take;
+            } else {  // the top levels
+                uint32_t levels = 0;
+                while (levels < per_depth.size() && hot + per_depth[levels] <= cap) hot += per_depth[levels++];
+                for (size_t i = 0; i < n; ++i) in_hot[i] = depth[i] < levels;
+            }
             uint32_t k = 0;
             for (size_t i = 0; i < n; ++i)
-                if (depth[i] < levels) pos[i] = k++;
+                if (in_hot[i]) pos[i] = k++;
             for (size_t i = 0; i < n; ++i)
-                if (depth[i] >= levels) pos[i] = k++;
+                if (!in_hot[i]) pos[i] = k++;
             lay.hot = hot;
         } else {
             uint32_t k = 0;
@@ -1122,7 +1129,7 @@ int rtx_walk_skip(const rtx_scene_desc* d, uint32_t flags, const rtx_camera* cam
     std::vector<rtx_entry> walk;
     std::vector<uint8_t> v;
     plan_walk(base, rebuilt ? &t : nullptr, rtxd::camera_octant(*cam), quadtab, *cam,
-              collapse_enabled((flags & RTX_SCENE_EVERY_BOX) != 0), walk, v);
+              collapse_enabled((flags & RTX_SCENE_EVERY_BOX) != 0), walk, v, nullptr);
     return copy_skip(v, skip, cap, n);
 }
 

@@ -35,9 +35,11 @@ void sample_node_passes(const std::vector<rtx_entry>& E, const std::vector<float
                         std::vector<double>& pass, double* walks);
 
 // The collapsed layout of E for pass estimates `pass` / `walks`: out = E without the node entries
-// the optimum leaves out, escapes renumbered.  skip[k] = 1 when the k-th node entry of E (in E's
-// order) is left out.  Returns false (out = E, no skips) when the tree is too deep to plan.
-bool collapse_layout(const std::vector<rtx_entry>& E, const std::vector<double>& pass, double walks,
-                     std::vector<rtx_entry>& out, std::vector<uint8_t>& skip);
+// the optimum leaves out (none unless allow_drop), escapes renumbered.  skip[k] = 1 when the k-th
+// node entry of E (in E's order) is left out; reads (optional) = each out entry's estimated reads
+// (the passes of its nearest kept ancestor).  Returns false (out = E, no skips, no reads) when the
+// tree is too deep to plan.
+bool collapse_layout(const std::vector<rtx_entry>& E, const std::vector<double>& pass, double walks, bool allow_drop,
+                     std::vector<rtx_entry>& out, std::vector<uint8_t>& skip, std::vector<double>* reads);
 
 }  // namespace rtxd

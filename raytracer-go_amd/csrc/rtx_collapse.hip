@@ -164,8 +164,8 @@ void sample_node_passes(const std::vector<rtx_entry>& E, const std::vector<float
             }
 }
 
-bool collapse_layout(const std::vector<rtx_entry>& E, const std::vector<double>& pass, double walks,
-                     std::vector<rtx_entry>& out, std::vector<uint8_t>& skip) {
+bool collapse_layout(const std::vector<rtx_entry>& E, const std::vector<double>& pass, double walks, bool allow_drop,
+                     std::vector<rtx_entry>& out, std::vector<uint8_t>& skip, std::vector<double>* reads) {
     const size_t n = E.size();
     std::vector<int32_t> parent(n, -1);
     std::vector<uint32_t> depth(n, 0), kids(n, 0);
@@ -194,6 +194,7 @@ bool collapse_layout(const std::vector<rtx_entry>& E, const std::vector<double>&
         }
     }
     skip.assign(n_nodes, 0);
+    if (reads) reads->clear();
     if (cells > (64ull << 20) || pass.size() != n) {
         out = E;
         return false;
@@ -210,7 +211,7 @@ bool collapse_layout(const std::vector<rtx_entry>& E, const std::vector<double>&
         const uint32_t d = depth[ii];
         counts.assign(d + 1, walks);
         for (int32_t y = parent[ii]; y >= 0; y = parent[y]) counts[depth[y] + 1] = pass[y];
-        const bool collapsible = kids[ii] > 0 && !prim_child[ii] && !sticks_out[ii];
+        const bool collapsible = allow_drop && kids[ii] > 0 && !prim_child[ii] && !sticks_out[ii];
         std::vector<double>& drop = acc_drop[ii];
         if (drop.size() < d + 1) drop.resize(d + 1, 0.0);
         cost.assign(d + 1, 0.0);
@@ -255,8 +256,15 @@ bool collapse_layout(const std::vector<rtx_entry>& E, const std::vector<double>&
     map[n] = m;
     out.clear();
     out.reserve(m);
+    if (reads) reads->reserve(m);
     for (size_t i = 0; i < n; ++i) {
         if (drop_entry[i]) continue;
+        if (reads) {  // estimated reads of the entry: the passes of its nearest kept ancestor
+            const uint32_t j = parent[i] >= 0 ? jn[parent[i]] : 0u;
+            int32_t y = parent[i];
+            while (y >= 0 && depth[y] + 1 > j) y = parent[y];
+            reads->push_back(j == 0 || y < 0 ? walks : pass[y]);
+        }
         rtx_entry e = E[i];
         if (is_node[i]) {
             const int32_t esc = escape_of(e);
