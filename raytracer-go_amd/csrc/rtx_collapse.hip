@@ -1,7 +1,9 @@
 // rtx_collapse.hip — the collapsed walk (host code; see rtx_collapse.h).
 #include "rtx_collapse.h"
 
+#include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 
 namespace rtxd {
@@ -128,9 +130,10 @@ void sample_node_passes(const std::vector<rtx_entry>& E, const std::vector<float
     if (E.empty() || cam.image_width == 0 || cam.image_height == 0) return;
     // 64 columns of the image, rows in proportion; two paths per point, up to 4 segments each
     // (randSpheres averages 2.9 segments per sample)
-    const uint32_t gx = 64;
-    uint32_t gy = (uint32_t)std::lround(64.0 * cam.image_height / cam.image_width);
-    gy = gy < 1 ? 1 : (gy > 64 ? 64 : gy);
+    const char* env = std::getenv("RTX_PLAN_GRID");  // (A/B of the sample size)
+    const uint32_t gx = env ? (uint32_t)std::max(1l, std::min(1024l, std::strtol(env, nullptr, 10))) : 64u;
+    uint32_t gy = (uint32_t)std::lround((double)gx * cam.image_height / cam.image_width);
+    gy = gy < 1 ? 1 : (gy > gx ? gx : gy);
     uint64_t rng = 0x9E3779B97F4A7C15ull;
     for (uint32_t yi = 0; yi < gy; ++yi)
         for (uint32_t xi = 0; xi < gx; ++xi)

@@ -27,6 +27,9 @@
 #ifndef RTX_SUB_MAX  // samples per unit of a render with >= 128 units of 8 samples per resident wave
 #define RTX_SUB_MAX 16
 #endif
+#ifndef RTX_HYB_BATCH  // 1: primitive batching also for a scene in HBM with an LDS cache (A/B)
+#define RTX_HYB_BATCH 0
+#endif
 #ifndef RTX_ASM_STEP  // 1: the timed kernel's walk step in assembly (trav_step_asm); 0 for A/B
 #define RTX_ASM_STEP 1
 #endif
@@ -263,7 +266,8 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
         if (TIME) clk = __builtin_amdgcn_s_memtime();
         // primitive batching only for a scene in LDS: a lane that waits re-reads its entry, which
         // from HBM cost config 4 +34 %
-        traverse_phase<COUNT, STEPS, QUADS, USE_LDS, HYB, USE_LDS>(mode, t, r, E, n_entries, thresh, cnt, wave_iters,
+        traverse_phase<COUNT, STEPS, QUADS, USE_LDS, HYB, USE_LDS || (RTX_HYB_BATCH && HYB)>(
+            mode, t, r, E, n_entries, thresh, cnt, wave_iters,
                                                               lane_steps, shade_phases, shade_lanes, idle_lanes,
                                                               parked, deferred, p.prim_batch);
         if (TIME) {
