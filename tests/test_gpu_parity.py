@@ -347,6 +347,29 @@ def test_rebuilt_tree_full_frame(torch_cuda, built, scene, width, spp, allowed):
     assert float(np.abs(a - b).max()) <= 1e-6
 
 
+@pytest.mark.parametrize("scene,width,spp,reference_bvh", [
+    ("random_spheres", 1920, 16, False), ("random_spheres", 1920, 8, True), ("stress_100k", 1920, 4, False),
+    ("cornell_box", 600, 24, False), ("earth_dielectric", 3840, 2, False)])
+def test_collapsed_walk_full_frame(torch_cuda, built, scene, width, spp, reference_bvh):
+    """The collapsed walk (rtx_collapse.h) against every box test (RTX_SCENE_EVERY_BOX) on whole
+    frames, both kernels: the same image bit for bit and the same segments, sphere tests, hits, texel
+    fetches and draws; only the box tests fall."""
+    s = rtx.HostScene(scene, 1)
+    cam = s.camera(width=width, spp=spp)
+    reg = rtx.Region(0, 0, cam.image_width, cam.image_height, 0, 1)
+    col = rtx.DeviceScene(s.desc, reference_bvh=reference_bvh)
+    full = rtx.DeviceScene(s.desc, reference_bvh=reference_bvh, every_box=True)
+    assert col.walk_skip(cam).any() and not full.walk_skip(cam).any()
+    for counters in (False, True):
+        a, sa = gpu_region(torch_cuda, col, cam, 99, reg, counters=counters)
+        b, sb = gpu_region(torch_cuda, full, cam, 99, reg, counters=counters)
+        assert np.array_equal(a, b), (counters, int((a != b).any(axis=2).sum()))
+        if counters:
+            for k in ("samples", "segments", "prim_tests", "hits", "texel_fetches", "rng_draws"):
+                assert getattr(sa, k) == getattr(sb, k), k
+            assert sa.node_visits < 0.9 * sb.node_visits
+
+
 @pytest.mark.parametrize("octant", range(8))
 def test_every_camera_octant(torch_cuda, spheres, dev_spheres, octant):
     """Cameras looking along each of the 8 direction octants (randSpheres seen from every side and from
