@@ -257,6 +257,25 @@ def roofline(st: dict, pixels: int, kernel_s: float, workload: str, traffic_path
     return out
 
 
+def walk_desc(st, skips, near_skips) -> str:
+    """The walked layout(s) of a render, from its stats and the plans' skip masks."""
+    import rtx
+
+    lay = st.get("walk_layout", 0)
+    tiered = bool(lay & rtx.RTX_LAYOUT_TIERED)
+    lay &= ~rtx.RTX_LAYOUT_TIERED
+
+    def col(m):
+        return f"collapsed: {int(m.sum())} of {len(m)} node tests left out" if m.any() else "every box test"
+
+    if lay == rtx.RTX_LAYOUT_REFERENCE:
+        return "reference tree, " + col(skips)
+    if tiered:
+        return (f"tiered: near tree ({col(near_skips)}), guarded tree for {st.get('deferred_paths', 0)} deferred "
+                f"paths ({col(skips)}), camera octant {lay}")
+    return f"rebuilt tree, camera octant {lay}, " + col(skips)
+
+
 def framebuffer_hash(img) -> str:
     import numpy as np
 
@@ -299,6 +318,7 @@ def main():
     W, H, S = cam.image_width, cam.image_height, cam.samples_per_pixel
     dev = rtx.DeviceScene(scene.desc)  # one-time upload to this rank's HBM
     skips = dev.walk_skip(cam)  # the walk's plan for this camera (rtx_collapse.h), made before timing
+    near_skips = dev.near_skip(cam) if dev.near_region(cam)[1] else None  # the tiered walk's near tree (§14)
     reg = rtx.Region(0, 0, W, H, rank, world)
     R = max_shard_rows(H, world)
     shard = torch.zeros((R, W, 3), dtype=torch.float32, device="cuda")
@@ -391,10 +411,8 @@ def main():
             "segments_per_sample": round(tot["segments"] / tot["samples"], 4),
             "node_visits_per_segment": round(tot["node_visits"] / tot["segments"], 3),
             "kernel_ms_avg": round(avg_kernel_s * 1e3, 3),
-            "walk_layout": ("reference tree" if st.get("walk_layout") == rtx.RTX_LAYOUT_REFERENCE else
-                            f"rebuilt tree, camera octant {st.get('walk_layout')}")
-                           + (f", collapsed: {int(skips.sum())} of {len(skips)} node tests left out" if skips.any()
-                              else ", every box test"),
+            "walk_layout": walk_desc(st, skips, near_skips),
+            "prim_tests_per_segment": round(tot["prim_tests"] / tot["segments"], 3),
             "schedule": schedule(st),
             "roofline": roofline(st, my_rows * W, avg_kernel_s, profile_workload if world == 1 else "-",
                                  args.traffic, args.valu),

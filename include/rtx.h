@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define RTX_ABI_VERSION 7
+#define RTX_ABI_VERSION 8
 
 /* ---- status codes ------------------------------------------------------------ */
 enum {
@@ -245,11 +245,15 @@ typedef struct rtx_stats {
                                (rtx_scene_topology), RTX_LAYOUT_REFERENCE = the caller's tree  */
     uint64_t gather_kind;   /* ABI 6, rtx_render: how the bands were assembled (RTX_GATHER_*)    */
     uint64_t scene_placement; /* ABI 6: where the walk read the scene (RTX_SCENE_IN_LDS / ...)    */
+    uint64_t deferred_paths;  /* ABI 8, tiered walk: paths the near pass handed to the far pass  */
+    uint64_t redo_chunks;     /* ABI 8, tiered walk: sample chunks rendered again whole by the far
+                                 walk because the queue of deferred paths overflowed             */
 } rtx_stats;
 #define RTX_SCENE_IN_HBM 0u    /* entries from HBM (through L2)                                   */
 #define RTX_SCENE_IN_LDS 1u    /* the whole scene and its materials copied into LDS per workgroup */
 #define RTX_SCENE_LDS_CACHE 2u /* top levels cached in LDS, the rest from HBM                     */
 #define RTX_LAYOUT_REFERENCE 8u
+#define RTX_LAYOUT_TIERED 16u  /* ABI 8: walk_layout bit: the render walked in two tiers (RTX_SCENE_NO_TIER) */
 #define RTX_GATHER_NONE 0u   /* one band: it is the image                                        */
 #define RTX_GATHER_RCCL 1u   /* ncclGather of the padded bands to device 0, de-interleave kernel  */
 #define RTX_GATHER_DEVICE 2u /* RTX_SIM_BANDS (tests): bands on device 0, device copies, kernel   */
@@ -304,6 +308,17 @@ int rtx_scene_create(const rtx_scene_desc* desc, rtx_scene** out);
  * rtx_stats.node_visits.  RTX_SCENE_EVERY_BOX (or RTX_COLLAPSE=0 in the environment) keeps
  * every box test, as bvh.go:220-249 makes them. */
 #define RTX_SCENE_EVERY_BOX 2u
+/* ABI 8.  The tiered walk.  A scene walked over the library's own tree also
+ * gets a NEAR tree: the spheres themselves as leaves, each behind its own box grown by the
+ * float32 sphere test's error bound for ray origins inside a NEAR REGION (the box of the
+ * scene's non-huge spheres grown by a quarter of its extent).  A render whose camera lies in
+ * the region walks every segment that starts there on the near tree (3.9x fewer sphere
+ * tests on randSpheres); a path whose segment starts outside it is handed, once, to a
+ * second pass that continues it on the guarded tree (the reference's leaves).  The closest
+ * hit of every segment is the one bvh.go:220-249 returns (DESIGN.md §14 states why and what
+ * the tests check).  RTX_SCENE_NO_TIER (or RTX_TIER=0 in the environment) walks the guarded
+ * tree alone. */
+#define RTX_SCENE_NO_TIER 4u
 int rtx_scene_create_ex(const rtx_scene_desc* desc, uint32_t flags, rtx_scene** out);
 
 /* The tree a rebuilt scene walks for camera octant `octant` (rtx_camera_octant): *n_nodes
@@ -312,6 +327,9 @@ int rtx_scene_create_ex(const rtx_scene_desc* desc, uint32_t flags, rtx_scene** 
  * caller's tree reports *n_nodes = 0, *root = -1.  For tests and tools.                */
 int rtx_scene_topology(const rtx_scene* scene, uint32_t octant, rtx_bvh_node* nodes, uint32_t cap, uint32_t* n_nodes,
                        int32_t* root);
+/* ABI 8: octant | RTX_TREE_NEAR names the near tree of a tiered scene (rtx_scene_topology,
+ * rtx_walk_tree; *n_nodes = 0, *root = -1 when the scene has none). */
+#define RTX_TREE_NEAR 0x100u
 
 /* The same without a scene or a device: the tree rtx_scene_create_ex(desc, flags) walks for
  * `octant` (*n_nodes = 0, *root = -1 when it would keep the caller's).  Host only.       */
@@ -330,6 +348,21 @@ int rtx_scene_walk_skip(rtx_scene* scene, const rtx_camera* cam, uint8_t* skip, 
  * a first render with `cam`.  Host only.                                                   */
 int rtx_walk_skip(const rtx_scene_desc* desc, uint32_t flags, const rtx_camera* cam, uint8_t* skip, uint32_t cap,
                   uint32_t* n);
+
+/* ABI 8.  The near region of a tiered scene (box = min xyz, max xyz; a segment whose origin o
+ * has box[k] <= o[k] <= box[3 + k] for every k starts in it, a NaN origin does not; box is left
+ * alone when the scene has no near tree), and *active = whether renders with `cam` qualify:
+ * the camera's rays start in the region, spheres only, no Perlin texture.  (A render also
+ * needs both walks in the LDS copy; rtx_stats.walk_layout & RTX_LAYOUT_TIERED says whether it
+ * walked in two tiers.)  For tests and tools. */
+int rtx_scene_near_region(rtx_scene* scene, const rtx_camera* cam, float box[6], uint32_t* active);
+/* ABI 8.  rtx_scene_walk_skip of the near walk for `cam` (over rtx_scene_topology's
+ * octant | RTX_TREE_NEAR tree). */
+int rtx_scene_near_skip(rtx_scene* scene, const rtx_camera* cam, uint8_t* skip, uint32_t cap, uint32_t* n);
+/* ABI 8.  The same without a scene or a device: the near region rtx_scene_create_ex(desc,
+ * flags) would walk with and *active for `cam`.  Host only. */
+int rtx_walk_near_region(const rtx_scene_desc* desc, uint32_t flags, const rtx_camera* cam, float box[6],
+                         uint32_t* active);
 
 /* Octant of the camera's viewing direction (pixel00 + du W/2 + dv H/2 - center): bit k set
  * when it points to negative axis k. */

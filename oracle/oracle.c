@@ -343,6 +343,7 @@ typedef struct {
     float t, u, v;
     uint32_t material;
     int front;
+    const rtx_sphere* sphere; /* the sphere hit (NULL for a quad): the tiered walk's hit check */
 } hit_t;
 
 typedef struct {
@@ -364,6 +365,7 @@ static hit_t new_hit_info(float t, float u, float v, vec3 dir, vec3 point, vec3 
     h.u = u;
     h.v = v;
     h.material = mat;
+    h.sphere = NULL;
     return h;
 }
 
@@ -397,6 +399,7 @@ static int sphere_hit(const ctx_t* cx, const rtx_sphere* s, const ray_t* r, floa
     float v = theta / PI_F32;                                              /* :126 */
     (void)cx;
     *out = new_hit_info(t, u, v, r->dir, point, norm, s->material);        /* :128 */
+    out->sphere = s;
     return 1;
 }
 
@@ -455,14 +458,32 @@ void oracle_node_hooks(uint64_t* tested, uint64_t* passed, const uint8_t* skip) 
     g_node_skip = skip;
 }
 
+/* The tiered walk hook (rtx.h RTX_SCENE_NO_TIER): from the first segment of a
+ * path whose origin lies outside the near box on, the path walks the far description (with its
+ * own skips) instead of the one being rendered — the device hands such a path to its far pass,
+ * which walks the far tree to the path's end.  Both describe trees over the same spheres and
+ * materials. */
+static const rtx_scene_desc* g_tier_far;
+static const uint8_t* g_tier_far_skip;
+static float g_tier_box[6];
+static __thread int g_tier_path_far; /* this thread's current path has left the near region */
+
+void oracle_tier(const float near_box[6], const rtx_scene_desc* far, const uint8_t* far_skip) {
+    g_tier_far = far;
+    g_tier_far_skip = far_skip;
+    if (near_box) memcpy(g_tier_box, near_box, sizeof(g_tier_box));
+}
+
 /* (*BVH).Hit, bvh.go:220-249. */
 static int bvh_hit(const ctx_t* cx, const rtx_bvh_node* n, const ray_t* r, float tmin, float tmax, hit_t* out) {
     const size_t id = (size_t)(n - cx->s->nodes);
-    if (!g_node_skip || !g_node_skip[id]) {
+    const int far = g_tier_far && cx->s == g_tier_far;
+    const uint8_t* skip = far ? g_tier_far_skip : g_node_skip;
+    if (!skip || !skip[id]) {
         cx->c->node_visits++;
-        if (g_node_tested) __atomic_fetch_add(&g_node_tested[id], 1, __ATOMIC_RELAXED);
+        if (g_node_tested && !far) __atomic_fetch_add(&g_node_tested[id], 1, __ATOMIC_RELAXED);
         if (!aabb_hit(n, r, tmin, tmax)) return 0;                          /* :221 */
-        if (g_node_passed) __atomic_fetch_add(&g_node_passed[id], 1, __ATOMIC_RELAXED);
+        if (g_node_passed && !far) __atomic_fetch_add(&g_node_passed[id], 1, __ATOMIC_RELAXED);
     }
     hit_t hl, hr;
     int hit_left = hit_ref(cx, n->left, r, tmin, tmax, &hl, 0);             /* :225 */
@@ -516,8 +537,39 @@ static int list_hit(const ctx_t* cx, const rtx_list* l, const ray_t* r, float tm
     return hit_any;
 }
 
+static int world_hit_tree(const ctx_t* cx, const ray_t* r, float tmin, float tmax, hit_t* out);
+
 /* The world passed to Render: a BVH (one root) or a World list, hittables.go:55-72. */
 static int world_hit(const ctx_t* cx, const ray_t* r, float tmin, float tmax, hit_t* out) {
+    if (g_tier_far && cx->s != g_tier_far) {
+        int far = g_tier_path_far ||
+                  !(r->origin.x >= g_tier_box[0] && r->origin.x <= g_tier_box[3] && r->origin.y >= g_tier_box[1] &&
+                    r->origin.y <= g_tier_box[4] && r->origin.z >= g_tier_box[2] && r->origin.z <= g_tier_box[5]);
+        if (!far) {
+            /* The near walk, then its hit check: the hit sphere's own box (NewSphere's NewAabb,
+             * hittables.go:85-94, inside its reference leaf's box) must pass Aabb.Hit with the
+             * bound just past the hit; else the segment is walked again on the far tree. */
+            int h = world_hit_tree(cx, r, tmin, tmax, out);
+            if (!h || !out->sphere) return h;
+            const rtx_sphere* sp = out->sphere;
+            rtx_bvh_node own;
+            for (int k = 0; k < 3; ++k) {
+                float p1 = sp->center[k] + sp->radius * -1.0f, p2 = sp->center[k] + sp->radius;
+                own.bmin[k] = p1 < p2 ? p1 : p2;
+                own.bmax[k] = p1 < p2 ? p2 : p1;
+            }
+            if (aabb_hit(&own, r, tmin, nextafterf(out->t, INFINITY))) return h;
+        }
+        g_tier_path_far = 1;
+        ctx_t fx = *cx;  /* from the path's first far segment on: the far tree */
+        fx.s = g_tier_far;
+        return world_hit(&fx, r, tmin, tmax, out);
+    }
+    return world_hit_tree(cx, r, tmin, tmax, out);
+}
+
+/* The world's roots in order (the walk of one description). */
+static int world_hit_tree(const ctx_t* cx, const ray_t* r, float tmin, float tmax, hit_t* out) {
     int hit_any = 0;
     float closest = tmax;
     for (uint32_t i = 0; i < cx->s->n_roots; ++i) {
@@ -883,6 +935,7 @@ static vec3 sample_color(const ctx_t* cx, uint32_t i, uint32_t j, uint32_t k) {
     rng.draws = &cx->c->rng_draws;
     ray_t r = get_ray(cx, &rng, i, j);
     cx->c->samples++;
+    g_tier_path_far = 0;
     if (cx->order == ORACLE_ORDER_ITERATIVE) return ray_color_iter(cx, r, &rng, (int)cx->cam->max_depth);
     return ray_color_ref(cx, &r, &rng, (int)cx->cam->max_depth);
 }

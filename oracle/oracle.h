@@ -84,6 +84,11 @@ void oracle_camera_init(float aspect_ratio, int32_t image_width, const oracle_ca
  * (indexed like desc->nodes, counted atomically), and nodes whose box test is left out. */
 void oracle_node_hooks(uint64_t* tested, uint64_t* passed, const uint8_t* skip);
 
+/* Tiered-walk hook (NULL far = off): a segment whose origin lies outside near_box (min xyz, max
+ * xyz; NaN is outside) walks `far` (same spheres and materials, its own node table and roots)
+ * with far_skip instead of the rendered description. */
+void oracle_tier(const float near_box[6], const rtx_scene_desc* far, const uint8_t* far_skip);
+
 int oracle_render(const rtx_scene_desc* scene, const rtx_camera* cam, uint64_t seed, const rtx_region* region,
                   int order, int threads, float* out, oracle_counters* counters);
 

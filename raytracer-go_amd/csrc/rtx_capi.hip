@@ -62,7 +62,7 @@ struct DeviceLayout {
 
 struct DeviceCopy {
     int device = -1;
-    DeviceLayout lay[8];
+    DeviceLayout lay[16];  // [0, 8): the walk of each camera octant; [8, 16): the near walks of a tiered scene
     rtx_material* materials = nullptr;
     rtx_texture* textures = nullptr;
     uint32_t* texels = nullptr;
@@ -81,6 +81,8 @@ struct DeviceCopy {
 struct Scratch {
     float* ptr = nullptr;
     size_t bytes = 0;
+    float4* defer = nullptr;  // the tiered walk's queue of deferred paths (64 B per record)
+    size_t defer_bytes = 0;
     hipEvent_t last = nullptr;
     int scenes = 0;
 };
@@ -152,6 +154,7 @@ void release_scratch_locked(int device) {
     if (hipSetDevice(device) == hipSuccess) {
         if (sc.last) (void)hipEventSynchronize(sc.last);
         if (sc.ptr) (void)hipFree(sc.ptr);
+        if (sc.defer) (void)hipFree(sc.defer);
         if (sc.last) (void)hipEventDestroy(sc.last);
     }
     (void)hipSetDevice(cur);
@@ -281,11 +284,14 @@ struct rtx_scene {
     // rebuilt scene (topo) has one per camera octant.  Each is planned on first use, for the
     // camera of that render: the tree's entries less the box tests the collapsed walk leaves
     // out (rtx_collapse.h; skips[k]: per node entry of the uncollapsed walk, 1 = left out).
-    std::vector<rtx_entry> layouts[8];
-    std::vector<uint8_t> skips[8];
-    std::vector<double> reads[8];  // estimated reads per entry of layouts[k] (the hot set of a big scene)
-    bool planned[8] = {};
+    // Slots [8, 16) hold the near walks of a tiered scene (near_topo).
+    std::vector<rtx_entry> layouts[16];
+    std::vector<uint8_t> skips[16];
+    std::vector<double> reads[16];  // estimated reads per entry of layouts[k] (the hot set of a big scene)
+    bool planned[16] = {};
     bool rebuilt = false;
+    bool tiered = false;     // near_topo built: renders whose camera lies in its near region walk in two tiers
+    rtxd::Topology near_topo;
     bool every_box = false;  // RTX_SCENE_EVERY_BOX: no box test left out
     rtxd::Topology topo;
     std::vector<float> quadtab;  // 16 floats per quad (rtx_layout.h)
@@ -479,15 +485,20 @@ void plan_walk(const std::vector<rtx_entry>& base, const rtxd::Topology* topo, u
     rtxd::collapse_layout(E, pass, walks, collapse, out, skip, reads);
 }
 
-// Layout slot of a camera: its octant for a rebuilt scene, else 0.
-uint32_t layout_slot(const rtx_scene* s, const rtx_camera* cam) { return s->rebuilt ? rtxd::camera_octant(*cam) : 0u; }
+// Layout slot of a camera: its octant for a rebuilt scene, else 0; near walks of a tiered scene
+// at 8 + octant.
+uint32_t layout_slot(const rtx_scene* s, const rtx_camera* cam, bool near = false) {
+    return near ? 8u + rtxd::camera_octant(*cam) : (s->rebuilt ? rtxd::camera_octant(*cam) : 0u);
+}
 
 // The walk for `cam` as threaded entries (s->mu held), planned on the slot's first use.
-int scene_layout(rtx_scene* s, const rtx_camera* cam, const std::vector<rtx_entry>** out) {
-    const uint32_t k = layout_slot(s, cam);
+int scene_layout(rtx_scene* s, const rtx_camera* cam, const std::vector<rtx_entry>** out, bool near = false) {
+    const uint32_t k = layout_slot(s, cam, near);
+    if (near && !s->tiered) return fail(RTX_ERR_INVALID_ARG, "scene has no near walk");
     if (!s->planned[k]) {
-        plan_walk(s->base, s->rebuilt ? &s->topo : nullptr, k, s->quadtab, *cam, collapse_enabled(s->every_box),
-                  s->layouts[k], s->skips[k], &s->reads[k]);
+        const rtxd::Topology* t = near ? &s->near_topo : (s->rebuilt ? &s->topo : nullptr);
+        plan_walk(s->base, t, k & 7u, s->quadtab, *cam, collapse_enabled(s->every_box), s->layouts[k], s->skips[k],
+                  &s->reads[k]);
         s->planned[k] = true;
     }
     *out = &s->layouts[k];
@@ -495,11 +506,11 @@ int scene_layout(rtx_scene* s, const rtx_camera* cam, const std::vector<rtx_entr
 }
 
 // Upload the walk layout for `cam` to copy c (current device = c's; s->mu held).
-int ensure_layout(rtx_scene* s, DeviceCopy* c, const rtx_camera* cam) {
-    const uint32_t oct = layout_slot(s, cam);
+int ensure_layout(rtx_scene* s, DeviceCopy* c, const rtx_camera* cam, bool near = false) {
+    const uint32_t oct = layout_slot(s, cam, near);
     if (c->lay[oct].entries) return RTX_OK;
     const std::vector<rtx_entry>* E = nullptr;
-    if (int rc = scene_layout(s, cam, &E)) return rc;
+    if (int rc = scene_layout(s, cam, &E, near)) return rc;
     DeviceLayout& lay = c->lay[oct];
     HIP_TRY(hipMalloc(&lay.entries, (E->size() + 1) * sizeof(rtx_entry) + s->quadtab.size() * sizeof(float)));
     {  // device layout: all 'a' halves, then all 'b' halves (rtxd::SceneRef), each ending
@@ -685,6 +696,33 @@ int topology_mode(uint32_t flags, const std::vector<rtx_entry>& ref) {
     return rtxd::precise_enough(ref) ? 1 : 0;
 }
 
+// The tiered walk: a guarded scene also gets a near tree (spheres behind their own
+// boxes grown for origins in the near region), unless RTX_SCENE_NO_TIER or RTX_TIER=0.
+bool tier_topology(uint32_t flags, int mode, const std::vector<rtx_entry>& base, rtxd::Topology& near) {
+    if (mode != 1 || (flags & RTX_SCENE_NO_TIER)) return false;
+    const char* e = std::getenv("RTX_TIER");
+    if (e && std::strcmp(e, "0") == 0) return false;
+    float box[6];
+    return rtxd::near_region(base, box) && rtxd::build_topology(base, false, near, box);
+}
+
+// A tiered scene walks in two tiers for a camera whose rays all start in the near region (the
+// defocus disk's box, with room for rounding, inside it): else the guarded walk alone.
+bool camera_in_box(const float* b, const rtx_camera* cam) {
+    for (int k = 0; k < 3; ++k) {
+        const double c = cam->center[k];
+        const double rad = cam->defocus_angle > 0.0f
+                               ? std::fabs((double)cam->defocus_disk_u[k]) + std::fabs((double)cam->defocus_disk_v[k])
+                               : 0.0;
+        const double pad = rad * 1.0e-3 + std::fabs(c) * 1.0e-6 + 1.0e-6;
+        if (!(c - rad - pad > (double)b[k] && c + rad + pad < (double)b[3 + k])) return false;
+    }
+    return true;
+}
+bool camera_in_near(const rtx_scene* s, const rtx_camera* cam) {
+    return s->tiered && camera_in_box(s->near_topo.near_box, cam);
+}
+
 // A scene whose base holds the reference's walk of one tree: take the walk's own tree when it
 // qualifies (spheres only; rtxd::build_topology).
 void adopt_topology(rtx_scene* s, uint32_t flags) {
@@ -692,6 +730,7 @@ void adopt_topology(rtx_scene* s, uint32_t flags) {
     const int mode = topology_mode(flags, s->base);
     if (mode == 0 || !rtxd::build_topology(s->base, mode == 1, s->topo)) return;
     s->rebuilt = true;
+    s->tiered = tier_topology(flags, mode, s->base, s->near_topo);
 }
 
 // The quad table of a scene description (rtx_layout.h): (Q, material), (u, 0), (v, 0), (w, 0).
@@ -708,8 +747,8 @@ void quad_table(const rtx_scene_desc* d, std::vector<float>& tab) {
     }
 }
 
-uint64_t walk_layout(const rtx_scene* s, const rtx_camera* cam) {
-    return s->rebuilt ? rtxd::camera_octant(*cam) : RTX_LAYOUT_REFERENCE;
+uint64_t walk_layout(const rtx_scene* s, const rtx_camera* cam, bool tiered) {
+    return (s->rebuilt ? rtxd::camera_octant(*cam) : RTX_LAYOUT_REFERENCE) | (tiered ? RTX_LAYOUT_TIERED : 0u);
 }
 
 int check_camera(const rtx_camera* cam) {
@@ -803,11 +842,23 @@ rtxd::Params make_params(const rtx_scene* s, const DeviceCopy* c, uint32_t oct, 
 
 // Enqueue one region on the current device, bracketed by HIP events on `stream`.
 // *chunks receives the number of sample chunks (render kernel launches).
+// *tiered: whether the render walks in two tiers.
 int enqueue_on(rtx_scene* s, DeviceCopy* c, const rtx_camera* cam, uint64_t seed, const rtx_region* r, float* d_out,
-               hipStream_t stream, uint32_t flags, bool timed, uint32_t* chunks) {
+               hipStream_t stream, uint32_t flags, bool timed, uint32_t* chunks, bool* tiered) {
     const uint32_t oct = layout_slot(s, cam);  // the walk's layout (rtx_topology.h, rtx_collapse.h)
     if (int rc = ensure_layout(s, c, cam)) return rc;
     rtxd::Params p = make_params(s, c, oct, cam, seed, r, d_out);
+    // the tiered walk: a camera in the near region, both walks in the LDS copy (not for the
+    // RTX_FLAG_NO_LDS A/B)
+    bool tier = camera_in_near(s, cam) && !(flags & RTX_FLAG_NO_LDS) && p.n_quads == 0 &&
+                !p.has_noise && rtxd::scene_placement(p, flags) == RTX_SCENE_IN_LDS;
+    rtxd::Params pn;
+    if (tier) {
+        if (int rc = ensure_layout(s, c, cam, true)) return rc;
+        pn = make_params(s, c, 8u + oct, cam, seed, r, d_out);
+        tier = rtxd::scene_placement(pn, flags) == RTX_SCENE_IN_LDS;
+    }
+    *tiered = false;
     const uint32_t th = (flags >> 8) & 0x7Fu;  // RTX_FLAG_SHADE_THRESH(n) override
     if (th) p.shade_thresh = th > 64 ? 64 : th;
     *chunks = 0;
@@ -843,12 +894,48 @@ int enqueue_on(rtx_scene* s, DeviceCopy* c, const rtx_camera* cam, uint64_t seed
         p.grid_pct = env_knob("RTX_ITEM_GRID", 100, 1, 100);
         p.debug_launch = env_knob("RTX_DEBUG_LAUNCH", 0, 0, 1);
         p.prim_batch = env_knob("RTX_PRIM_BATCH", 16, 1, 65);  // 65: primitive tests only when no node is left
+        if (tier) {
+            // The queue of deferred paths, per device: an eighth of the chunk's items (measured:
+            // 3.2 % of randSpheres' paths leave the near region), at most RTX_DEFER_MB (default
+            // 4 GiB) of records; RTX_DEFER_CAP overrides (tests).  A chunk that overflows it is
+            // rendered again whole by the redo pass.
+            const uint64_t items = chunk * (per_sample / 12);
+            uint64_t cap = std::max<uint64_t>(items / 8, 4096);
+            cap = std::min<uint64_t>(cap, ((uint64_t)env_knob("RTX_DEFER_MB", 4096, 1, 1 << 20) << 20) / 64);
+            cap = std::min<uint64_t>(cap, 0xFFFFFFFFull / 2);
+            if (const char* e = std::getenv("RTX_DEFER_CAP")) cap = std::strtoull(e, nullptr, 10);
+            const size_t need = (size_t)std::max<uint64_t>(cap, 1) * 64;
+            if (scr->defer_bytes < need) {
+                HIP_TRY(hipEventSynchronize(scr->last));
+                if (scr->defer) HIP_TRY(hipFree(scr->defer));
+                scr->defer = nullptr;
+                scr->defer_bytes = 0;
+                HIP_TRY(hipMalloc(&scr->defer, need));
+                scr->defer_bytes = need;
+            }
+            rtxd::Params lay = pn;  // the near pass: every setting of p, the near walk's layout
+            pn = p;
+            pn.entries = lay.entries;
+            pn.n_entries = lay.n_entries;
+            pn.n_hot = lay.n_hot;
+            pn.start = lay.start;
+            pn.prim_end = lay.prim_end;
+            pn.tier = 1;
+            p.tier = 2;
+            pn.defer = p.defer = scr->defer;
+            pn.defer_cap = p.defer_cap = (uint32_t)cap;
+            pn.defer_count = p.defer_count = reinterpret_cast<uint32_t*>(c->counters + 22);  // low: records
+            pn.redo_flag = p.redo_flag = reinterpret_cast<uint32_t*>(c->counters + 22) + 1;  // high: overflow
+            std::memcpy(pn.near_min, s->near_topo.near_box, 3 * sizeof(float));
+            std::memcpy(pn.near_max, s->near_topo.near_box + 3, 3 * sizeof(float));
+            *tiered = true;
+        }
     }
     c->placement = rtxd::scene_placement(p, flags);
     // every stats slot, the unit queue head and the watchdog flag start at 0 for every render
     HIP_TRY(hipMemsetAsync(c->counters, 0, rtxd::COUNTER_SLOTS * sizeof(unsigned long long), stream));
     if (timed) HIP_TRY(hipEventRecord(c->ev0, stream));
-    HIP_TRY(rtxd::launch_render(p, flags, stream));
+    HIP_TRY(*tiered ? rtxd::launch_render(pn, flags, stream, &p) : rtxd::launch_render(p, flags, stream));
     if (timed) HIP_TRY(hipEventRecord(c->ev1, stream));
     HIP_TRY(hipEventRecord(scr->last, stream));
     return RTX_OK;
@@ -882,6 +969,8 @@ int collect_on(DeviceCopy* c, bool count, uint64_t samples, uint32_t chunks, rtx
     st->deferred_lanes = h[17];
     for (int q = 0; q < 4; ++q) st->shade_split_cycles[q] = h[18 + q];
     st->sample_chunks = chunks;
+    st->deferred_paths = h[23];
+    st->redo_chunks = h[24];
     st->kernel_ms = ms;
     st->scene_placement = c->placement;
     return RTX_OK;
@@ -983,6 +1072,8 @@ void add_stats(rtx_stats* acc, const rtx_stats& s) {
     acc->deferred_lanes += s.deferred_lanes;
     for (int q = 0; q < 4; ++q) acc->shade_split_cycles[q] += s.shade_split_cycles[q];
     acc->sample_chunks = std::max(acc->sample_chunks, s.sample_chunks);
+    acc->deferred_paths += s.deferred_paths;
+    acc->redo_chunks += s.redo_chunks;
     acc->scene_placement = s.scene_placement;
 }
 
@@ -1075,16 +1166,19 @@ uint64_t rtx_scene_export(const rtx_scene* s, void* out, uint64_t cap) {
 int rtx_scene_topology(const rtx_scene* s, uint32_t octant, rtx_bvh_node* nodes, uint32_t cap, uint32_t* n_nodes,
                        int32_t* root) {
     g_last_error.clear();
+    const bool near = (octant & RTX_TREE_NEAR) != 0;
+    octant &= ~RTX_TREE_NEAR;
     if (!s || !n_nodes || !root || octant > 7) return fail(RTX_ERR_INVALID_ARG, "bad argument");
-    if (!s->rebuilt) {
+    if (near ? !s->tiered : !s->rebuilt) {
         *n_nodes = 0;
         *root = -1;
         return RTX_OK;
     }
+    const rtxd::Topology& t = near ? s->near_topo : s->topo;
     std::vector<rtx_bvh_node> v;
-    rtxd::orient_topology(s->topo, octant, v);
+    rtxd::orient_topology(t, octant, v);
     *n_nodes = (uint32_t)v.size();
-    *root = s->topo.root;
+    *root = t.root;
     if (nodes && cap >= v.size()) std::memcpy(nodes, v.data(), v.size() * sizeof(rtx_bvh_node));
     return RTX_OK;
 }
@@ -1107,6 +1201,51 @@ int rtx_scene_walk_skip(rtx_scene* s, const rtx_camera* cam, uint8_t* skip, uint
     const std::vector<rtx_entry>* E = nullptr;
     if (int rc = scene_layout(s, cam, &E)) return rc;
     return copy_skip(s->skips[layout_slot(s, cam)], skip, cap, n);
+}
+
+int rtx_scene_near_skip(rtx_scene* s, const rtx_camera* cam, uint8_t* skip, uint32_t cap, uint32_t* n) {
+    g_last_error.clear();
+    if (!s || !n) return fail(RTX_ERR_INVALID_ARG, "bad argument");
+    if (int rc = check_camera(cam)) return rc;
+    std::lock_guard<std::mutex> lk(s->mu);
+    const std::vector<rtx_entry>* E = nullptr;
+    if (int rc = scene_layout(s, cam, &E, true)) return rc;
+    return copy_skip(s->skips[layout_slot(s, cam, true)], skip, cap, n);
+}
+
+int rtx_scene_near_region(rtx_scene* s, const rtx_camera* cam, float box[6], uint32_t* active) {
+    g_last_error.clear();
+    if (!s || !box || !active) return fail(RTX_ERR_INVALID_ARG, "bad argument");
+    if (int rc = check_camera(cam)) return rc;
+    std::lock_guard<std::mutex> lk(s->mu);
+    *active = 0;
+    if (!s->tiered) return RTX_OK;
+    std::memcpy(box, s->near_topo.near_box, 6 * sizeof(float));
+    *active = camera_in_near(s, cam) && !s->has_noise && s->quadtab.empty();
+    return RTX_OK;
+}
+
+int rtx_walk_near_region(const rtx_scene_desc* d, uint32_t flags, const rtx_camera* cam, float box[6],
+                         uint32_t* active) {
+    g_last_error.clear();
+    if (!d || !box || !active) return fail(RTX_ERR_INVALID_ARG, "bad argument");
+    if (int rc = check_camera(cam)) return rc;
+    if (d->n_roots == 0 || !d->roots) return fail(RTX_ERR_INVALID_ARG, "scene has no root");
+    if (d->n_nodes && !d->nodes) return fail(RTX_ERR_INVALID_ARG, "nodes is NULL");
+    if (int rc = validate_tables(d)) return rc;
+    if (int rc = check_acyclic(d)) return rc;
+    std::vector<rtx_entry> base;
+    for (uint32_t i = 0; i < d->n_roots; ++i)
+        if (int rc = emit(d, d->roots[i], base)) return rc;
+    *active = 0;
+    rtxd::Topology t, nt;
+    const int mode = d->n_roots == 1 ? topology_mode(flags, base) : 0;
+    if (mode == 0 || !rtxd::build_topology(base, mode == 1, t) || !tier_topology(flags, mode, base, nt)) return RTX_OK;
+    std::memcpy(box, nt.near_box, 6 * sizeof(float));
+    bool noise = false;
+    for (uint32_t i = 0; i < d->n_textures; ++i) noise |= d->textures[i].type == RTX_TEX_NOISE;
+    *active = camera_in_box(nt.near_box, cam) && d->n_quads == 0 && !noise;
+    return RTX_OK;
 }
 
 int rtx_walk_skip(const rtx_scene_desc* d, uint32_t flags, const rtx_camera* cam, uint8_t* skip, uint32_t cap,
@@ -1136,6 +1275,8 @@ int rtx_walk_skip(const rtx_scene_desc* d, uint32_t flags, const rtx_camera* cam
 int rtx_walk_tree(const rtx_scene_desc* d, uint32_t flags, uint32_t octant, rtx_bvh_node* nodes, uint32_t cap,
                   uint32_t* n_nodes, int32_t* root) {
     g_last_error.clear();
+    const bool near = (octant & RTX_TREE_NEAR) != 0;
+    octant &= ~RTX_TREE_NEAR;
     if (!d || !n_nodes || !root || octant > 7) return fail(RTX_ERR_INVALID_ARG, "bad argument");
     if (d->n_roots == 0 || !d->roots) return fail(RTX_ERR_INVALID_ARG, "scene has no root");
     if (d->n_nodes && !d->nodes) return fail(RTX_ERR_INVALID_ARG, "nodes is NULL");
@@ -1146,7 +1287,8 @@ int rtx_walk_tree(const rtx_scene_desc* d, uint32_t flags, uint32_t octant, rtx_
         if (int rc = emit(d, d->roots[i], ref)) return rc;
     rtxd::Topology t;
     const int mode = topology_mode(flags, ref);
-    if (d->n_roots != 1 || mode == 0 || !rtxd::build_topology(ref, mode == 1, t)) {
+    if (d->n_roots != 1 || mode == 0 || !rtxd::build_topology(ref, mode == 1, t) ||
+        (near && !tier_topology(flags, mode, ref, t))) {
         *n_nodes = 0;
         *root = -1;
         return RTX_OK;
@@ -1189,11 +1331,13 @@ int rtx_render_region_device(rtx_scene* s, const rtx_camera* cam, uint64_t seed,
     HIP_TRY(hipSetDevice(cur));
     const bool count = (flags & RTX_FLAG_COUNTERS) != 0;
     uint32_t chunks = 0;
-    if (int rc = enqueue_on(s, c, cam, seed, region, d_out, (hipStream_t)hip_stream, flags, stats != nullptr, &chunks))
+    bool tiered = false;
+    if (int rc = enqueue_on(s, c, cam, seed, region, d_out, (hipStream_t)hip_stream, flags, stats != nullptr, &chunks,
+                            &tiered))
         return rc;
     if (!stats) return RTX_OK;
     const int rc = collect_on(c, count, (uint64_t)region_rows(region) * region->width * cam->samples_per_pixel, chunks, stats);
-    stats->walk_layout = walk_layout(s, cam);
+    stats->walk_layout = walk_layout(s, cam, tiered);
     return rc;
 }
 
@@ -1235,6 +1379,7 @@ int rtx_render_ex(rtx_scene* s, const rtx_camera* cam, uint64_t seed, int n_gpus
     rtx_stats total;
     std::memset(&total, 0, sizeof(total));
     int rc = RTX_OK;
+    bool tiered = false;
     // 1. Each band (rows y % n == d) renders on its device, the devices concurrently.
     for (int d = 0; d < n && rc == RTX_OK; ++d) {
         const int dv = dev_of(d);
@@ -1247,7 +1392,7 @@ int rtx_render_ex(rtx_scene* s, const rtx_camera* cam, uint64_t seed, int n_gpus
             rc = fail(RTX_ERR_OOM, "hipMalloc band %zu B", band_bytes);
             break;
         }
-        rc = enqueue_on(s, c, cam, seed, &regs[d], bufs[d], streams[d], kflags, true, &chunks[d]);
+        rc = enqueue_on(s, c, cam, seed, &regs[d], bufs[d], streams[d], kflags, true, &chunks[d], &tiered);
     }
     // 2. Wait for every band (and read its counters), so gather_ms times only the gather.
     for (int d = 0; d < n && rc == RTX_OK; ++d) {
@@ -1355,7 +1500,7 @@ int rtx_render_ex(rtx_scene* s, const rtx_camera* cam, uint64_t seed, int n_gpus
     for (int d = 0; d < n; ++d)  // nothing of this call still in flight when the buffers are reused
         if (streams[d] && hipSetDevice(dev_of(d)) == hipSuccess) (void)hipStreamSynchronize(streams[d]);
     (void)hipSetDevice(cur);
-    total.walk_layout = walk_layout(s, cam);
+    total.walk_layout = walk_layout(s, cam, tiered);
     total.gather_kind = kind;
     if (rc == RTX_OK && stats) *stats = total;
     return rc;

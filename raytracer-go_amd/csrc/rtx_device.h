@@ -424,7 +424,7 @@ constexpr uint32_t RTX_DEV_TEX_INLINE = 0xFFFFFFFFu;
 // ---------------------------------------------------------------------------------
 // Kernel parameters
 // ---------------------------------------------------------------------------------
-constexpr uint32_t COUNTER_SLOTS = 24;  // device stats slots (rtx_capi.hip collect_on)
+constexpr uint32_t COUNTER_SLOTS = 26;  // device stats slots (rtx_capi.hip collect_on)
 
 struct Params {
     const float4* entries;   // n_entries + 1 'a' halves, as many 'b', 4 * n_quads (SceneRef)
@@ -457,6 +457,16 @@ struct Params {
     uint32_t prim_batch;  // v3: primitive tests wait for this many lanes (trav_step_batched); 0 = off
     uint32_t start;       // walk position of the walk's first entry (the root)
     uint32_t prim_end;    // scene in the LDS copy: its primitives are stored below this position
+    // The tiered walk: the near pass walks the near tree and hands every path whose
+    // next segment starts outside the near region [near_min, near_max] to the far pass, which walks
+    // the guarded tree.  A path is handed over once, as a 64-B record at its segment start.
+    uint32_t tier;          // 0: one walk; 1: the near pass; 2: the far pass (resumes the records)
+    uint32_t redo_only;     // 1: render the chunk only if the near pass overflowed its queue
+    float near_min[3], near_max[3];
+    float4* defer;          // the records: 4 float4 each (origin | pixel, dir | sample, thr | seg, acc | slot)
+    uint32_t defer_cap;     // records the queue holds
+    uint32_t* defer_count;  // records written (the far pass reads min(count, cap))
+    uint32_t* redo_flag;    // set when a record did not fit: the chunk's redo pass renders it whole
 };
 
 struct Ray {
@@ -797,6 +807,25 @@ __device__ __forceinline__ float med3(float a, float b, float c) {
 // origin (a zero direction component gives 1/dir = inf and 0 * inf = NaN when the origin lies
 // on a slab plane, which the reference ignores (`t0 > min` is false for NaN) — those rays take
 // the select path).  20 VALU per box instead of 24.
+// The tiered walk's hit check: whether the sphere (centre, radius) = sa's own box,
+// NewAabb(c - r, c + r) as NewSphere makes it (hittables.go:85-94), passes Aabb.Hit (bvh.go:52-61,
+// 84-102) for the ray with interval [0.001, the float after t.closest] — the bound at which the
+// guarded walk's test of the sphere's leaf box (a superset) would still accept this hit.
+__device__ __forceinline__ bool own_box_pass(const Trav& t, const Ray& r, const float4 sa) {
+    const float rr = sa.w * -1.0f;
+    const float ax = sa.x + rr, bx = sa.x + sa.w, ay = sa.y + rr, by = sa.y + sa.w, az = sa.z + rr, bz = sa.z + sa.w;
+    const float mnx = __builtin_fminf(ax, bx), mxx = __builtin_fmaxf(ax, bx);
+    const float mny = __builtin_fminf(ay, by), mxy = __builtin_fmaxf(ay, by);
+    const float mnz = __builtin_fminf(az, bz), mxz = __builtin_fmaxf(az, bz);
+    const float t0x = ((t.nx ? mxx : mnx) - r.o.x) * t.ix, t1x = ((t.nx ? mnx : mxx) - r.o.x) * t.ix;
+    const float t0y = ((t.ny ? mxy : mny) - r.o.y) * t.iy, t1y = ((t.ny ? mny : mxy) - r.o.y) * t.iy;
+    const float t0z = ((t.nz ? mxz : mnz) - r.o.z) * t.iz, t1z = ((t.nz ? mnz : mxz) - r.o.z) * t.iz;
+    const float bound = __int_as_float(__float_as_int(t.closest) + 1);  // t.closest > 0, finite
+    const float lo = __builtin_fmaxf(__builtin_fmaxf(__builtin_fmaxf(0.001f, t0x), t0y), t0z);
+    const float hi = __builtin_fminf(__builtin_fminf(__builtin_fminf(bound, t1x), t1y), t1z);
+    return lo < hi;
+}
+
 template <bool COUNT, bool MED3 = false>
 __device__ __forceinline__ void box_step(Trav& t, const Ray& r, const float4 ea, const float4 eb, int32_t tag,
                                          Counters& cnt) {

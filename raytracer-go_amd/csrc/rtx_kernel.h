@@ -8,7 +8,10 @@ struct Params;
 // chunk; the caller provides p.scratch / p.kn / p.sub).  flags: RTX_FLAG_COUNTERS selects
 // the instantiation that accumulates the work counters into p.counters; RTX_FLAG_NO_LDS
 // reads the scene from global memory (A/B, identical output).
-hipError_t launch_render(const Params& p, uint32_t flags, hipStream_t stream);
+// far != nullptr: a tiered walk: p is the near pass (p.tier = 1), *far the far
+// pass over the same region (tier 2), per chunk: near pass, far pass, redo pass (the far layout
+// over the whole chunk, only if the near pass's queue overflowed), then the reduction.
+hipError_t launch_render(const Params& p, uint32_t flags, hipStream_t stream, const Params* far = nullptr);
 // Where a launch reads the scene (RTX_SCENE_IN_LDS / LDS_CACHE / IN_HBM, rtx.h).
 uint32_t scene_placement(const Params& p, uint32_t flags);
 }  // namespace rtxd

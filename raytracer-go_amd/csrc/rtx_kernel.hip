@@ -175,10 +175,22 @@ __device__ __forceinline__ void split_clk(uint64_t& acc, uint64_t& clk) {
 // ------------------------------------------------------------------------------------
 // CLK (RTX_FLAG_TIMING, diagnostics): the timed kernel (asm walk, no work counters) with the
 // counting kernel's s_memtime split of wave cycles into walk and shading phases.
+//
+// TIER: 1 = the near pass of a tiered walk: a path whose next segment starts
+// outside the near region is written to the defer queue (its segment start: ray, throughput,
+// colour so far, pixel, sample, segment, scratch slot) and its lane takes a new item; 2 = the far
+// pass: the items are the queue's records, each resumed at its segment start on the guarded tree.
+// Every sample's Philox blocks are keyed by (pixel, sample, event), so a path resumed in another
+// launch draws exactly what it would have drawn.
 template <bool COUNT, bool USE_LDS, bool QUADS, bool NOISE, int WAVES = 8, int MINW = 0, bool HYB = false,
-          bool CLK = false>
+          bool CLK = false, int TIER = 0>
 __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
     constexpr bool TIME = COUNT || CLK;
+    // the redo pass of a tiered chunk runs only when the near pass's queue overflowed
+    if (p.redo_only) {
+        if (__builtin_amdgcn_readfirstlane(*(volatile uint32_t*)p.redo_flag) == 0u) return;
+        if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&p.counters[24], 1ull);  // chunks redone
+    }
     // walk steps between two wave votes (A/B with primitive batching: 4 +0.7 %, 8 +0.8 %, 12 +1.3 %)
     constexpr uint32_t WAVE_BLOCK = 64 * WAVES, STEPS = RTX_WALK_STEPS;
     extern __shared__ float4 lds_entries[];
@@ -224,7 +236,12 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
     const uint32_t tiles_x = (p.width + 7u) / 8u;
     const uint32_t n_tiles = tiles_x * ((p.rows + 7u) / 8u);
     const uint32_t nsub = (p.kn + p.sub - 1u) / p.sub;
-    const uint64_t n_units = (uint64_t)n_tiles * nsub;
+    // far pass: units of 64 queue records
+    const uint32_t n_rec = TIER == 2 ? min(__builtin_amdgcn_readfirstlane(*(volatile uint32_t*)p.defer_count), p.defer_cap)
+                                     : 0u;
+    const uint64_t n_units = TIER == 2 ? (uint64_t)((n_rec + 63u) / 64u) : (uint64_t)n_tiles * nsub;
+    if (TIER == 2 && blockIdx.x == 0 && threadIdx.x == 0 && n_rec)
+        atomicAdd(&p.counters[23], (unsigned long long)n_rec);  // deferred paths, all chunks
     const size_t tile_floats = (size_t)n_tiles * 64 * 3;  // one sample of every tile (tile-major scratch)
 
     // the wave's unit (uniform, kept in SGPRs: every value below is derived from readfirstlane):
@@ -253,6 +270,35 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
         ++items_done;
     };
 
+    // near pass: hand the lanes with `far` set (their segment starts at r) to the far pass (the whole
+    // wave is here; one queue atomic per wave)
+    auto defer = [&](const bool far) {
+        const uint64_t fm = ballot(far);
+        if (fm == 0) return;
+        uint32_t b = 0;
+        if (lane == 0) b = atomicAdd(p.defer_count, (uint32_t)__popcll(fm));
+        b = __builtin_amdgcn_readfirstlane(b);
+        if (far) {
+            const uint32_t slot = b + (uint32_t)__popcll(fm & ((1ull << lane) - 1ull));
+            if (slot < p.defer_cap) {
+                float4* q = p.defer + 4 * (size_t)slot;
+                q[0] = make_float4(r.o.x, r.o.y, r.o.z, __uint_as_float(rng.pixel));
+                q[1] = make_float4(r.d.x, r.d.y, r.d.z, __uint_as_float(rng.sample));
+                q[2] = make_float4(thr.x, thr.y, thr.z, __uint_as_float(seg));
+                q[3] = make_float4(acc.x, acc.y, acc.z, __uint_as_float((uint32_t)pix));
+            } else {
+                atomicOr(p.redo_flag, 1u);  // the redo pass renders the chunk again, whole
+            }
+            mode = M_CLAIM;
+        }
+    };
+    auto defer_far = [&](bool& ready) {  // segments that would start outside the near region
+        const bool far = ready && !(r.o.x >= p.near_min[0] && r.o.x <= p.near_max[0] && r.o.y >= p.near_min[1] &&
+                                    r.o.y <= p.near_max[1] && r.o.z >= p.near_min[2] && r.o.z <= p.near_max[2]);
+        defer(far);
+        if (far) ready = false;
+    };
+
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
     uint32_t iter = 0;
     for (;;) {
@@ -278,6 +324,16 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
         if (ballot(mode != M_DONE) == 0) break;
 
         // ---- shading phase ----------------------------------------------------------
+        if constexpr (TIER == 1) {
+            // The near walk's closest hit is the guarded walk's when the hit sphere's own box (inside
+            // its reference leaf's) passes with the bound just past the hit; else the
+            // segment is walked again on the guarded tree by the far pass.
+            const bool check = mode == M_SHADE && t.hit >= 0;
+            bool bad = false;
+            if (check) bad = !own_box_pass(t, r, E.a[t.hit]);
+            if (COUNT && bad) --cnt.segments;  // the far pass walks the segment again and counts it
+            defer(bad);
+        }
         U4 b0{0u, 0u, 0u, 0u};
         if (mode == M_SHADE && t.hit >= 0) b0 = rng.block(seg + 1, 0u);
         const Scatter sc = coop_scatter<QUADS>(p, E, rng, seg + 1, mode == M_SHADE ? t.hit : -1, b0);
@@ -298,6 +354,7 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
                 ready = true;
             }
         }
+        if constexpr (TIER == 1) defer_far(ready);  // before the claims: the lane takes a new item now
         if (TIME) split_clk(split[1], clk);
         // Lanes without an item take the next ones of the wave's unit; new camera rays
         // at one program point.  Loops only for max depth 0 and ragged tiles.
@@ -309,7 +366,11 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
                 if (lane == 0) un = atomicAdd(p.tile_counter, 1u);
                 const uint32_t uu = __builtin_amdgcn_readfirstlane(un);  // the whole wave is here: lane 0's
                 exhausted = uu >= n_units;
-                if (!exhausted) {
+                if (!exhausted && TIER == 2) {
+                    u_k0 = 64u * uu;  // the unit's first record
+                    u_items = min(64u, n_rec - u_k0);
+                    cursor = 0;
+                } else if (!exhausted) {
                     const uint32_t u_tile = uu / nsub;
                     u_x8 = (u_tile % tiles_x) * 8u;
                     u_r8 = (u_tile / tiles_x) * 8u;
@@ -325,7 +386,19 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
             }
             const uint32_t rank = (uint32_t)__popcll(wm & ((1ull << lane) - 1ull));
             bool got = false;
-            if (mode == M_CLAIM && rank < u_items - cursor) {
+            if (TIER == 2 && mode == M_CLAIM && rank < u_items - cursor) {  // resume a record
+                const float4* q = p.defer + 4 * (size_t)(u_k0 + cursor + rank);
+                const float4 q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3];
+                r = Ray{v3(q0.x, q0.y, q0.z), v3(q1.x, q1.y, q1.z)};
+                rng.pixel = __float_as_uint(q0.w);
+                rng.sample = __float_as_uint(q1.w);
+                thr = v3(q2.x, q2.y, q2.z);
+                seg = __float_as_uint(q2.w);
+                acc = v3(q3.x, q3.y, q3.z);
+                pix = __float_as_uint(q3.w);
+                mode = M_START;
+                ready = true;
+            } else if (TIER != 2 && mode == M_CLAIM && rank < u_items - cursor) {
                 const uint32_t j = cursor + rank, l = j & 63u;  // sample-major within the unit
                 const uint32_t lx = u_x8 + (l & 7u);
                 const uint32_t lr = u_r8 + (l >> 3);
@@ -353,6 +426,7 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
                 }
             }
         }
+        if constexpr (TIER == 1) defer_far(ready);  // a camera ray outside the region (the host's gate makes it rare)
         if (TIME) split_clk(split[2], clk);
         if (ready) {  // begin a segment: world.Hit (ray.go:36)
             if (COUNT) ++cnt.segments;
@@ -425,6 +499,26 @@ constexpr uint32_t LDS_MAX_BYTES = 64 * 1024;
 
 // v3: chunks of p.kn samples (the scratch holds one chunk), each rendered by a
 // resident-capacity grid of render_items and summed into p.out by reduce_samples.
+// Samples per unit: 8, or fewer when that leaves under 8 units per resident wave (a small
+// image's last units would run on a near-empty GPU).  Measured at 100 spp: 1920x1080 8 -1.6 % vs
+// 16; 400x225 2 -42 % vs 16; Cornell 600x600 8 -3 % vs 16.  16 when that still leaves >= 64
+// units per wave (the drain stays short): 1920x1080x500 -0.9 % vs 8 (142.5 vs 143.8 ms).
+inline uint32_t unit_samples(uint64_t tiles, uint32_t kn, int waves, int per_cu, int cus) {
+    const uint64_t per_wave = tiles * kn / (8ull * waves * (uint64_t)per_cu * cus);
+    return per_wave >= 128 ? RTX_SUB_MAX : (per_wave >= 8 ? 8u : (per_wave >= 4 ? 4u : (per_wave >= 2 ? 2u : 1u)));
+}
+
+hipError_t resident_grid(const void* kern, int block, size_t shmem, int* per_cu, int* cus) {
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e == hipSuccess) e = hipDeviceGetAttribute(cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, kern, block, shmem);
+    if (*per_cu < 1) *per_cu = 1;
+    return e;
+}
+
+// v3: chunks of p.kn samples (the scratch holds one chunk), each rendered by a
+// resident-capacity grid of render_items and summed into p.out by reduce_samples.
 template <bool COUNT, bool QUADS, bool NOISE, int WAVES = 8, int MINW = 0, bool CLK = false>
 hipError_t launch_items(Params p, bool use_lds, hipStream_t stream) {
     // a scene too big for LDS: its top levels (p.n_hot entries) cached in LDS when the
@@ -436,28 +530,16 @@ hipError_t launch_items(Params p, bool use_lds, hipStream_t stream) {
                               : (hyb ? render_items<COUNT, false, QUADS, NOISE, WAVES, MINW, !NOISE, CLK>
                                      : render_items<COUNT, false, QUADS, NOISE, WAVES, MINW, false, CLK>);
     constexpr int block = 64 * WAVES;
-    int dev = 0, cus = 0, per_cu = 0;
-    hipError_t e = hipGetDevice(&dev);
-    if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, block, shmem);
+    int cus = 0, per_cu = 0;
+    hipError_t e = resident_grid((const void*)kern, block, shmem, &per_cu, &cus);
     if (e != hipSuccess) return e;
-    if (per_cu < 1) per_cu = 1;
     const uint32_t spp = p.cam.samples_per_pixel, chunk = p.kn, sub = p.sub;
     const uint64_t tiles = (uint64_t)((p.width + 7) / 8) * ((p.rows + 7) / 8);
     const uint64_t slots = tiles * 64;  // pixels of the tile-major scratch (ragged tiles padded)
     for (uint32_t k0 = 0; k0 < spp; k0 += chunk) {
         p.k0 = k0;
         p.kn = spp - k0 < chunk ? spp - k0 : chunk;
-        if (sub == 0) {
-            // Samples per unit: 8, or fewer when that leaves under 8 units per resident wave
-            // (a small image's last units would run on a near-empty GPU).  Measured at 100 spp:
-            // 1920x1080 8 -1.6 % vs 16; 400x225 2 -42 % vs 16; Cornell 600x600 8 -3 % vs 16.
-            // 16 when that still leaves >= 64 units per wave (the drain stays short): 1920x1080x500
-            // -0.9 % vs 8 (142.5 vs 143.8 ms).
-            const uint64_t per_wave = tiles * p.kn / (8ull * WAVES * (uint64_t)per_cu * cus);
-            p.sub = per_wave >= 128 ? RTX_SUB_MAX
-                                    : (per_wave >= 8 ? 8u : (per_wave >= 4 ? 4u : (per_wave >= 2 ? 2u : 1u)));
-        }
+        if (sub == 0) p.sub = unit_samples(tiles, p.kn, WAVES, per_cu, cus);
         const uint64_t units = tiles * ((p.kn + p.sub - 1) / p.sub);
         uint64_t blocks = (uint64_t)per_cu * cus;
         if (blocks > (units + WAVES - 1) / WAVES) blocks = (units + WAVES - 1) / WAVES;  // no wave starts idle
@@ -471,6 +553,55 @@ hipError_t launch_items(Params p, bool use_lds, hipStream_t stream) {
                            (uint32_t)(k0 + p.kn >= spp));
         e = hipGetLastError();
         if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
+// The tiered walk of a sphere scene whose near and guarded layouts are both in
+// the LDS copy: per chunk the near pass (pn), the far pass over its queue (pf), the redo pass (pf
+// over the whole chunk; its waves return at once unless the queue overflowed), the reduction.
+template <bool COUNT, int WAVES, int MINW, bool CLK = false>
+hipError_t launch_tiered(Params pn, Params pf, hipStream_t stream) {
+    const auto kn = render_items<COUNT, true, false, false, WAVES, MINW, false, CLK, 1>;
+    const auto kf = render_items<COUNT, true, false, false, WAVES, MINW, false, CLK, 2>;
+    const auto kr = render_items<COUNT, true, false, false, WAVES, MINW, false, false, 0>;
+    const size_t sn = lds_fixed_bytes(pn.n_entries, 0, pn.n_materials, pn.n_textures);
+    const size_t sf = lds_fixed_bytes(pf.n_entries, 0, pf.n_materials, pf.n_textures);
+    constexpr int block = 64 * WAVES;
+    int cus = 0, per_n = 0, per_f = 0;
+    hipError_t e = resident_grid((const void*)kn, block, sn, &per_n, &cus);
+    if (e == hipSuccess) e = resident_grid((const void*)kf, block, sf, &per_f, &cus);
+    if (e != hipSuccess) return e;
+    const uint32_t spp = pn.cam.samples_per_pixel, chunk = pn.kn, sub = pn.sub;
+    const uint64_t tiles = (uint64_t)((pn.width + 7) / 8) * ((pn.rows + 7) / 8);
+    const uint64_t slots = tiles * 64;
+    Params pr = pf;  // the redo pass: the far layout over the chunk's units
+    pr.tier = 0;
+    pr.redo_only = 1;
+    pf.redo_only = 0;
+    for (uint32_t k0 = 0; k0 < spp; k0 += chunk) {
+        pn.k0 = pf.k0 = pr.k0 = k0;
+        pn.kn = pf.kn = pr.kn = spp - k0 < chunk ? spp - k0 : chunk;
+        pn.sub = sub ? sub : unit_samples(tiles, pn.kn, WAVES, per_n, cus);
+        pf.sub = pr.sub = pn.sub;
+        const uint64_t units = tiles * ((pn.kn + pn.sub - 1) / pn.sub);
+        uint64_t bn = (uint64_t)per_n * cus, br = (uint64_t)per_f * cus;
+        if (bn > (units + WAVES - 1) / WAVES) bn = (units + WAVES - 1) / WAVES;
+        if (br > (units + WAVES - 1) / WAVES) br = (units + WAVES - 1) / WAVES;
+        if (pn.debug_launch)
+            fprintf(stderr, "rtx tiered: waves/wg %d, wgs/CU %d / %d, grid %llu, sub %u, units %llu, lds %zu / %zu B, cap %u\n",
+                    WAVES, per_n, per_f, (unsigned long long)bn, pn.sub, (unsigned long long)units, sn, sf, pn.defer_cap);
+        // the unit queue head, and the chunk's record count + overflow flag (one u64 slot)
+        if ((e = hipMemsetAsync(pn.tile_counter, 0, sizeof(uint32_t), stream)) != hipSuccess) return e;
+        if ((e = hipMemsetAsync(pn.defer_count, 0, 2 * sizeof(uint32_t), stream)) != hipSuccess) return e;
+        hipLaunchKernelGGL(kn, dim3((uint32_t)bn), dim3(block), sn, stream, pn);
+        if ((e = hipMemsetAsync(pf.tile_counter, 0, sizeof(uint32_t), stream)) != hipSuccess) return e;
+        hipLaunchKernelGGL(kf, dim3((uint32_t)per_f * cus), dim3(block), sf, stream, pf);
+        if ((e = hipMemsetAsync(pr.tile_counter, 0, sizeof(uint32_t), stream)) != hipSuccess) return e;
+        hipLaunchKernelGGL(kr, dim3((uint32_t)br), dim3(block), sf, stream, pr);
+        hipLaunchKernelGGL(reduce_samples, dim3((uint32_t)((slots + 255) / 256)), dim3(256), 0, stream, pn,
+                           (uint32_t)(k0 + pn.kn >= spp));
+        if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     return hipSuccess;
 }
@@ -508,10 +639,19 @@ uint32_t scene_placement(const Params& p, uint32_t flags) {
     return p.n_hot > 0 && !p.has_noise ? RTX_SCENE_LDS_CACHE : RTX_SCENE_IN_HBM;
 }
 
-hipError_t launch_render(const Params& p, uint32_t flags, hipStream_t stream) {
+hipError_t launch_render(const Params& p, uint32_t flags, hipStream_t stream, const Params* far) {
     if (p.width == 0 || p.rows == 0) return hipSuccess;
     if (!p.scratch) return hipErrorInvalidValue;  // the caller sizes the sample scratch
     const bool count = (flags & RTX_FLAG_COUNTERS) != 0;
+    if (far) {  // the caller checked: spheres only, both layouts in the LDS copy, no noise
+        if (p.tier != 1 || far->tier != 2 || !p.defer || !far->defer || p.n_quads || p.has_noise ||
+            scene_placement(p, flags) != RTX_SCENE_IN_LDS || scene_placement(*far, flags) != RTX_SCENE_IN_LDS)
+            return hipErrorInvalidValue;
+        if (!count && (flags & RTX_FLAG_TIMING))  // diagnostics: the wave-cycle split of both passes
+            return launch_tiered<false, RTX_V3_WAVES, RTX_V3_MINW, true>(p, *far, stream);
+        return count ? launch_tiered<true, RTX_V3_WAVES, 0>(p, *far, stream)
+                     : launch_tiered<false, RTX_V3_WAVES, RTX_V3_MINW>(p, *far, stream);
+    }
     const bool use_lds = scene_placement(p, flags) == RTX_SCENE_IN_LDS;
     if (!count && (flags & RTX_FLAG_TIMING) && !p.has_noise && p.item_waves != 4)  // diagnostics: sphere scenes
         return p.n_quads ? launch_items<false, true, false, RTX_V3_WAVES, RTX_V3_MINW, true>(p, use_lds, stream)

@@ -17,6 +17,11 @@
 // set can then differ where the float32 sphere test reports hits outside a sphere's box
 // (DESIGN.md §12 measures where).
 //
+// NEAR (the tiered walk): the units are the spheres, each behind its own box grown
+// by the float32 sphere test's error bound for ray origins inside a NEAR REGION (near_region):
+// a hit the test reports from there lies inside that box, so such rays reach every sphere they
+// can hit.  Rays from outside the region walk the guarded tree instead (the kernel's far pass).
+//
 // Either tree is walked near child first along the camera's viewing direction: one threaded
 // layout per camera octant, made on first use.
 #pragma once
@@ -30,6 +35,8 @@ namespace rtxd {
 
 struct Topology {
     bool guarded = true;
+    bool near = false;     // unguarded units behind boxes grown for origins in near_box
+    float near_box[6] = {};  // min xyz, max xyz (near trees)
     uint32_t n_internal = 0;          // SAH nodes: nodes[0 .. n_internal)
     // nodes: the SAH nodes (children in canonical order: left = the low side of the split), then
     // (guarded) one copy of each unit's node with its sphere refs
@@ -47,7 +54,19 @@ struct Topology {
 // (rtx_layout.h, reference order).  Returns false (out untouched) when the tree does not qualify:
 // anything but spheres, a sphere outside a leaf node of one or two spheres (guarded), or fewer
 // than two units.
-bool build_topology(const std::vector<rtx_entry>& ref, bool guarded, Topology& out);
+// near_box (unguarded only): grow every sphere's box by sphere_margin for origins in that box.
+bool build_topology(const std::vector<rtx_entry>& ref, bool guarded, Topology& out, const float* near_box = nullptr);
+
+// The near region of a tiered walk: the box of the spheres that are not huge (precise_enough's
+// core) grown by a quarter of its largest extent on every side, min xyz then max xyz.  False when
+// the scene has no finite core.
+bool near_region(const std::vector<rtx_entry>& ref, float box[6]);
+
+// How far outside a sphere (centre c, radius r) the float32 sphere test can put a hit for a ray
+// origin at distance <= dmax from c: sqrt(r^2 + 2^-17 (dmax^2 + r^2)) - r, plus 2^-20 (dmax + r)
+// for the rounding of the slab test.  (The test's error in |P - c|^2 - r^2 is K eps (dmax^2 + r^2)
+// with K <= 9.5 measured over 4e7 near-tangent rays; 2^-17 = 128 eps.)
+double sphere_margin(double r, double dmax);
 
 // Whether the scene's spheres are small against the float32 sphere test's error (see the .hip):
 // the gate of the default (guarded) rebuild.

@@ -179,15 +179,10 @@ void build_sah(const std::vector<Box>& boxes, const std::vector<int32_t>& item_r
 
 }  // namespace
 
-// The float32 sphere test (hittables.go:96-116) forms c = |oc|^2 - r^2 from squares of order D^2
-// (D: the ray origin's distance to the centre), so it reports hits up to about eps D^2 / r outside a
-// sphere's silhouette.  Where such hits can reach past the innermost box, the order in which two
-// units are tried can decide which of two nearby spheres is the closest hit (DESIGN.md §12), so the
-// tree is rebuilt only where that zone is a small fraction of the spheres: eps D^2 / r_min^2 < 2^-7,
-// D the diagonal of the scene without its huge spheres (a sphere is huge when its radius exceeds the
-// extent of all smaller ones: main.go's ground, r = 1000).  randSpheres and the config-5 scene pass
-// (1.4e-3); config 4's 316-unit slab of r = 0.2 spheres fails (0.3).
-bool precise_enough(const std::vector<rtx_entry>& ref) {
+namespace {
+// The box of the spheres that are not huge (a sphere is huge when its radius exceeds the extent
+// of all smaller ones: main.go's ground, r = 1000), and the smallest radius.
+bool core_box(const std::vector<rtx_entry>& ref, Box& core, double& rmin) {
     std::vector<std::pair<float, uint32_t>> rad;  // (radius, entry), spheres only
     for (uint32_t i = 0; i < ref.size(); ++i)
         if (tag_of(ref[i]) >= 0) rad.push_back({std::fabs(ref[i].a[3]), i});
@@ -210,14 +205,50 @@ bool precise_enough(const std::vector<rtx_entry>& ref) {
         if (!(rad[keep - 1].first > ext)) break;
         --keep;
     }
-    const Box& b = pre[keep - 1];
+    core = pre[keep - 1];
+    rmin = rad[0].first;
+    return true;
+}
+}  // namespace
+
+// The float32 sphere test (hittables.go:96-116) forms c = |oc|^2 - r^2 from squares of order D^2
+// (D: the ray origin's distance to the centre), so it reports hits up to about eps D^2 / r outside a
+// sphere's silhouette.  Where such hits can reach past the innermost box, the order in which two
+// units are tried can decide which of two nearby spheres is the closest hit (DESIGN.md §12), so the
+// tree is rebuilt only where that zone is a small fraction of the spheres: eps D^2 / r_min^2 < 2^-7,
+// D the diagonal of the scene without its huge spheres (a sphere is huge when its radius exceeds the
+// extent of all smaller ones: main.go's ground, r = 1000).  randSpheres and the config-5 scene pass
+// (1.4e-3); config 4's 316-unit slab of r = 0.2 spheres fails (0.3).
+bool precise_enough(const std::vector<rtx_entry>& ref) {
+    Box b;
+    double rmin = 0.0;
+    if (!core_box(ref, b, rmin)) return false;
     double d2 = 0.0;
     for (int q = 0; q < 3; ++q) d2 += ((double)b.mx[q] - b.mn[q]) * ((double)b.mx[q] - b.mn[q]);
-    const double rmin = rad[0].first;
     return rmin > 0.0 && std::ldexp(d2, -24) / (rmin * rmin) < std::ldexp(1.0, -7);
 }
 
-bool build_topology(const std::vector<rtx_entry>& ref, bool guarded, Topology& out) {
+bool near_region(const std::vector<rtx_entry>& ref, float box[6]) {
+    Box b;
+    double rmin = 0.0;
+    if (!core_box(ref, b, rmin)) return false;
+    double ext = 0.0;
+    for (int q = 0; q < 3; ++q) ext = std::max(ext, (double)b.mx[q] - (double)b.mn[q]);
+    if (!std::isfinite(ext)) return false;
+    for (int q = 0; q < 3; ++q) {  // rounded outward: the region only grows
+        box[q] = std::nextafter((float)((double)b.mn[q] - 0.25 * ext), -INFINITY);
+        box[3 + q] = std::nextafter((float)((double)b.mx[q] + 0.25 * ext), INFINITY);
+        if (!std::isfinite(box[q]) || !std::isfinite(box[3 + q])) return false;
+    }
+    return true;
+}
+
+double sphere_margin(double r, double dmax) {
+    return std::sqrt(r * r + std::ldexp(dmax * dmax + r * r, -17)) - r + std::ldexp(dmax + r, -20);
+}
+
+bool build_topology(const std::vector<rtx_entry>& ref, bool guarded, Topology& out, const float* near_box) {
+    if (guarded && near_box) return false;
     // the units, in the reference's walk order: [first entry, end) of each
     std::vector<std::pair<uint32_t, uint32_t>> units;
     const uint32_t n = (uint32_t)ref.size();
@@ -243,6 +274,10 @@ bool build_topology(const std::vector<rtx_entry>& ref, bool guarded, Topology& o
     if (units.size() < 2) return false;
     Topology t;
     t.guarded = guarded;
+    if (near_box) {
+        t.near = true;
+        std::memcpy(t.near_box, near_box, sizeof(t.near_box));
+    }
     const uint32_t U = (uint32_t)units.size();
     t.n_internal = U - 1;
     std::vector<Box> boxes(U);
@@ -258,6 +293,20 @@ bool build_topology(const std::vector<rtx_entry>& ref, bool guarded, Topology& o
                 boxes[u].mx[k] = h.b[k];
             }
             item_ref[u] = (int32_t)(t.n_internal + u);
+        } else if (near_box) {  // the sphere's box grown by its margin for origins in the near region
+            const double r = std::fabs((double)h.a[3]);
+            double d2 = 0.0;  // farthest corner of the region from the centre
+            for (int k = 0; k < 3; ++k) {
+                const double lo = (double)near_box[k] - h.a[k], hi = (double)near_box[3 + k] - h.a[k];
+                d2 += std::max(lo * lo, hi * hi);
+            }
+            const double m = sphere_margin(r, std::sqrt(d2));
+            for (int k = 0; k < 3; ++k) {  // rounded outward
+                boxes[u].mn[k] = std::nextafter((float)((double)h.a[k] - r - m), -INFINITY);
+                boxes[u].mx[k] = std::nextafter((float)((double)h.a[k] + r + m), INFINITY);
+                if (!std::isfinite(boxes[u].mn[k]) || !std::isfinite(boxes[u].mx[k])) return false;
+            }
+            item_ref[u] = RTX_REF_PRIM(RTX_PRIM_SPHERE, word(&h.b[1]));
         } else {  // the sphere's box: NewSphere's NewAabb(center - r, center + r), hittables.go:85-94
             for (int k = 0; k < 3; ++k) {
                 const float p1 = h.a[k] + (h.a[3] * -1.0f), p2 = h.a[k] + h.a[3];

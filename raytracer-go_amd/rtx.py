@@ -31,7 +31,10 @@ RTX_FLAG_NO_LDS = 4
 RTX_FLAG_TIMING = 1 << 20  # diagnostics: timed kernel + wave-cycle split
 RTX_SCENE_REFERENCE_BVH = 1  # rtx_scene_create_ex: keep the caller's tree and the reference's visit order
 RTX_SCENE_EVERY_BOX = 2  # rtx_scene_create_ex: the walk leaves no box test out (ABI 7, rtx_collapse.h)
+RTX_SCENE_NO_TIER = 4  # rtx_scene_create_ex: no tiered walk (ABI 8)
 RTX_LAYOUT_REFERENCE = 8  # Stats.walk_layout of a scene walking the caller's tree
+RTX_LAYOUT_TIERED = 16  # Stats.walk_layout bit: the render walked in two tiers (ABI 8)
+RTX_TREE_NEAR = 0x100  # rtx_scene_topology / rtx_walk_tree octant bit: the near tree (ABI 8)
 RTX_GATHER_NONE, RTX_GATHER_RCCL, RTX_GATHER_DEVICE, RTX_GATHER_HOST = 0, 1, 2, 3  # Stats.gather_kind
 RTX_SCENE_IN_HBM, RTX_SCENE_IN_LDS, RTX_SCENE_LDS_CACHE = 0, 1, 2  # Stats.scene_placement
 RTX_IMAGE_TEXEL_WORDS = 2  # RGBA16 image texels: two uint32 words each (rtx.h)
@@ -106,7 +109,8 @@ class Stats(ctypes.Structure):
                 ("shade_lanes", c_uint64), ("trav_cycles", c_uint64), ("shade_cycles", c_uint64),
                 ("idle_lanes", c_uint64), ("cache_hits", c_uint64), ("sample_chunks", c_uint64),
                 ("parked_lanes", c_uint64), ("deferred_lanes", c_uint64), ("shade_split_cycles", c_uint64 * 4),
-                ("walk_layout", c_uint64), ("gather_kind", c_uint64), ("scene_placement", c_uint64)]
+                ("walk_layout", c_uint64), ("gather_kind", c_uint64), ("scene_placement", c_uint64),
+                ("deferred_paths", c_uint64), ("redo_chunks", c_uint64)]
 
     def as_dict(self) -> dict:
         return {name: (list(v) if not isinstance(v := getattr(self, name), (int, float)) else v)
@@ -119,6 +123,7 @@ RTX_SYMBOLS = [
     "rtx_ppm_max_bytes", "rtx_encode_ppm_device", "rtx_render_ppm", "rtx_scene_create_spheres", "rtx_scene_export",
     "rtx_release_device_memory", "rtx_device_scratch_bytes", "rtx_scene_create_ex", "rtx_scene_topology",
     "rtx_camera_octant", "rtx_walk_tree", "rtx_render_ex", "rtx_scene_walk_skip", "rtx_walk_skip",
+    "rtx_scene_near_region", "rtx_scene_near_skip", "rtx_walk_near_region",
 ]
 RTXHOST_SYMBOLS = [
     "rtxhost_build_scene", "rtxhost_scene_free", "rtxhost_scene_desc", "rtxhost_scene_camera",
@@ -168,6 +173,13 @@ def load() -> ctypes.CDLL:
     L.rtx_scene_walk_skip.restype = c_int
     L.rtx_walk_skip.argtypes = [POINTER(SceneDesc), c_uint32, POINTER(Camera), c_void_p, c_uint32, POINTER(c_uint32)]
     L.rtx_walk_skip.restype = c_int
+    L.rtx_scene_near_region.argtypes = [c_void_p, POINTER(Camera), POINTER(c_float), POINTER(c_uint32)]
+    L.rtx_scene_near_region.restype = c_int
+    L.rtx_scene_near_skip.argtypes = [c_void_p, POINTER(Camera), c_void_p, c_uint32, POINTER(c_uint32)]
+    L.rtx_scene_near_skip.restype = c_int
+    L.rtx_walk_near_region.argtypes = [POINTER(SceneDesc), c_uint32, POINTER(Camera), POINTER(c_float),
+                                       POINTER(c_uint32)]
+    L.rtx_walk_near_region.restype = c_int
     L.rtx_camera_octant.argtypes = [POINTER(Camera)]
     L.rtx_camera_octant.restype = c_uint32
     L.rtx_scene_destroy.argtypes = [c_void_p]
@@ -300,14 +312,16 @@ class HostScene:
 class DeviceScene:
     """rtx_scene_create: the tables uploaded once to the current HIP device."""
 
-    def __init__(self, desc_ptr=None, handle=None, reference_bvh: bool = False, every_box: bool = False):
+    def __init__(self, desc_ptr=None, handle=None, reference_bvh: bool = False, every_box: bool = False,
+                 no_tier: bool = False):
         L = load()
         self.build_ms = None
         if handle is not None:
             self._h = handle
             return
         h = c_void_p()
-        flags = (RTX_SCENE_REFERENCE_BVH if reference_bvh else 0) | (RTX_SCENE_EVERY_BOX if every_box else 0)
+        flags = ((RTX_SCENE_REFERENCE_BVH if reference_bvh else 0) | (RTX_SCENE_EVERY_BOX if every_box else 0) |
+                 (RTX_SCENE_NO_TIER if no_tier else 0))
         check(L.rtx_scene_create_ex(desc_ptr, flags, ctypes.byref(h)), "rtx_scene_create_ex")
         self._h = h
 
@@ -362,6 +376,28 @@ class DeviceScene:
             return desc_ptr
         arr, n, root = t
         return desc_with_tree(desc_ptr, arr, n, root)
+
+    def near_region(self, cam: Camera):
+        """(box (6 floats: min xyz, max xyz) or None, active) — rtx_scene_near_region."""
+        box, act = (c_float * 6)(), c_uint32()
+        for i in range(6):
+            box[i] = float("nan")
+        check(load().rtx_scene_near_region(self._h, ctypes.byref(cam), box, ctypes.byref(act)), "rtx_scene_near_region")
+        vals = [float(v) for v in box]
+        return (None if vals[0] != vals[0] else vals), bool(act.value)
+
+    def near_desc(self, desc_ptr, cam: Camera):
+        """The description of the near tree the scene walks for cam (rtx_scene_topology octant | RTX_TREE_NEAR)."""
+        t = self.topology(camera_octant(cam) | RTX_TREE_NEAR)
+        if t is None:
+            return None
+        arr, n, root = t
+        return desc_with_tree(desc_ptr, arr, n, root)
+
+    def near_skip(self, cam: Camera):
+        """rtx_scene_near_skip: the near walk's skips for cam (numpy uint8)."""
+        return _skip_mask(lambda buf, cap, n: load().rtx_scene_near_skip(self._h, ctypes.byref(cam), buf, cap, n),
+                          "rtx_scene_near_skip")
 
     def walk_skip(self, cam: Camera):
         """rtx_scene_walk_skip: per node entry of the uncollapsed walk for cam (visit order), 1 where
@@ -460,6 +496,30 @@ def desc_with_tree(desc_ptr, arr, n: int, root: int):
     p = ctypes.pointer(w)
     p._keep = (arr, roots, desc_ptr)  # the arrays live as long as the pointer
     return p
+
+
+def walk_near_region(desc_ptr, cam: Camera, flags: int = 0):
+    """rtx_walk_near_region (host only): (box or None, active)."""
+    box, act = (c_float * 6)(), c_uint32()
+    for i in range(6):
+        box[i] = float("nan")
+    check(load().rtx_walk_near_region(desc_ptr, flags, ctypes.byref(cam), box, ctypes.byref(act)),
+          "rtx_walk_near_region")
+    vals = [float(v) for v in box]
+    return (None if vals[0] != vals[0] else vals), bool(act.value)
+
+
+def walk_near_desc(desc_ptr, cam: Camera, flags: int = 0):
+    """rtx_walk_tree (host only) of the near tree for cam's octant, or None."""
+    L = load()
+    n, root = c_uint32(), c_int32()
+    oc = camera_octant(cam) | RTX_TREE_NEAR
+    check(L.rtx_walk_tree(desc_ptr, flags, oc, None, 0, ctypes.byref(n), ctypes.byref(root)), "rtx_walk_tree")
+    if n.value == 0 and root.value == -1:
+        return None
+    arr = (BvhNode * max(n.value, 1))()
+    check(L.rtx_walk_tree(desc_ptr, flags, oc, arr, n.value, ctypes.byref(n), ctypes.byref(root)), "rtx_walk_tree")
+    return desc_with_tree(desc_ptr, arr, int(n.value), int(root.value))
 
 
 def walk_tree_desc(desc_ptr, cam: Camera, flags: int = 0):

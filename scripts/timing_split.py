@@ -21,11 +21,12 @@ ap.add_argument("--scene", default="random_spheres")
 ap.add_argument("--width", type=int, default=1920)
 ap.add_argument("--spp", type=int, default=100)
 ap.add_argument("--reps", type=int, default=3)
+ap.add_argument("--no-tier", action="store_true", help="the guarded walk alone (RTX_SCENE_NO_TIER)")
 a = ap.parse_args()
 torch.cuda.set_device(0)
 s = rtx.HostScene(a.scene, 1)
 cam = s.camera(width=a.width, spp=a.spp)
-dev = rtx.DeviceScene(s.desc)
+dev = rtx.DeviceScene(s.desc, no_tier=a.no_tier)
 reg = rtx.Region(0, 0, cam.image_width, cam.image_height, 0, 1)
 out = torch.empty((cam.image_height, cam.image_width, 3), dtype=torch.float32, device="cuda")
 st = torch.cuda.current_stream().cuda_stream
@@ -42,7 +43,9 @@ def run(flags):
 plain = run(0)
 t = run(rtx.RTX_FLAG_TIMING)
 cyc = t.trav_cycles + t.shade_cycles
-res = {"scene": a.scene, "width": a.width, "spp": a.spp, "timed_ms": round(plain.kernel_ms, 3),
+res = {"scene": a.scene, "width": a.width, "spp": a.spp, "walk_layout": plain.walk_layout,
+       "timed_ms": round(plain.kernel_ms, 3), "wave_gcycles": {"walk": round(t.trav_cycles / 1e9, 3),
+       "shade": round(t.shade_cycles / 1e9, 3), "split": [round(v / 1e9, 3) for v in t.shade_split_cycles]},
        "timing_variant_ms": round(t.kernel_ms, 3),
        "walk_share": round(t.trav_cycles / cyc, 4), "shade_share": round(t.shade_cycles / cyc, 4),
        "split": {k: round(v / cyc, 4) for k, v in zip(("scatter", "shade", "claim_camera", "begin"), t.shade_split_cycles)}}

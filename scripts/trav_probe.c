@@ -119,6 +119,7 @@ static int sah_leaf = 1;
 static int guard = 0;
 static int32_t* GUARD_OF; /* guard 3: sphere -> its reference leaf node */
 static float INFL = 0.02f;
+static int FAR; static float RN = 1e30f; static uint64_t n_far;
 static float c_isect = 1.5f;
 
 static aabb_t prim_box(const rtx_scene_desc* s, int32_t ref) {
@@ -199,7 +200,8 @@ static void sah_walk(const rtx_scene_desc* s, int ni, const ray_t* r, float* clo
         for (int i = n->first; i < n->first + n->count; ++i) {
             int32_t pr[2] = {SP[i], SP[i]};
             int np = 1;
-            if (guard == 3) {  /* the sphere's reference leaf box, then the sphere */
+            if (guard == 4) { /* own inflated box only */ }
+            else if (guard == 3) {  /* the sphere's reference leaf box, then the sphere */
                 const rtx_bvh_node* gb = &s->nodes[GUARD_OF[(~SP[i]) & 0x0FFFFFFF]];
                 p->box++;
                 if (!aabb_hit(gb, r, 0.001f, *closest)) continue;
@@ -261,7 +263,7 @@ static void sah_probe(const rtx_scene_desc* s, const ray_t* r, float t_ref) {
 /* guard: 1: the SAH units are the reference tree's leaves (nodes of 1-2 primitives), with their boxes */
 static void sah_setup(const rtx_scene_desc* s) {
     int n = (int)s->n_spheres;
-    if (guard == 3) {  /* single spheres, navigation boxes = own boxes inflated by INFL */
+    if (guard == 3 || guard == 4) {  /* single spheres, navigation boxes = own boxes inflated by INFL (4: no leaf check) */
         GUARD_OF = malloc(n * 4);
         for (uint32_t i = 0; i < s->n_nodes; ++i) {
             const rtx_bvh_node* b = &s->nodes[i];
@@ -313,6 +315,12 @@ static void probe_segment(const ctx_t* cx, const ray_t* r, int hit_any, const hi
         far_hist[b]++;
     }
     float t_ref = hit_any ? h->t : INFINITY;
+    {
+        float o[3] = {r->origin.x, r->origin.y, r->origin.z}, dm = 0;
+        for (int k = 0; k < 3; ++k) { float e = o[k] < CORE_MN[k] ? CORE_MN[k] - o[k] : (o[k] > CORE_MX[k] ? o[k] - CORE_MX[k] : 0); if (e > dm) dm = e; }
+        FAR = dm > RN;
+        if (FAR) { n_far++; return; }
+    }
     for (int m = 0; m < 2; ++m) {
         probe_t* p = m ? &P_dist : &P_oct;
         float closest = INFINITY;
@@ -327,8 +335,11 @@ static void probe_segment(const ctx_t* cx, const ray_t* r, int hit_any, const hi
     sah_probe(s, r, t_ref);
 }
 
+static uint64_t n_far_paths, n_paths, n_far_before;
 static vec3 probe_color(const ctx_t* cx, ray_t r, rng_t* rng, int depth) {
     vec3 thr = v3(1.0f, 1.0f, 1.0f), acc = v3(0.0f, 0.0f, 0.0f);
+    n_paths++; n_far_before = n_far;
+    struct F { uint64_t* a; uint64_t b; } fin = {&n_far_paths, 0}; (void)fin;
     for (; depth > 0; --depth) {
         hit_t h;
         cx->c->segments++;
@@ -338,6 +349,7 @@ static vec3 probe_color(const ctx_t* cx, ray_t r, rng_t* rng, int depth) {
         probe_ref_prim += cx->c->prim_tests - pt;
         segs++;
         probe_segment(cx, &r, hit_any, &h);
+        if (n_far_before != (uint64_t)-1 && n_far != n_far_before) { n_far_paths++; n_far_before = (uint64_t)-1; }
         if (!hit_any) return acc;
         int has_emit;
         vec3 emit = material_emit(cx, &h, &has_emit);
@@ -363,6 +375,7 @@ int main(int argc, char** argv) {
     rtx_camera cam;
     if (getenv("GUARD")) guard = atoi(getenv("GUARD"));
     if (getenv("INFL")) INFL = atof(getenv("INFL"));
+    if (getenv("RN")) RN = atof(getenv("RN"));
     if (getenv("LEAF")) sah_leaf = atoi(getenv("LEAF"));
     if (getenv("CI")) c_isect = atof(getenv("CI"));
     sah_setup(s);
@@ -392,6 +405,9 @@ int main(int argc, char** argv) {
     printf("  origin outside the core box by <=0/5/10/20/40/80/160/more:");
     for (int q = 0; q < 8; ++q) printf(" %.2e", (double)far_hist[q] / segs);
     printf("\n");
+    printf("  far segments (origin > RN outside the core box): %.4f\n", (double)n_far / segs);
+    segs -= n_far;
+    printf("  paths with a far segment: %.4f of %llu\n", (double)n_far_paths / n_paths, (unsigned long long)n_paths);
     printf("  sah : box %.2f prim %.2f per segment, t mismatches %llu (%d nodes, leaf <= %d)\n", (double)P_sah.box / segs,
            (double)P_sah.prim / segs, (unsigned long long)P_sah.mism_t, n_sn, sah_leaf);
     printf("  saho: box %.2f prim %.2f per segment, t mismatches %llu\n", (double)P_saho.box / segs,

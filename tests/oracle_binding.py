@@ -89,6 +89,8 @@ def load():
     L.oracle_ycbcr_texels.restype = c_int
     L.oracle_node_hooks.argtypes = [c_void_p, c_void_p, c_void_p]
     L.oracle_node_hooks.restype = None
+    L.oracle_tier.argtypes = [c_void_p, c_void_p, c_void_p]
+    L.oracle_tier.restype = None
     _lib = L
     return L
 
@@ -133,10 +135,21 @@ def region_rows(reg: rtx.Region) -> int:
 
 
 def render(desc_ptr, cam: rtx.Camera, seed: int, region: rtx.Region, order: int = ORDER_REFERENCE,
-           threads: int = 0, skip=None):
+           threads: int = 0, skip=None, tier=None):
     """Oracle render of a region -> (float32 array [rows, width, 3], counters dict).  skip: per node
-    of desc_ptr's table, 1 = leave its box test out (a collapsed walk, rtx.node_skip)."""
+    of desc_ptr's table, 1 = leave its box test out (a collapsed walk, rtx.node_skip).  tier: (near
+    box, far description, far skip or None): the tiered walk (oracle_tier), desc_ptr being the near
+    tree."""
     L = load()
+    if tier is not None:
+        box, far, fsk = tier
+        boxa = (c_float * 6)(*box)
+        fska = None if fsk is None else np.ascontiguousarray(fsk, np.uint8)
+        L.oracle_tier(boxa, ctypes.cast(far, c_void_p), None if fska is None else fska.ctypes.data_as(c_void_p))
+        try:
+            return render(desc_ptr, cam, seed, region, order, threads, skip)
+        finally:
+            L.oracle_tier(None, None, None)
     if threads <= 0:
         threads = min(16, os.cpu_count() or 1)
     rows = region_rows(region)

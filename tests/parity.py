@@ -16,6 +16,10 @@ and holds both to the oracle (oracle/oracle.c):
      and draws — the tree changes the work, not a single path;
   3. within the north-star bar, |delta| <= 1e-4 per channel, of the oracle in the reference's
      own (recursive) colour order on the caller's tree.
+A render that walks in two tiers (rtx_stats.walk_layout & RTX_LAYOUT_TIERED) is
+held to the oracle's tiered walk (oracle_tier): the near tree with its skips for segments that
+start in the near region, the guarded tree with its skips for the others; check 2 then holds
+that walk to the caller's tree as well.
 """
 from __future__ import annotations
 
@@ -50,10 +54,21 @@ def walk_of(dev, desc, cam):
     return walk, rtx.node_skip(walk, dev.walk_skip(cam))
 
 
-def oracle_checks(desc, walk, cam, seed, reg, skip=None):
+def tier_of(dev, desc, cam):
+    """(near tree description, its skips, (near box, guarded tree, its skips)) of a scene that walks
+    in two tiers for cam, or None."""
+    box, active = dev.near_region(cam)
+    if not active:
+        return None
+    near = dev.near_desc(desc, cam)
+    far, fskip = walk_of(dev, desc, cam)
+    return near, rtx.node_skip(near, dev.near_skip(cam)), (box, far, fskip)
+
+
+def oracle_checks(desc, walk, cam, seed, reg, skip=None, tier=None):
     """(iterative image on the walked tree with its skips, its counters, reference-order image on
     the caller's tree); asserts check 2 and the collapsed walk's own check."""
-    it, cnt = ob.render(walk, cam, seed, reg, ob.ORDER_ITERATIVE, skip=skip)
+    it, cnt = ob.render(walk, cam, seed, reg, ob.ORDER_ITERATIVE, skip=skip, tier=tier)
     if walk is not desc or (skip is not None and skip.any()):
         it0, cnt0 = ob.render(desc, cam, seed, reg, ob.ORDER_ITERATIVE)
         assert np.array_equal(it, it0), f"walked tree changes the image: max {np.abs(it - it0).max()}"
@@ -66,8 +81,12 @@ def oracle_checks(desc, walk, cam, seed, reg, skip=None):
 
 def check_scene(torch, dev, desc, cam, seed, reg, flags=0, kernels=("timed", "counting")):
     """Checks 1-3 for both kernels on one region; returns (timed image, counting stats, oracle counters)."""
-    walk, skip = walk_of(dev, desc, cam)
-    it, cnt, ref = oracle_checks(desc, walk, cam, seed, reg, skip)
+    tier = tier_of(dev, desc, cam) if not flags & rtx.RTX_FLAG_NO_LDS else None
+    if tier is not None:
+        walk, skip, tw = tier
+    else:
+        (walk, skip), tw = walk_of(dev, desc, cam), None
+    it, cnt, ref = oracle_checks(desc, walk, cam, seed, reg, skip, tw)
     img = st = None
     for k in kernels:
         gpu, s = gpu_region(torch, dev, cam, seed, reg, counters=(k == "counting"), flags=flags)
@@ -76,7 +95,10 @@ def check_scene(torch, dev, desc, cam, seed, reg, flags=0, kernels=("timed", "co
         d = float(np.abs(gpu - ref).max()) if gpu.size else 0.0
         assert d <= TOL, f"{k} kernel: max |delta| = {d} > {TOL} vs the reference-order oracle"
         want = rtx.camera_octant(cam) if walk is not desc else rtx.RTX_LAYOUT_REFERENCE
+        if tier is not None:
+            want |= rtx.RTX_LAYOUT_TIERED
         assert s.walk_layout == want, (k, s.walk_layout, want)
+        assert s.redo_chunks == 0, (k, s.redo_chunks)
         if k == "counting":
             assert_counters_equal(s, cnt)
             st = s

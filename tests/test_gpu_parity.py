@@ -327,21 +327,25 @@ def test_config_full_frame_windows(torch_cuda, built, name):
 REBUILT_FRAMES = [("random_spheres", 1920, 500, 0), ("random_spheres", 1920, 2000, 0), ("earth_dielectric", 3840, 1000, 4)]
 
 
+@pytest.mark.parametrize("tiered", [True, False])
 @pytest.mark.parametrize("scene,width,spp,allowed", REBUILT_FRAMES)
-def test_rebuilt_tree_full_frame(torch_cuda, built, scene, width, spp, allowed):
-    """The library's rebuilt tree (rtx_topology.h) against the caller's (RTX_SCENE_REFERENCE_BVH) on
-    whole BASELINE frames (C2, C3 on one GPU, C5) from the timed kernel: bit-identical, but for at
-    most `allowed` pixels, each far inside the north-star bar."""
+def test_rebuilt_tree_full_frame(torch_cuda, built, scene, width, spp, allowed, tiered):
+    """The library's rebuilt trees (rtx_topology.h) — the tiered walk (near tree + guarded tree,
+    DESIGN.md §14) and the guarded tree alone (RTX_SCENE_NO_TIER) — against the caller's
+    (RTX_SCENE_REFERENCE_BVH) on whole BASELINE frames (C2, C3 on one GPU, C5) from the timed
+    kernel: bit-identical, but for at most `allowed` pixels, each far inside the north-star bar."""
     s = rtx.HostScene(scene, 1)
     cam = s.camera(width=width, spp=spp)
-    fast = rtx.DeviceScene(s.desc)
+    fast = rtx.DeviceScene(s.desc, no_tier=not tiered)
     assert fast.topology(rtx.camera_octant(cam)) is not None  # this scene is walked over the rebuilt tree
     reg = rtx.Region(0, 0, cam.image_width, cam.image_height, 0, 1)
     a, sa = gpu_region(torch_cuda, fast, cam, 2024, reg, counters=False)
     del fast
     ref = rtx.DeviceScene(s.desc, reference_bvh=True)
     b, sb = gpu_region(torch_cuda, ref, cam, 2024, reg, counters=False)
-    assert sa.walk_layout == rtx.camera_octant(cam) and sb.walk_layout == rtx.RTX_LAYOUT_REFERENCE
+    want = rtx.camera_octant(cam) | (rtx.RTX_LAYOUT_TIERED if tiered else 0)
+    assert sa.walk_layout == want and sb.walk_layout == rtx.RTX_LAYOUT_REFERENCE
+    assert sa.redo_chunks == 0 and (sa.deferred_paths > 0) == tiered
     diff = np.argwhere((a != b).any(axis=2))
     assert len(diff) <= allowed, (len(diff), diff[:8].tolist(), float(np.abs(a - b).max()))
     assert float(np.abs(a - b).max()) <= 1e-6
@@ -383,7 +387,7 @@ def test_every_camera_octant(torch_cuda, spheres, dev_spheres, octant):
     assert rtx.camera_octant(cam) == octant
     reg = rtx.Region(0, 0, cam.image_width, cam.image_height, 0, 1)
     _, st, _ = check_scene(torch_cuda, dev_spheres, spheres.desc, cam, 3 + octant, reg)
-    assert st.walk_layout == octant
+    assert st.walk_layout & ~rtx.RTX_LAYOUT_TIERED == octant
 
 
 @pytest.mark.parametrize("name,stride", [("C2", 36), ("C4", 36)])
@@ -402,3 +406,29 @@ def test_config_rows_vs_oracle(torch_cuda, built, name, stride):
     want = gpu[rows.rank::stride]
     bad = np.argwhere((want != it).any(axis=2))
     assert len(bad) == 0, (len(bad), bad[:8].tolist(), float(np.abs(want - it).max()))
+
+
+@pytest.mark.parametrize("cap", [0, 64])
+def test_tier_queue_overflow_redo(torch_cuda, spheres, dev_spheres, monkeypatch, cap):
+    """The tiered walk's queue of deferred paths too small for the chunk
+    (RTX_DEFER_CAP): the redo pass renders the chunk again, whole, on the guarded tree — the same
+    image, bit for bit, as the oracle on the caller's tree and as the render with room."""
+    cam = spheres.camera(width=160, spp=12, depth=50)
+    reg = rtx.Region(0, 0, cam.image_width, cam.image_height, 0, 1)
+    want, _ = gpu_region(torch_cuda, dev_spheres, cam, 21, reg, counters=False)
+    it, _ = ob.render(spheres.desc, cam, 21, reg, ob.ORDER_ITERATIVE)
+    assert np.array_equal(want, it)
+    monkeypatch.setenv("RTX_DEFER_CAP", str(cap))
+    got, st = gpu_region(torch_cuda, dev_spheres, cam, 21, reg, counters=False)
+    assert st.walk_layout & rtx.RTX_LAYOUT_TIERED and st.redo_chunks == 1 and st.deferred_paths <= cap
+    assert np.array_equal(got, want)
+
+
+def test_tier_deferred_paths_c2_crop(torch_cuda, spheres, dev_spheres):
+    """The counting kernel's deferred paths on a C2 window: some paths leave the near region (the
+    ground's far side, paths trapped in the ground sphere), a few percent of them."""
+    cam = spheres.camera(width=1920, spp=64, depth=50)
+    reg = rtx.Region(900, 600, 96, 64, 0, 1)
+    _, st, _ = check_scene(torch_cuda, dev_spheres, spheres.desc, cam, 5, reg)
+    assert st.walk_layout & rtx.RTX_LAYOUT_TIERED
+    assert 0 < st.deferred_paths < 0.2 * st.samples, (st.deferred_paths, st.samples)

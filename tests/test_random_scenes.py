@@ -165,8 +165,11 @@ def test_random_scene_bitexact(built, seed, n_spheres, n_quads, axis_aligned):
     pd = ctypes.pointer(d)
     dev = rtx.DeviceScene(pd)
     walk, skip = parity.walk_of(dev, pd, cam)  # the tree the scene walks (sphere-only trees may be rebuilt)
+    tier = parity.tier_of(dev, pd, cam)  # ... and walk in two tiers
+    if tier is not None:
+        walk, skip, tier = tier
     reg = rtx.Region(0, 0, cam.image_width, cam.image_height, 0, 1)
-    it, cnt = ob.render(walk, cam, seed, reg, ob.ORDER_ITERATIVE, skip=skip)
+    it, cnt = ob.render(walk, cam, seed, reg, ob.ORDER_ITERATIVE, skip=skip, tier=tier)
     if walk is not pd:  # the rebuilt tree: same image and paths as the caller's tree on the oracle
         it0, cnt0 = ob.render(pd, cam, seed, reg, ob.ORDER_ITERATIVE)
         assert np.array_equal(it, it0, equal_nan=True)

@@ -1,0 +1,224 @@
+"""The tiered walk on the CPU: rtx_walk_near_region / rtx_walk_tree(octant |
+RTX_TREE_NEAR) build it without a device.
+
+A tiered scene walks every segment that starts in the NEAR REGION on the near tree: the spheres
+themselves as leaves, each behind its own box grown by the float32 sphere test's error bound for
+origins in that region; a path whose segment starts outside it walks the guarded tree (the
+reference's leaves) to its end.  These tests pin the region, the near tree's shape and margins, the
+soundness claim the walk rests on — from any origin in the region, a hit the float32 sphere test
+(hittables.go:96-116) reports lies where every box above its sphere passes (InBoundary,
+bvh.go:84-102, with the bound just past the hit) — and, on the oracle, that the tiered walk changes no
+path: image, segments, hits and draws equal the reference tree's, bit for bit.
+"""
+import ctypes
+import math
+
+import numpy as np
+import pytest
+
+import oracle_binding as ob
+import rtx
+
+F = np.float32
+
+
+def near_tree(desc, cam, flags=0):
+    L = rtx.load()
+    n, root = ctypes.c_uint32(), ctypes.c_int32()
+    oc = rtx.camera_octant(cam) | rtx.RTX_TREE_NEAR
+    rtx.check(L.rtx_walk_tree(desc, flags, oc, None, 0, ctypes.byref(n), ctypes.byref(root)), "rtx_walk_tree")
+    if n.value == 0:
+        return None, root.value
+    arr = (rtx.BvhNode * n.value)()
+    rtx.check(L.rtx_walk_tree(desc, flags, oc, arr, n.value, ctypes.byref(n), ctypes.byref(root)), "rtx_walk_tree")
+    return arr, root.value
+
+
+def sphere_index(ref):
+    p = (~ref) & 0xFFFFFFFF
+    assert p >> 28 == rtx.RTX_PRIM_SPHERE
+    return p & 0x0FFFFFFF
+
+
+def margin(r, dmax):
+    """rtx_topology.h sphere_margin, restated: sqrt(r^2 + 2^-17 (dmax^2 + r^2)) - r + 2^-20 (dmax + r)."""
+    return math.sqrt(r * r + math.ldexp(dmax * dmax + r * r, -17)) - r + math.ldexp(dmax + r, -20)
+
+
+def spheres_of(desc):
+    d = desc.contents
+    c = np.array([list(d.spheres[i].center) for i in range(d.n_spheres)], np.float32)
+    r = np.array([d.spheres[i].radius for i in range(d.n_spheres)], np.float32)
+    return c, r
+
+
+@pytest.mark.parametrize("scene", ["random_spheres", "earth_dielectric"])
+def test_near_region(built, scene):
+    """The region holds every non-huge sphere and the camera's defocus disk, and is the core box grown
+    by a quarter of its largest extent; renders with the main.go camera qualify."""
+    s = rtx.HostScene(scene, 1)
+    cam = s.camera(width=96, spp=2)
+    box, active = rtx.walk_near_region(s.desc, cam)
+    assert box is not None and active
+    lo, hi = np.array(box[:3]), np.array(box[3:])
+    c, r = spheres_of(s.desc)
+    small = np.abs(r) < 10  # all but the r = 1000 ground
+    core_lo = (c[small] - np.abs(r[small])[:, None]).min(0)
+    core_hi = (c[small] + np.abs(r[small])[:, None]).max(0)
+    ext = (core_hi - core_lo).max()
+    assert np.allclose(lo, core_lo - 0.25 * ext, atol=1e-5) and np.allclose(hi, core_hi + 0.25 * ext, atol=1e-5)
+    assert (np.array(list(cam.center)) > lo).all() and (np.array(list(cam.center)) < hi).all()
+
+
+@pytest.mark.parametrize("scene,flags", [("random_spheres", rtx.RTX_SCENE_NO_TIER),
+                                         ("random_spheres", rtx.RTX_SCENE_REFERENCE_BVH),
+                                         ("cornell_box", 0), ("stress_100k", 0), ("perlin_demo", 0)])
+def test_no_near_tree(built, scene, flags):
+    """No tiers with RTX_SCENE_NO_TIER or the caller's tree, for quads, or where the guarded rebuild's
+    precision gate fails (config 4); a Perlin scene has a near tree but does not qualify."""
+    s = rtx.HostScene(scene, 1)
+    cam = s.camera(width=64, spp=1)
+    box, active = rtx.walk_near_region(s.desc, cam, flags)
+    assert not active
+    if scene != "perlin_demo":
+        assert box is None and near_tree(s.desc, cam, flags)[0] is None
+
+
+@pytest.mark.parametrize("scene", ["random_spheres", "earth_dielectric"])
+def test_near_tree_shape(built, scene):
+    """Every sphere is a leaf exactly once; every box contains its children's; the box just above a
+    sphere contains the sphere's box grown by its margin for the farthest corner of the region."""
+    s = rtx.HostScene(scene, 1)
+    cam = s.camera(width=96, spp=2)
+    box, _ = rtx.walk_near_region(s.desc, cam)
+    arr, root = near_tree(s.desc, cam)
+    assert arr is not None and root == 0
+    c, r = spheres_of(s.desc)
+    corners = np.array([[box[3 * ((m >> k) & 1) + k] for k in range(3)] for m in range(8)], np.float64)
+    seen_nodes, seen_sph = np.zeros(len(arr), np.int32), np.zeros(len(c), np.int32)
+    stack = [root]
+    while stack:
+        i = stack.pop()
+        seen_nodes[i] += 1
+        nd = arr[i]
+        for ch in (nd.left, nd.right):
+            if ch >= 0:
+                for k in range(3):
+                    assert nd.bmin[k] <= arr[ch].bmin[k] and nd.bmax[k] >= arr[ch].bmax[k]
+                stack.append(ch)
+                continue
+            j = sphere_index(ch)
+            seen_sph[j] += 1
+            rr = abs(float(r[j]))
+            dmax = float(np.sqrt(((corners - c[j].astype(np.float64)) ** 2).sum(1)).max())
+            m = margin(rr, dmax)
+            for k in range(3):
+                assert nd.bmin[k] <= float(c[j][k]) - rr - m and nd.bmax[k] >= float(c[j][k]) + rr + m
+    assert (seen_nodes == 1).all() and (seen_sph == 1).all()
+
+
+def sphere_t(o, d, c, r, tmin=F(0.001)):
+    """Sphere.Hit's root (hittables.go:96-116) in float32, left-associative, no FMA; NaN = no hit."""
+    oc = o - c
+    a = (d[:, 0] * d[:, 0] + d[:, 1] * d[:, 1]) + d[:, 2] * d[:, 2]
+    hb = (d[:, 0] * oc[:, 0] + d[:, 1] * oc[:, 1]) + d[:, 2] * oc[:, 2]
+    cc = ((oc[:, 0] * oc[:, 0] + oc[:, 1] * oc[:, 1]) + oc[:, 2] * oc[:, 2]) - r * r
+    disc = hb * hb - a * cc
+    ok = disc >= 0
+    sq = np.sqrt(np.where(ok, disc, F(0)).astype(np.float64)).astype(F)
+    t1 = (-hb - sq) / a
+    t2 = (-hb + sq) / a
+    t = np.where(t1 > tmin, t1, np.where(t2 > tmin, t2, F(np.nan)))
+    return np.where(ok, t, F(np.nan)).astype(F)
+
+
+def slab_pass(o, d, mn, mx, lo, hi):
+    """(*Aabb).Hit (bvh.go:52-61, InBoundary :84-102) in float32, elementwise."""
+    rmin, rmax = lo.copy(), hi.copy()
+    ok = np.ones(len(o), bool)
+    for k in range(3):
+        inv = F(1) / d[:, k]
+        t0 = (mn[:, k] - o[:, k]) * inv
+        t1 = (mx[:, k] - o[:, k]) * inv
+        sw = inv < 0
+        t0, t1 = np.where(sw, t1, t0), np.where(sw, t0, t1)
+        rmin = np.where(t0 > rmin, t0, rmin)
+        rmax = np.where(t1 < rmax, t1, rmax)
+        ok &= rmin < rmax
+    return ok
+
+
+def test_near_tree_reaches_every_reported_hit(built):
+    """From origins in the near region, every hit the float32 sphere test reports — on near-tangent
+    rays, where its error is largest — passes the slab test of every box above its sphere in the near
+    tree with the running bound just past the hit: the walk reaches it."""
+    s = rtx.HostScene("random_spheres", 1)
+    cam = s.camera(width=96, spp=2)
+    box, _ = rtx.walk_near_region(s.desc, cam)
+    arr, root = near_tree(s.desc, cam)
+    c, r = spheres_of(s.desc)
+    parent_box = {}  # sphere -> boxes of its ancestors
+    stack = [(root, [])]
+    while stack:
+        i, anc = stack.pop()
+        chain = anc + [i]
+        for ch in (arr[i].left, arr[i].right):
+            if ch >= 0:
+                stack.append((ch, chain))
+            else:
+                parent_box[sphere_index(ch)] = chain
+    rng = np.random.default_rng(7)
+    lo, hi = np.array(box[:3]), np.array(box[3:])
+    n_hits = 0
+    for trial in range(6):
+        N = 100_000
+        j = rng.integers(0, len(c), N)
+        if trial % 3 == 0:
+            j[:] = int(np.argmax(np.abs(r)))  # the ground sphere
+        o = rng.uniform(lo, hi, (N, 3)).astype(F)
+        cj, rj = c[j], np.abs(r[j])
+        # aim at a point of the sphere's silhouette as seen from o, offset by a relative 1e-6 .. 1e-2
+        u = (cj - o).astype(np.float64)
+        u /= np.linalg.norm(u, axis=1)[:, None]
+        w = rng.normal(size=(N, 3))
+        w -= (w * u).sum(1)[:, None] * u
+        w /= np.linalg.norm(w, axis=1)[:, None]
+        off = rj * (1 + rng.normal(scale=[1e-6, 1e-4, 1e-2][trial % 3], size=N))
+        d = ((cj.astype(np.float64) + w * off[:, None]) - o) * rng.uniform(0.1, 10, N)[:, None]
+        d = d.astype(F)
+        t = sphere_t(o, d, cj, rj.astype(F))
+        hit = ~np.isnan(t)
+        n_hits += int(hit.sum())
+        bound = np.nextafter(t[hit], F(np.inf))
+        oh, dh, jh = o[hit], d[hit], j[hit]
+        for sph in np.unique(jh):
+            sel = jh == sph
+            for node in parent_box[int(sph)]:
+                mn = np.tile(np.array(list(arr[node].bmin), F), (sel.sum(), 1))
+                mx = np.tile(np.array(list(arr[node].bmax), F), (sel.sum(), 1))
+                ok = slab_pass(oh[sel], dh[sel], mn, mx, np.full(sel.sum(), F(0.001)), bound[sel])
+                assert ok.all(), (int(sph), node, int((~ok).sum()))
+    assert n_hits > 100_000
+
+
+@pytest.mark.parametrize("scene,width,spp", [("random_spheres", 192, 4), ("earth_dielectric", 160, 3)])
+def test_tiered_oracle_equals_reference(built, scene, width, spp):
+    """The oracle's tiered walk (near tree for paths in the near region, the guarded tree from a path's
+    first segment outside it on) against the reference's tree: the same image bit for bit and the same
+    segments, hits, texel fetches and draws; fewer box and sphere tests."""
+    s = rtx.HostScene(scene, 1)
+    cam = s.camera(width=width, spp=spp)
+    box, active = rtx.walk_near_region(s.desc, cam)
+    assert active
+    near = rtx.walk_near_desc(s.desc, cam)
+    far = rtx.walk_tree_desc(s.desc, cam)
+    reg = rtx.Region(0, 0, cam.image_width, cam.image_height, 0, 1)
+    a, ca = ob.render(s.desc, cam, 2024, reg, ob.ORDER_ITERATIVE)
+    b, cb = ob.render(near, cam, 2024, reg, ob.ORDER_ITERATIVE, tier=(box, far, None))
+    assert np.array_equal(a, b)
+    for k in ("samples", "segments", "hits", "texel_fetches", "rng_draws"):
+        assert ca[k] == cb[k], k
+    assert cb["prim_tests"] < 0.7 * ca["prim_tests"] and cb["node_visits"] < 0.7 * ca["node_visits"]
+    # every segment in the near tree alone (no far tier): the same image here too
+    c, _ = ob.render(near, cam, 2024, reg, ob.ORDER_ITERATIVE)
+    assert np.array_equal(a, c)
