@@ -896,11 +896,12 @@ int enqueue_on(rtx_scene* s, DeviceCopy* c, const rtx_camera* cam, uint64_t seed
         p.prim_batch = env_knob("RTX_PRIM_BATCH", 16, 1, 65);  // 65: primitive tests only when no node is left
         if (tier) {
             // The queue of deferred paths, per device: an eighth of the chunk's items (measured:
-            // 3.2 % of randSpheres' paths leave the near region), at most RTX_DEFER_MB (default
-            // 4 GiB) of records; RTX_DEFER_CAP overrides (tests).  A chunk that overflows it is
-            // rendered again whole by the redo pass.
+            // 3.2 % of randSpheres' paths leave the near region), at least 2^21 records (the near
+            // pass's waves take slots in blocks of 64), at most RTX_DEFER_MB (default 4 GiB) of
+            // records; RTX_DEFER_CAP overrides (tests).  A chunk that overflows it is rendered
+            // again whole by the redo pass.
             const uint64_t items = chunk * (per_sample / 12);
-            uint64_t cap = std::max<uint64_t>(items / 8, 4096);
+            uint64_t cap = std::max<uint64_t>(items / 8, 1u << 21);
             cap = std::min<uint64_t>(cap, ((uint64_t)env_knob("RTX_DEFER_MB", 4096, 1, 1 << 20) << 20) / 64);
             cap = std::min<uint64_t>(cap, 0xFFFFFFFFull / 2);
             if (const char* e = std::getenv("RTX_DEFER_CAP")) cap = std::strtoull(e, nullptr, 10);

@@ -23,3 +23,10 @@ if [ -n "$SPLIT" ]; then
         tail -1 "$OUT/split$nt.json"
     done
 fi
+if [ -n "$PROF" ]; then
+    step 300 "$OUT/prof.log" rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \
+        python scripts/render_once.py --spp 500
+    python -c "
+import csv
+for r in csv.DictReader(open('$OUT/prof/run_kernel_stats.csv')): print(r['Name'][:70], r['Calls'], r['AverageNs'])" || true
+fi
