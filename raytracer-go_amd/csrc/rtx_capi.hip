@@ -923,6 +923,11 @@ int enqueue_on(rtx_scene* s, DeviceCopy* c, const rtx_camera* cam, uint64_t seed
             pn.prim_end = lay.prim_end;
             pn.tier = 1;
             p.tier = 2;
+            // the near pass's walk is cheaper: it shades in larger batches and tests primitives in
+            // smaller ones (C2 at 100 spp: 56 / 12 lanes 23.15 ms, 48 / 16 23.49 ms; the far pass keeps
+            // the defaults), unless RTX_SHADE_THRESH / RTX_SHADE_THRESH(n) / RTX_PRIM_BATCH say otherwise
+            if (!th && !std::getenv("RTX_SHADE_THRESH")) pn.shade_thresh = 56;
+            if (!std::getenv("RTX_PRIM_BATCH")) pn.prim_batch = 12;
             pn.defer = p.defer = scr->defer;
             pn.defer_cap = p.defer_cap = (uint32_t)cap;
             pn.defer_count = p.defer_count = reinterpret_cast<uint32_t*>(c->counters + 22);  // low: records
