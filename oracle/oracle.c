@@ -373,7 +373,18 @@ static hit_t new_hit_info(float t, float u, float v, vec3 dir, vec3 point, vec3 
 static inline int interval_in(float mn, float mx, float v) { return mn - 0.0f < v && v < mx + 0.0f; }
 
 /* (*Sphere).Hit, hittables.go:96-132. */
-static int sphere_hit(const ctx_t* cx, const rtx_sphere* s, const ray_t* r, float tmin, float tmax, hit_t* out) {
+/* The tie rule of a walk over another tree than the reference's (oracle_sphere_rank): rank[i] is
+ * sphere i's place in the reference walk; a root equal to the bound wins when its sphere comes
+ * before the bound's hit (rank trank) — the tie bvh.go:220-249 resolves for the sphere it meets
+ * first.  A no-op on the reference's own order. */
+static const uint32_t* g_sphere_rank;
+void oracle_sphere_rank(const uint32_t* rank) { g_sphere_rank = rank; }
+static inline uint32_t hit_rank(const ctx_t* cx, const hit_t* h) {
+    return g_sphere_rank && h->sphere ? g_sphere_rank[h->sphere - cx->s->spheres] : 0u;
+}
+
+static int sphere_hit(const ctx_t* cx, const rtx_sphere* s, const ray_t* r, float tmin, float tmax, hit_t* out,
+                      uint32_t trank) {
     vec3 c = v3(s->center[0], s->center[1], s->center[2]);
     vec3 a_sub_c = v_sub(r->origin, c);                                    /* :97 */
     float a = v_lensq(r->dir);                                             /* :98 */
@@ -384,11 +395,12 @@ static int sphere_hit(const ctx_t* cx, const rtx_sphere* s, const ray_t* r, floa
     float sqt = (float)sqrt((double)disc);                                 /* :108 */
     float t;
     float r1 = (-half_b - sqt) / a;                                        /* :110 */
-    if (interval_in(tmin, tmax, r1)) {
+    const int ranked = g_sphere_rank && cx && g_sphere_rank[s - cx->s->spheres] < trank;
+    if (interval_in(tmin, tmax, r1) || (ranked && tmin < r1 && r1 == tmax)) {
         t = r1;
     } else {
         float r2 = (-half_b + sqt) / a;                                    /* :112 */
-        if (interval_in(tmin, tmax, r2)) t = r2;
+        if (interval_in(tmin, tmax, r2) || (ranked && tmin < r2 && r2 == tmax)) t = r2;
         else return 0;
     }
     vec3 point = ray_at(r, t);                                             /* :118 */
@@ -442,7 +454,8 @@ static int aabb_hit(const rtx_bvh_node* n, const ray_t* r, float tmin, float tma
     return 0;
 }
 
-static int hit_ref(const ctx_t* cx, int32_t ref, const ray_t* r, float tmin, float tmax, hit_t* out, int dup);
+static int hit_ref(const ctx_t* cx, int32_t ref, const ray_t* r, float tmin, float tmax, hit_t* out, int dup,
+                   uint32_t trank);
 
 /* Walk hooks (set between renders, read by every render thread): per-node box tests and
  * passes, and the nodes whose box test a collapsed walk leaves out.  Leaving a node's test
@@ -475,7 +488,8 @@ void oracle_tier(const float near_box[6], const rtx_scene_desc* far, const uint8
 }
 
 /* (*BVH).Hit, bvh.go:220-249. */
-static int bvh_hit(const ctx_t* cx, const rtx_bvh_node* n, const ray_t* r, float tmin, float tmax, hit_t* out) {
+static int bvh_hit(const ctx_t* cx, const rtx_bvh_node* n, const ray_t* r, float tmin, float tmax, hit_t* out,
+                   uint32_t trank) {
     const size_t id = (size_t)(n - cx->s->nodes);
     const int far = g_tier_far && cx->s == g_tier_far;
     const uint8_t* skip = far ? g_tier_far_skip : g_node_skip;
@@ -486,10 +500,11 @@ static int bvh_hit(const ctx_t* cx, const rtx_bvh_node* n, const ray_t* r, float
         if (g_node_passed && !far) __atomic_fetch_add(&g_node_passed[id], 1, __ATOMIC_RELAXED);
     }
     hit_t hl, hr;
-    int hit_left = hit_ref(cx, n->left, r, tmin, tmax, &hl, 0);             /* :225 */
+    int hit_left = hit_ref(cx, n->left, r, tmin, tmax, &hl, 0, trank);      /* :225 */
     float rmax = tmax;                                                      /* :227 */
-    if (hit_left) rmax = hl.t;                                              /* :228-230 */
-    int hit_right = hit_ref(cx, n->right, r, tmin, rmax, &hr, n->right == n->left); /* :232 */
+    uint32_t rrank = trank;
+    if (hit_left) { rmax = hl.t; rrank = hit_rank(cx, &hl); }               /* :228-230 */
+    int hit_right = hit_ref(cx, n->right, r, tmin, rmax, &hr, n->right == n->left, rrank); /* :232 */
     if (hit_left && hit_right) {                                            /* :234 */
         *out = (hl.t < hr.t) ? hl : hr;
         return 1;
@@ -499,9 +514,11 @@ static int bvh_hit(const ctx_t* cx, const rtx_bvh_node* n, const ray_t* r, float
     return 0;
 }
 
-static int list_hit(const ctx_t* cx, const rtx_list* l, const ray_t* r, float tmin, float tmax, hit_t* out);
+static int list_hit(const ctx_t* cx, const rtx_list* l, const ray_t* r, float tmin, float tmax, hit_t* out,
+                    uint32_t trank);
 
-static int hit_ref(const ctx_t* cx, int32_t ref, const ray_t* r, float tmin, float tmax, hit_t* out, int dup) {
+static int hit_ref(const ctx_t* cx, int32_t ref, const ray_t* r, float tmin, float tmax, hit_t* out, int dup,
+                   uint32_t trank) {
     if (ref >= 0 || ((uint32_t)(~ref)) >> 28 == RTX_PRIM_LIST) {
         /* A node or a nested World.  As the right child of a one-element split (dup,
          * bvh.go:162-165) its second call runs with the bound clipped to the first one's hit
@@ -509,8 +526,8 @@ static int hit_ref(const ctx_t* cx, int32_t ref, const ray_t* r, float tmin, flo
          * once, so its work is not counted here either. */
         oracle_counters saved;
         if (dup) saved = *cx->c;
-        int h = ref >= 0 ? bvh_hit(cx, &cx->s->nodes[ref], r, tmin, tmax, out)
-                         : list_hit(cx, &cx->s->lists[((uint32_t)(~ref)) & 0x0FFFFFFFu], r, tmin, tmax, out);
+        int h = ref >= 0 ? bvh_hit(cx, &cx->s->nodes[ref], r, tmin, tmax, out, trank)
+                         : list_hit(cx, &cx->s->lists[((uint32_t)(~ref)) & 0x0FFFFFFFu], r, tmin, tmax, out, trank);
         if (dup) *cx->c = saved;
         return h;
     }
@@ -519,19 +536,21 @@ static int hit_ref(const ctx_t* cx, int32_t ref, const ray_t* r, float tmin, flo
     cx->c->prim_tests_ref++;
     if (!dup) cx->c->prim_tests++;
     if (type == RTX_PRIM_QUAD) return quad_hit(&cx->s->quads[idx], r, tmin, tmax, out);
-    return sphere_hit(cx, &cx->s->spheres[idx], r, tmin, tmax, out);
+    return sphere_hit(cx, &cx->s->spheres[idx], r, tmin, tmax, out, trank);
 }
 
 /* (*World).Hit, hittables.go:55-72, of a World nested in the tree (RTX_PRIM_LIST). */
-static int list_hit(const ctx_t* cx, const rtx_list* l, const ray_t* r, float tmin, float tmax, hit_t* out) {
+static int list_hit(const ctx_t* cx, const rtx_list* l, const ray_t* r, float tmin, float tmax, hit_t* out,
+                    uint32_t trank) {
     int hit_any = 0;
     float closest = tmax;
     for (uint32_t i = 0; i < l->count; ++i) {
         hit_t h;
-        if (hit_ref(cx, cx->s->list_refs[l->first + i], r, tmin, closest, &h, 0)) {
+        if (hit_ref(cx, cx->s->list_refs[l->first + i], r, tmin, closest, &h, 0, trank)) {
             hit_any = 1;
             *out = h;
             closest = h.t;
+            trank = hit_rank(cx, &h);
         }
     }
     return hit_any;
@@ -572,12 +591,14 @@ static int world_hit(const ctx_t* cx, const ray_t* r, float tmin, float tmax, hi
 static int world_hit_tree(const ctx_t* cx, const ray_t* r, float tmin, float tmax, hit_t* out) {
     int hit_any = 0;
     float closest = tmax;
+    uint32_t trank = 0;  /* (no hit yet: no tie to win) */
     for (uint32_t i = 0; i < cx->s->n_roots; ++i) {
         hit_t h;
-        if (hit_ref(cx, cx->s->roots[i], r, tmin, closest, &h, 0)) {
+        if (hit_ref(cx, cx->s->roots[i], r, tmin, closest, &h, 0, trank)) {
             hit_any = 1;
             *out = h;
             closest = h.t;
+            trank = hit_rank(cx, &h);
         }
     }
     return hit_any;

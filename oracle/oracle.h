@@ -89,6 +89,11 @@ void oracle_node_hooks(uint64_t* tested, uint64_t* passed, const uint8_t* skip);
  * with far_skip instead of the rendered description. */
 void oracle_tier(const float near_box[6], const rtx_scene_desc* far, const uint8_t* far_skip);
 
+/* Tie-rule hook (NULL = off): rank[i] = sphere i's place in the reference walk.  A root equal to
+ * the running bound then wins when its sphere ranks before the bound's hit, as it would in the
+ * reference's order (the device's walks over rebuilt trees do the same). */
+void oracle_sphere_rank(const uint32_t* rank);
+
 int oracle_render(const rtx_scene_desc* scene, const rtx_camera* cam, uint64_t seed, const rtx_region* region,
                   int order, int threads, float* out, oracle_counters* counters);
 

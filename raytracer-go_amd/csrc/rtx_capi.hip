@@ -292,6 +292,7 @@ struct rtx_scene {
     bool rebuilt = false;
     bool tiered = false;     // near_topo built: renders whose camera lies in its near region walk in two tiers
     rtxd::Topology near_topo;
+    std::vector<uint32_t> sphere_rank;  // rebuilt scenes: each sphere's place in the reference walk (base)
     bool every_box = false;  // RTX_SCENE_EVERY_BOX: no box test left out
     rtxd::Topology topo;
     std::vector<float> quadtab;  // 16 floats per quad (rtx_layout.h)
@@ -562,13 +563,30 @@ int ensure_layout(rtx_scene* s, DeviceCopy* c, const rtx_camera* cam, bool near 
                 if (!in_hot[i]) pos[i] = k++;
             lay.hot = hot;
         } else {
+            // primitives first, in the reference walk's order (the caller's tree walks them in that
+            // order; a rebuilt tree's are sorted back into it): the walk's tie rule compares entry
+            // indices for that order (sphere_test RANKED, rtx_device.h)
+            std::vector<uint32_t> prims;
+            for (size_t i = 0; i < n; ++i) {
+                int32_t tag;
+                std::memcpy(&tag, &(*E)[i].b[3], 4);
+                if (tag != RTX_E_NODE) prims.push_back((uint32_t)i);
+            }
+            if (s->rebuilt) {  // spheres only
+                auto rank = [&](uint32_t i) {
+                    int32_t si;
+                    std::memcpy(&si, &(*E)[i].b[1], 4);
+                    return s->sphere_rank[(uint32_t)si];
+                };
+                std::stable_sort(prims.begin(), prims.end(), [&](uint32_t a, uint32_t b) { return rank(a) < rank(b); });
+            }
             uint32_t k = 0;
-            for (int pass = 0; pass < 2; ++pass)
-                for (size_t i = 0; i < n; ++i) {
-                    int32_t tag;
-                    std::memcpy(&tag, &(*E)[i].b[3], 4);
-                    if ((tag != RTX_E_NODE) == (pass == 0)) pos[i] = k++;
-                }
+            for (uint32_t i : prims) pos[i] = k++;
+            for (size_t i = 0; i < n; ++i) {
+                int32_t tag;
+                std::memcpy(&tag, &(*E)[i].b[3], 4);
+                if (tag == RTX_E_NODE) pos[i] = k++;
+            }
             for (size_t i = 0; i < n; ++i) {
                 int32_t tag;
                 std::memcpy(&tag, &(*E)[i].b[3], 4);
@@ -730,6 +748,14 @@ void adopt_topology(rtx_scene* s, uint32_t flags) {
     const int mode = topology_mode(flags, s->base);
     if (mode == 0 || !rtxd::build_topology(s->base, mode == 1, s->topo)) return;
     s->rebuilt = true;
+    for (const rtx_entry& e : s->base) {  // the walk's tie rule: the reference's order of the spheres
+        int32_t tag, si;
+        std::memcpy(&tag, &e.b[3], 4);
+        std::memcpy(&si, &e.b[1], 4);
+        if (tag < 0) continue;
+        if (s->sphere_rank.size() <= (size_t)si) s->sphere_rank.resize((size_t)si + 1, 0xFFFFFFFFu);
+        if (s->sphere_rank[(size_t)si] == 0xFFFFFFFFu) s->sphere_rank[(size_t)si] = (uint32_t)(&e - s->base.data());
+    }
     s->tiered = tier_topology(flags, mode, s->base, s->near_topo);
 }
 

@@ -761,7 +761,12 @@ __device__ __forceinline__ float div_by(float n, float a, float y) {
 
 // (*Sphere).Hit, hittables.go:96-116, of the sphere entry (ea, eb) at `pos` against (tmin, closest).
 // SAFE: the two divisions by a as div_by.
-template <bool COUNT, bool SAFE = false>
+// RANKED (the LDS layout, whose primitives are stored in the reference walk's order): a root equal
+// to `closest` also wins when the sphere comes before the current hit in the reference's order —
+// the tie bvh.go:220-249 resolves for the sphere it meets first (the right subtree is clipped to the
+// left's hit, strictly).  A walk over another tree (rtx_topology.h) meets equal roots in another
+// order; this rule gives every order the reference's answer.  (A no-op on the reference's own order.)
+template <bool COUNT, bool SAFE = false, bool RANKED = false>
 __device__ __forceinline__ void sphere_test(Trav& t, const Ray& r, const float4 ea, const float4 eb, uint32_t pos,
                                             Counters& cnt) {
     const float tmin = 0.001f;  // ray.go:37
@@ -780,6 +785,7 @@ __device__ __forceinline__ void sphere_test(Trav& t, const Ray& r, const float4 
             tt = SAFE ? div_by(-hb + sq, t.a, t.ra) : (-hb + sq) / t.a;    // :112
             ok = tmin < tt && tt < t.closest;
         }
+        if (RANKED && tt == t.closest && entry_of(pos) < t.hit) ok = true;  // (t.hit = -1: no hit yet)
         if (ok) {
             t.closest = tt;
             t.hit = entry_of(pos);
@@ -882,7 +888,7 @@ __device__ __forceinline__ void trav_step(Trav& t, const Ray& r, const SceneRef 
         box_step<COUNT, MED3>(t, r, ea, eb, tag, cnt);
     } else {
         if (QUADS && tag == RTX_E_QUAD) quad_test<COUNT>(t, r, E, ea, eb, t.i, cnt);
-        else sphere_test<COUNT, MED3>(t, r, ea, eb, t.i, cnt);
+        else sphere_test<COUNT, MED3, FIXED>(t, r, ea, eb, t.i, cnt);
         t.i = (uint32_t)__float_as_int(eb.z);  // the primitive's successor
     }
 }
@@ -913,7 +919,7 @@ __device__ __forceinline__ uint32_t trav_step_batched(Trav& t, const Ray& r, con
         if (__builtin_amdgcn_inverse_ballot_w64(pm)) {  // = prim, as the vote's mask (no second compare)
             if (COUNT && HYB && t.i < E.hot) ++cnt.cache_hits;
             if (QUADS && tag == RTX_E_QUAD) quad_test<COUNT>(t, r, E, ea, eb, t.i, cnt);
-            else sphere_test<COUNT, MED3>(t, r, ea, eb, t.i, cnt);
+            else sphere_test<COUNT, MED3, FIXED>(t, r, ea, eb, t.i, cnt);
             t.i = (uint32_t)__float_as_int(eb.z);
         }
     } else if (__builtin_amdgcn_inverse_ballot_w64(bm)) {  // lanes on a node (the sentinel's step is a no-op)
@@ -1078,6 +1084,10 @@ __device__ __forceinline__ uint32_t trav_step_batched(Trav& t, const Ray& r, con
         "v_cmp_lt_f32_e64 %[l1], %[tmin], v16\n\t" /* tmin < t < closest */  \
         "v_cmp_lt_f32_e64 %[l2], v16, %[cl]\n\t"                             \
         "s_and_b64 %[l1], %[l1], %[l2]\n\t" /* (disc < 0: NaN roots fail) */ \
+        "v_cmp_eq_f32_e64 %[l2], v16, %[cl]\n\t" /* or a tie won by the     */ \
+        "v_cmp_lt_i32_e64 %[g1], v14, %[hit]\n\t" /* reference's earlier sphere */\
+        "s_and_b64 %[l2], %[l2], %[g1]\n\t" /* (sphere_test RANKED) */       \
+        "s_or_b64 %[l1], %[l1], %[l2]\n\t"                                  \
         "v_cndmask_b32_e64 %[cl], %[cl], v16, %[l1]\n\t"                     \
         "v_cndmask_b32_e64 %[hit], %[hit], v14, %[l1]\n\t"                   \
         RTX_PRIM_RUN_TAIL(K, WAIT)                                           \
@@ -1178,6 +1188,10 @@ __device__ __forceinline__ uint32_t trav_step_batched(Trav& t, const Ray& r, con
         "v_cmp_lt_f32_e64 %[l1], %[tmin], v16\n\t" /* tmin < t < closest */  \
         "v_cmp_lt_f32_e64 %[l2], v16, %[cl]\n\t"                             \
         "s_and_b64 %[l1], %[l1], %[l2]\n\t" /* (disc < 0: NaN roots fail) */ \
+        "v_cmp_eq_f32_e64 %[l2], v16, %[cl]\n\t" /* or a tie won by the     */ \
+        "v_cmp_lt_i32_e64 %[g1], v14, %[hit]\n\t" /* reference's earlier sphere */\
+        "s_and_b64 %[l2], %[l2], %[g1]\n\t" /* (sphere_test RANKED) */       \
+        "s_or_b64 %[l1], %[l1], %[l2]\n\t"                                  \
         "v_cndmask_b32_e64 %[cl], %[cl], v16, %[l1]\n\t"                     \
         "v_cndmask_b32_e64 %[hit], %[hit], v14, %[l1]\n"                     \
         "LT%=_" #K ":\n\t"                                                   \

@@ -28,19 +28,21 @@ ap.add_argument("--lib", default=os.path.join(os.path.dirname(os.path.dirname(os
                 help="the library the profiled run loaded: its hash ties the profile to the code (bench.py checks it)")
 args = ap.parse_args()
 
-vals = {"FETCH_SIZE": [], "WRITE_SIZE": []}
+# Per counter and kernel, the median over its dispatches; summed over the matching kernels (a
+# tiered render launches its near, far and redo passes: DESIGN.md §14).
+vals = {"FETCH_SIZE": {}, "WRITE_SIZE": {}}
 for f in glob.glob(os.path.join(args.pmc_dir, "**", "*counter_collection.csv"), recursive=True):
     with open(f) as fh:
         for r in csv.DictReader(fh):
             if args.kernel in r["Kernel_Name"] and r["Counter_Name"] in vals:
-                vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
+                vals[r["Counter_Name"]].setdefault(r["Kernel_Name"], []).append(float(r["Counter_Value"]))
 assert vals["FETCH_SIZE"] and vals["WRITE_SIZE"], f"no {args.kernel} rows with FETCH_SIZE/WRITE_SIZE under {args.pmc_dir}"
-fetch = statistics.median(vals["FETCH_SIZE"]) * 1024 * 2  # KiB -> B, x2 gfx950 correction
-write = statistics.median(vals["WRITE_SIZE"]) * 1024
+fetch = sum(statistics.median(v) for v in vals["FETCH_SIZE"].values()) * 1024 * 2  # KiB -> B, x2 gfx950
+write = sum(statistics.median(v) for v in vals["WRITE_SIZE"].values()) * 1024
 out = {
     "workload": args.workload,
     "kernel": args.kernel,
-    "launches": {k: len(v) for k, v in vals.items()},
+    "launches": {c: {k: len(v) for k, v in d.items()} for c, d in vals.items()},
     "fetch_bytes_per_launch": fetch,
     "write_bytes_per_launch": write,
     "hbm_bytes_per_launch": fetch + write,

@@ -25,23 +25,29 @@ ap.add_argument("--lib", default=os.path.join(os.path.dirname(os.path.dirname(os
                 help="the library the profiled run loaded: its hash ties the profile to the code (bench.py checks it)")
 args = ap.parse_args()
 
-vals = {}
+# Per counter: the sum over every dispatch of the matching kernels (a tiered render launches its
+# near, far and redo passes: DESIGN.md §14), divided by the renders (the dispatches of each kernel).
+vals, disp = {}, {}
 for f in glob.glob(os.path.join(args.pmc_dir, "**", "*counter_collection.csv"), recursive=True):
     with open(f) as fh:
         for r in csv.DictReader(fh):
             if args.kernel in r["Kernel_Name"]:
-                vals.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
+                vals[r["Counter_Name"]] = vals.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+                disp.setdefault((f, r["Counter_Name"], r["Kernel_Name"]), set()).add(r.get("Dispatch_Id", ""))
 need = ["SQ_INSTS_VALU", "GRBM_GUI_ACTIVE", "SQ_THREAD_CYCLES_VALU"]
 assert all(k in vals for k in need), f"missing {need} for {args.kernel} under {args.pmc_dir}"
-insts = vals["SQ_INSTS_VALU"][0]
-cycles = vals["GRBM_GUI_ACTIVE"][0] / 8.0
+renders = {c: max(len(d) for (f, cc, k), d in disp.items() if cc == c) for c in need}
+insts = vals["SQ_INSTS_VALU"] / renders["SQ_INSTS_VALU"]
+cycles = vals["GRBM_GUI_ACTIVE"] / renders["GRBM_GUI_ACTIVE"] / 8.0
+thread_cycles = vals["SQ_THREAD_CYCLES_VALU"] / renders["SQ_THREAD_CYCLES_VALU"]
 out = {
     "workload": args.workload,
     "kernel": args.kernel,
     "valu_insts_per_launch": insts,
     "shader_cycles_per_launch": cycles,
     "valu_issue_frac": round(insts * 2.0 / (cycles * args.simds), 4),
-    "valu_lane_frac": round(vals["SQ_THREAD_CYCLES_VALU"][0] / (64.0 * insts), 4),
+    "valu_lane_frac": round(thread_cycles / (64.0 * insts), 4),
+    "kernels": sorted({k for (f, c, k) in disp}),
     "librtx_sha256_16": hashlib.sha256(open(args.lib, "rb").read()).hexdigest()[:16],
     "method": "rocprofv3 --kernel-trace --pmc SQ_INSTS_VALU SQ_THREAD_CYCLES_VALU GRBM_GUI_ACTIVE ...; "
               "issue frac = 2 cycles x SQ_INSTS_VALU / (GRBM_GUI_ACTIVE / 8 XCDs x 1024 SIMDs)",

@@ -23,7 +23,7 @@ static int ref_prim_hit(const rtx_scene_desc* s, int32_t ref, const ray_t* r, fl
     hit_t h;
     uint32_t p = (uint32_t)(~ref), type = p >> 28, idx = p & 0x0FFFFFFFu;
     int ok = type == RTX_PRIM_QUAD ? quad_hit(&s->quads[idx], r, tmin, tmax, &h)
-                                   : sphere_hit(NULL, &s->spheres[idx], r, tmin, tmax, &h);
+                                   : sphere_hit(NULL, &s->spheres[idx], r, tmin, tmax, &h, 0);
     if (ok) *t = h.t;
     return ok;
 }

@@ -91,6 +91,8 @@ def load():
     L.oracle_node_hooks.restype = None
     L.oracle_tier.argtypes = [c_void_p, c_void_p, c_void_p]
     L.oracle_tier.restype = None
+    L.oracle_sphere_rank.argtypes = [c_void_p]
+    L.oracle_sphere_rank.restype = None
     _lib = L
     return L
 
@@ -134,13 +136,48 @@ def region_rows(reg: rtx.Region) -> int:
     return int(load().oracle_region_rows(ctypes.byref(reg)))
 
 
+def sphere_ranks(desc_ptr):
+    """Each sphere's place in the reference walk of desc_ptr's tree (pre-order: roots in order, a
+    node's left subtree then its right — once when left == right —, a nested World's items in
+    order): the tie rule of a walk over another tree of the same spheres (oracle_sphere_rank)."""
+    d = desc_ptr.contents
+    rank = np.full(max(d.n_spheres, 1), 0xFFFFFFFF, np.uint32)
+    k = 0
+    for ri in range(d.n_roots):
+        stack = [d.roots[ri]]
+        while stack:
+            ref = stack.pop()
+            if ref >= 0:
+                nd = d.nodes[ref]
+                if nd.right != nd.left:
+                    stack.append(nd.right)
+                stack.append(nd.left)
+                continue
+            p = (~ref) & 0xFFFFFFFF
+            typ, idx = p >> 28, p & 0x0FFFFFFF
+            if typ == rtx.RTX_PRIM_LIST:
+                lst = d.lists[idx]
+                stack.extend(d.list_refs[lst.first + i] for i in reversed(range(lst.count)))
+            elif typ == rtx.RTX_PRIM_SPHERE and rank[idx] == 0xFFFFFFFF:
+                rank[idx] = k
+            k += 1
+    return rank
+
+
 def render(desc_ptr, cam: rtx.Camera, seed: int, region: rtx.Region, order: int = ORDER_REFERENCE,
-           threads: int = 0, skip=None, tier=None):
+           threads: int = 0, skip=None, tier=None, rank=None):
     """Oracle render of a region -> (float32 array [rows, width, 3], counters dict).  skip: per node
     of desc_ptr's table, 1 = leave its box test out (a collapsed walk, rtx.node_skip).  tier: (near
     box, far description, far skip or None): the tiered walk (oracle_tier), desc_ptr being the near
     tree."""
     L = load()
+    if rank is not None:  # the tie rule of a walk over a rebuilt tree (sphere_ranks of the caller's tree)
+        rk = np.ascontiguousarray(rank, np.uint32)
+        L.oracle_sphere_rank(rk.ctypes.data_as(c_void_p))
+        try:
+            return render(desc_ptr, cam, seed, region, order, threads, skip, tier)
+        finally:
+            L.oracle_sphere_rank(None)
     if tier is not None:
         box, far, fsk = tier
         boxa = (c_float * 6)(*box)

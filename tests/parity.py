@@ -68,7 +68,8 @@ def tier_of(dev, desc, cam):
 def oracle_checks(desc, walk, cam, seed, reg, skip=None, tier=None):
     """(iterative image on the walked tree with its skips, its counters, reference-order image on
     the caller's tree); asserts check 2 and the collapsed walk's own check."""
-    it, cnt = ob.render(walk, cam, seed, reg, ob.ORDER_ITERATIVE, skip=skip, tier=tier)
+    rank = ob.sphere_ranks(desc) if walk is not desc else None  # the walk's tie rule (sphere_test RANKED)
+    it, cnt = ob.render(walk, cam, seed, reg, ob.ORDER_ITERATIVE, skip=skip, tier=tier, rank=rank)
     if walk is not desc or (skip is not None and skip.any()):
         it0, cnt0 = ob.render(desc, cam, seed, reg, ob.ORDER_ITERATIVE)
         assert np.array_equal(it, it0), f"walked tree changes the image: max {np.abs(it - it0).max()}"

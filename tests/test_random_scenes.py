@@ -169,7 +169,8 @@ def test_random_scene_bitexact(built, seed, n_spheres, n_quads, axis_aligned):
     if tier is not None:
         walk, skip, tier = tier
     reg = rtx.Region(0, 0, cam.image_width, cam.image_height, 0, 1)
-    it, cnt = ob.render(walk, cam, seed, reg, ob.ORDER_ITERATIVE, skip=skip, tier=tier)
+    rank = ob.sphere_ranks(pd) if walk is not pd else None
+    it, cnt = ob.render(walk, cam, seed, reg, ob.ORDER_ITERATIVE, skip=skip, tier=tier, rank=rank)
     if walk is not pd:  # the rebuilt tree: same image and paths as the caller's tree on the oracle
         it0, cnt0 = ob.render(pd, cam, seed, reg, ob.ORDER_ITERATIVE)
         assert np.array_equal(it, it0, equal_nan=True)

@@ -214,11 +214,11 @@ def test_tiered_oracle_equals_reference(built, scene, width, spp):
     far = rtx.walk_tree_desc(s.desc, cam)
     reg = rtx.Region(0, 0, cam.image_width, cam.image_height, 0, 1)
     a, ca = ob.render(s.desc, cam, 2024, reg, ob.ORDER_ITERATIVE)
-    b, cb = ob.render(near, cam, 2024, reg, ob.ORDER_ITERATIVE, tier=(box, far, None))
+    b, cb = ob.render(near, cam, 2024, reg, ob.ORDER_ITERATIVE, tier=(box, far, None), rank=ob.sphere_ranks(s.desc))
     assert np.array_equal(a, b)
     for k in ("samples", "segments", "hits", "texel_fetches", "rng_draws"):
         assert ca[k] == cb[k], k
     assert cb["prim_tests"] < 0.7 * ca["prim_tests"] and cb["node_visits"] < 0.7 * ca["node_visits"]
     # every segment in the near tree alone (no far tier): the same image here too
-    c, _ = ob.render(near, cam, 2024, reg, ob.ORDER_ITERATIVE)
+    c, _ = ob.render(near, cam, 2024, reg, ob.ORDER_ITERATIVE, rank=ob.sphere_ranks(s.desc))
     assert np.array_equal(a, c)
