@@ -721,7 +721,8 @@ bool tier_topology(uint32_t flags, int mode, const std::vector<rtx_entry>& base,
     const char* e = std::getenv("RTX_TIER");
     if (e && std::strcmp(e, "0") == 0) return false;
     float box[6];
-    return rtxd::near_region(base, box) && rtxd::build_topology(base, false, near, box);
+    const double grow = env_knob("RTX_NEAR_GROW", 25, 0, 1000) / 100.0;  // percent of the core's extent (A/B)
+    return rtxd::near_region(base, box, grow) && rtxd::build_topology(base, false, near, box);
 }
 
 // A tiered scene walks in two tiers for a camera whose rays all start in the near region (the

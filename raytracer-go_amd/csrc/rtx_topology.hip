@@ -228,7 +228,7 @@ bool precise_enough(const std::vector<rtx_entry>& ref) {
     return rmin > 0.0 && std::ldexp(d2, -24) / (rmin * rmin) < std::ldexp(1.0, -7);
 }
 
-bool near_region(const std::vector<rtx_entry>& ref, float box[6]) {
+bool near_region(const std::vector<rtx_entry>& ref, float box[6], double grow) {
     Box b;
     double rmin = 0.0;
     if (!core_box(ref, b, rmin)) return false;
@@ -236,8 +236,8 @@ bool near_region(const std::vector<rtx_entry>& ref, float box[6]) {
     for (int q = 0; q < 3; ++q) ext = std::max(ext, (double)b.mx[q] - (double)b.mn[q]);
     if (!std::isfinite(ext)) return false;
     for (int q = 0; q < 3; ++q) {  // rounded outward: the region only grows
-        box[q] = std::nextafter((float)((double)b.mn[q] - 0.25 * ext), -INFINITY);
-        box[3 + q] = std::nextafter((float)((double)b.mx[q] + 0.25 * ext), INFINITY);
+        box[q] = std::nextafter((float)((double)b.mn[q] - grow * ext), -INFINITY);
+        box[3 + q] = std::nextafter((float)((double)b.mx[q] + grow * ext), INFINITY);
         if (!std::isfinite(box[q]) || !std::isfinite(box[3 + q])) return false;
     }
     return true;

@@ -22,6 +22,7 @@ ap.add_argument("--thresh", default="48")
 ap.add_argument("--batch", default="16")
 ap.add_argument("--sub", default="0")
 ap.add_argument("--tier", default="1,0")
+ap.add_argument("--grow", default="25", help="RTX_NEAR_GROW values (percent) for the tiered scenes")
 a = ap.parse_args()
 torch.cuda.set_device(0)
 s = rtx.HostScene(a.scene, 1)
@@ -29,14 +30,19 @@ cam = s.camera(width=a.width, spp=a.spp)
 reg = rtx.Region(0, 0, cam.image_width, cam.image_height, 0, 1)
 out = torch.empty((cam.image_height, cam.image_width, 3), dtype=torch.float32, device="cuda")
 stream = torch.cuda.current_stream().cuda_stream
-devs = {t: rtx.DeviceScene(s.desc, no_tier=(t == 0)) for t in map(int, a.tier.split(","))}
-for t, th, pb, sub in itertools.product(devs, a.thresh.split(","), a.batch.split(","), a.sub.split(",")):
+devs = {}
+for t in map(int, a.tier.split(",")):
+    for g in (a.grow.split(",") if t else ["-"]):
+        if g != "-":
+            os.environ["RTX_NEAR_GROW"] = g
+        devs[(t, g)] = rtx.DeviceScene(s.desc, no_tier=(t == 0))
+for (t, g), th, pb, sub in itertools.product(devs, a.thresh.split(","), a.batch.split(","), a.sub.split(",")):
     os.environ["RTX_PRIM_BATCH"] = pb
     os.environ["RTX_ITEM_SUB"] = sub
     ms = []
     for _ in range(a.reps):
-        st = devs[t].render_region(cam, 2024, reg, out.data_ptr(), stream, timed=True,
+        st = devs[(t, g)].render_region(cam, 2024, reg, out.data_ptr(), stream, timed=True,
                                    flags=rtx.RTX_FLAG_SHADE_THRESH(int(th)))
         ms.append(st.kernel_ms)
-    print(json.dumps({"tier": t, "thresh": int(th), "batch": int(pb), "sub": int(sub), "ms": round(min(ms), 3),
+    print(json.dumps({"tier": t, "grow": g, "deferred": st.deferred_paths, "thresh": int(th), "batch": int(pb), "sub": int(sub), "ms": round(min(ms), 3),
                       "all": [round(x, 3) for x in ms]}), flush=True)
