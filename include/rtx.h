@@ -311,7 +311,7 @@ int rtx_scene_create(const rtx_scene_desc* desc, rtx_scene** out);
 /* ABI 8.  The tiered walk.  A scene walked over the library's own tree also
  * gets a NEAR tree: the spheres themselves as leaves, each behind its own box grown by the
  * float32 sphere test's error bound for ray origins inside a NEAR REGION (the box of the
- * scene's non-huge spheres grown by a quarter of its extent).  A render whose camera lies in
+ * scene's non-huge spheres grown by its largest extent).  A render whose camera lies in
  * the region walks every segment that starts there on the near tree (3.9x fewer sphere
  * tests on randSpheres); a path whose segment starts outside it is handed, once, to a
  * second pass that continues it on the guarded tree (the reference's leaves).  The closest

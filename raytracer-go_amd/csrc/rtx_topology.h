@@ -58,9 +58,9 @@ struct Topology {
 bool build_topology(const std::vector<rtx_entry>& ref, bool guarded, Topology& out, const float* near_box = nullptr);
 
 // The near region of a tiered walk: the box of the spheres that are not huge (precise_enough's
-// core) grown by `grow` (a quarter) of its largest extent on every side, min xyz then max xyz.  False when
+// core) grown by `grow` times its largest extent on every side, min xyz then max xyz.  False when
 // the scene has no finite core.
-bool near_region(const std::vector<rtx_entry>& ref, float box[6], double grow = 0.25);
+bool near_region(const std::vector<rtx_entry>& ref, float box[6], double grow = 1.0);
 
 // How far outside a sphere (centre c, radius r) the float32 sphere test can put a hit for a ray
 // origin at distance <= dmax from c: sqrt(r^2 + 2^-17 (dmax^2 + r^2)) - r, plus 2^-20 (dmax + r)
