@@ -19,9 +19,9 @@ step 400 "$OUT/bench_prof.log" rocprofv3 --kernel-trace --stats -d "$OUT/prof" -
 RTX_NEAR_GROW=25 step 300 "$OUT/bench_grow25.json" python bench.py --steps 3 --warmup 1 --no-cpu
 RTX_TIER=0 step 300 "$OUT/bench_notier.json" python bench.py --steps 3 --warmup 1 --no-cpu
 for f in bench_grow25 bench_notier; do tail -1 "$OUT/$f.json" | cut -c1-200; done
-step 1100 "$OUT/pytest_gpu.log" python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread
+[ -n "$SKIP_TESTS" ] || step 1100 "$OUT/pytest_gpu.log" python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread
 grep -E "passed|failed" "$OUT/pytest_gpu.log" | tail -2
-step 200 "$OUT/smoke.log" python -c "import __graft_entry__ as g; g.smoke()"
+[ -n "$SKIP_TESTS" ] || step 200 "$OUT/smoke.log" python -c "import __graft_entry__ as g; g.smoke()"
 tail -1 "$OUT/smoke.log"
-TAG=$TAG/configs step 1500 "$OUT/configs.log" bash scripts/gpu_configs.sh
+[ -n "$SKIP_CONFIGS" ] || TAG=$TAG/configs step 1500 "$OUT/configs.log" bash scripts/gpu_configs.sh
 tail -2 "$OUT/configs.log"
