@@ -27,14 +27,18 @@ args = ap.parse_args()
 
 # Per counter: the sum over every dispatch of the matching kernels (a tiered render launches its
 # near, far and redo passes: DESIGN.md §14), divided by the renders (the dispatches of each kernel).
-vals, disp = {}, {}
-for f in glob.glob(os.path.join(args.pmc_dir, "**", "*counter_collection.csv"), recursive=True):
-    with open(f) as fh:
-        for r in csv.DictReader(fh):
-            if args.kernel in r["Kernel_Name"]:
-                vals[r["Counter_Name"]] = vals.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
-                disp.setdefault((f, r["Counter_Name"], r["Kernel_Name"]), set()).add(r.get("Dispatch_Id", ""))
+# All from the one pass that holds every counter needed (GRBM_GUI_ACTIVE is in other passes too).
 need = ["SQ_INSTS_VALU", "GRBM_GUI_ACTIVE", "SQ_THREAD_CYCLES_VALU"]
+vals, disp = {}, {}
+for f in sorted(glob.glob(os.path.join(args.pmc_dir, "**", "*counter_collection.csv"), recursive=True)):
+    with open(f) as fh:
+        rows = [r for r in csv.DictReader(fh) if args.kernel in r["Kernel_Name"]]
+    if not all(any(r["Counter_Name"] == k for r in rows) for k in need):
+        continue
+    for r in rows:
+        vals[r["Counter_Name"]] = vals.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+        disp.setdefault((f, r["Counter_Name"], r["Kernel_Name"]), set()).add(r.get("Dispatch_Id", ""))
+    break
 assert all(k in vals for k in need), f"missing {need} for {args.kernel} under {args.pmc_dir}"
 renders = {c: max(len(d) for (f, cc, k), d in disp.items() if cc == c) for c in need}
 insts = vals["SQ_INSTS_VALU"] / renders["SQ_INSTS_VALU"]
