@@ -1118,10 +1118,12 @@ extern "C" {
 
 int rtx_version(void) { return RTX_ABI_VERSION; }
 
+// (No build date: the library's bytes depend on its sources only, so the PMC profiles bench.py ties to the
+// library's hash stay valid across rebuilds of the same sources.)
 const char* rtx_build_info(void) {
-    return "librtx gfx950 megakernel (ABI 6: persistent (pixel, sample) item waves, LDS scene, threaded pre-order BVH "
-           "(binned-SAH walk tree per camera octant, or the caller's), RGBA16 image texels, RCCL band gather); built "
-           __DATE__ " " __TIME__;
+    return "librtx gfx950 megakernel (ABI 8: persistent (pixel, sample) item waves, LDS scene, threaded pre-order BVH "
+           "(binned-SAH walk trees per camera octant: tiered near / guarded, or the caller's), collapsed walk, "
+           "RGBA16 image texels, RCCL band gather)";
 }
 
 const char* rtx_last_error(void) { return g_last_error.c_str(); }
