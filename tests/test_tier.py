@@ -222,3 +222,32 @@ def test_tiered_oracle_equals_reference(built, scene, width, spp):
     # every segment in the near tree alone (no far tier): the same image here too
     c, _ = ob.render(near, cam, 2024, reg, ob.ORDER_ITERATIVE, rank=ob.sphere_ranks(s.desc))
     assert np.array_equal(a, c)
+
+
+@pytest.mark.parametrize("scene,width,spp,px,py,k", [
+    ("random_spheres", 1920, 500, 269, 370, 371),     # a camera ray grazing a box face: the hit check defers it
+    ("earth_dielectric", 3840, 1000, 1311, 469, 759),  # overlapping spheres 454 / 455 at one root: the tie rule
+    ("earth_dielectric", 3840, 1000, 3487, 1098, 691),
+])
+def test_tiered_oracle_known_cases(built, scene, width, spp, px, py, k):
+    """Single samples of the BASELINE frames where the near tree alone once differed from the reference
+    (found on whole GPU frames, traced on the oracle): the tiered walk with its hit
+    check and tie rule gives the reference's colour and path length."""
+    L = ob.load()
+    s = rtx.HostScene(scene, 1)
+    cam = s.camera(width=width, spp=spp)
+    box, active = rtx.walk_near_region(s.desc, cam)
+    assert active
+    near = rtx.walk_near_desc(s.desc, cam)
+    far = rtx.walk_tree_desc(s.desc, cam)
+    want, wc = ob.sample(s.desc, cam, 2024, px, py, k, ob.ORDER_ITERATIVE)
+    rank = np.ascontiguousarray(ob.sphere_ranks(s.desc), np.uint32)
+    L.oracle_sphere_rank(rank.ctypes.data_as(ctypes.c_void_p))
+    L.oracle_tier((ctypes.c_float * 6)(*box), ctypes.cast(far, ctypes.c_void_p), None)
+    try:
+        got, gc = ob.sample(near, cam, 2024, px, py, k, ob.ORDER_ITERATIVE)
+    finally:
+        L.oracle_tier(None, None, None)
+        L.oracle_sphere_rank(None)
+    assert np.array_equal(np.asarray(got), np.asarray(want)), (got, want)
+    assert gc["segments"] == wc["segments"] and gc["rng_draws"] == wc["rng_draws"]
