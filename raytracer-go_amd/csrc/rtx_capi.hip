@@ -83,6 +83,8 @@ struct Scratch {
     size_t bytes = 0;
     float4* defer = nullptr;  // the tiered walk's queue of deferred paths (64 B per record)
     size_t defer_bytes = 0;
+    uint32_t* redo = nullptr;  // the tiered walk's redo bits: one per sample of a chunk
+    size_t redo_bytes = 0;
     hipEvent_t last = nullptr;
     int scenes = 0;
 };
@@ -155,6 +157,7 @@ void release_scratch_locked(int device) {
         if (sc.last) (void)hipEventSynchronize(sc.last);
         if (sc.ptr) (void)hipFree(sc.ptr);
         if (sc.defer) (void)hipFree(sc.defer);
+        if (sc.redo) (void)hipFree(sc.redo);
         if (sc.last) (void)hipEventDestroy(sc.last);
     }
     (void)hipSetDevice(cur);
@@ -292,7 +295,7 @@ struct rtx_scene {
     bool rebuilt = false;
     bool tiered = false;     // near_topo built: renders whose camera lies in its near region walk in two tiers
     rtxd::Topology near_topo;
-    std::vector<uint32_t> sphere_rank;  // rebuilt scenes: each sphere's place in the reference walk (base)
+    std::vector<uint32_t> sphere_rank;  // each sphere's place in the reference walk (base): the tie rule
     bool every_box = false;  // RTX_SCENE_EVERY_BOX: no box test left out
     rtxd::Topology topo;
     std::vector<float> quadtab;  // 16 floats per quad (rtx_layout.h)
@@ -572,7 +575,13 @@ int ensure_layout(rtx_scene* s, DeviceCopy* c, const rtx_camera* cam, bool near 
                 std::memcpy(&tag, &(*E)[i].b[3], 4);
                 if (tag != RTX_E_NODE) prims.push_back((uint32_t)i);
             }
-            if (s->rebuilt) {  // spheres only
+            bool spheres = true;
+            for (uint32_t i : prims) {
+                int32_t tag;
+                std::memcpy(&tag, &(*E)[i].b[3], 4);
+                spheres &= tag >= 0;
+            }
+            if (spheres) {  // (a quad scene keeps the caller's tree: its walk meets them in that order)
                 auto rank = [&](uint32_t i) {
                     int32_t si;
                     std::memcpy(&si, &(*E)[i].b[1], 4);
@@ -612,6 +621,9 @@ int ensure_layout(rtx_scene* s, DeviceCopy* c, const rtx_camera* cam, bool near 
                 if (tag >= 0) {
                     const int32_t sph = RTX_DEV_SPHERE(tag);
                     std::memcpy(&soa[4 * (m + j) + 3], &sph, 4);
+                    int32_t si;  // the sphere's rank word (sphere_test RANK_WORD) in place of its index
+                    std::memcpy(&si, &(*E)[i].b[1], 4);
+                    std::memcpy(&soa[4 * (m + j) + 1], &s->sphere_rank[(uint32_t)si], 4);
                 }
             }
         }
@@ -714,16 +726,22 @@ int topology_mode(uint32_t flags, const std::vector<rtx_entry>& ref) {
     return rtxd::precise_enough(ref) ? 1 : 0;
 }
 
-// The tiered walk: a guarded scene also gets a near tree (spheres behind their own
-// boxes grown for origins in the near region), unless RTX_SCENE_NO_TIER or RTX_TIER=0.
-bool tier_topology(uint32_t flags, int mode, const std::vector<rtx_entry>& base, rtxd::Topology& near) {
-    if (mode != 1 || (flags & RTX_SCENE_NO_TIER)) return false;
+// The tiered walk: a scene of spheres under one tree also gets a near tree (spheres
+// behind their own boxes grown for origins in the near region), unless RTX_SCENE_NO_TIER,
+// RTX_SCENE_REFERENCE_BVH or RTX_TIER=0, or a node box does not contain the boxes of the spheres
+// below it (the hit check's argument needs that; NewBVH's always do).  Its far tree is the walk's
+// other tree: the guarded rebuild, or the caller's.  The region is the core box grown by
+// RTX_NEAR_GROW percent of its largest extent: 100 for scenes that pass precise_enough (randSpheres:
+// C2 at 100 spp 10 / 25 / 40 / 60 / 100 % -> 23.73 / 23.43 / 23.21 / 22.89 / 22.67 ms, 3.6 / 3.2 / 2.6 /
+// 1.8 / 0.9 % of the paths deferred), 1 for the others (config 4's 316-unit slab: its far spheres'
+// margins already set the boxes; the region need only hold the camera and the slab).
+bool tier_topology(uint32_t flags, const std::vector<rtx_entry>& base, rtxd::Topology& near) {
+    if (flags & (RTX_SCENE_NO_TIER | RTX_SCENE_REFERENCE_BVH)) return false;
     const char* e = std::getenv("RTX_TIER");
     if (e && std::strcmp(e, "0") == 0) return false;
+    if (!rtxd::own_boxes_nested(base)) return false;
     float box[6];
-    // the core box grown by its largest extent (percent; C2 at 100 spp: 10 / 25 / 40 / 60 / 100 % ->
-    // 23.73 / 23.43 / 23.21 / 22.89 / 22.67 ms, 3.6 / 3.2 / 2.6 / 1.8 / 0.9 % of the paths deferred)
-    const double grow = env_knob("RTX_NEAR_GROW", 100, 0, 1000) / 100.0;
+    const double grow = env_knob("RTX_NEAR_GROW", rtxd::precise_enough(base) ? 100 : 1, 0, 1000) / 100.0;
     return rtxd::near_region(base, box, grow) && rtxd::build_topology(base, false, near, box);
 }
 
@@ -744,22 +762,29 @@ bool camera_in_near(const rtx_scene* s, const rtx_camera* cam) {
     return s->tiered && camera_in_box(s->near_topo.near_box, cam);
 }
 
-// A scene whose base holds the reference's walk of one tree: take the walk's own tree when it
-// qualifies (spheres only; rtxd::build_topology).
-void adopt_topology(rtx_scene* s, uint32_t flags) {
-    s->every_box = (flags & RTX_SCENE_EVERY_BOX) != 0;
-    const int mode = topology_mode(flags, s->base);
-    if (mode == 0 || !rtxd::build_topology(s->base, mode == 1, s->topo)) return;
-    s->rebuilt = true;
-    for (const rtx_entry& e : s->base) {  // the walk's tie rule: the reference's order of the spheres
+// Each sphere's place in the reference walk of the caller's tree (its first entry in `base`): the walk's
+// tie rule (sphere_test RANKED / RANK_WORD) for walks over another tree or in another storage order.
+void rank_spheres(rtx_scene* s) {
+    s->sphere_rank.clear();
+    uint32_t k = 0;
+    for (const rtx_entry& e : s->base) {
         int32_t tag, si;
         std::memcpy(&tag, &e.b[3], 4);
         std::memcpy(&si, &e.b[1], 4);
         if (tag < 0) continue;
         if (s->sphere_rank.size() <= (size_t)si) s->sphere_rank.resize((size_t)si + 1, 0xFFFFFFFFu);
-        if (s->sphere_rank[(size_t)si] == 0xFFFFFFFFu) s->sphere_rank[(size_t)si] = (uint32_t)(&e - s->base.data());
+        if (s->sphere_rank[(size_t)si] == 0xFFFFFFFFu) s->sphere_rank[(size_t)si] = k;
+        ++k;
     }
-    s->tiered = tier_topology(flags, mode, s->base, s->near_topo);
+}
+
+// A scene whose base holds the reference's walk of one tree: take the walk's own tree when it
+// qualifies (spheres only; rtxd::build_topology), and its near tree.
+void adopt_topology(rtx_scene* s, uint32_t flags) {
+    s->every_box = (flags & RTX_SCENE_EVERY_BOX) != 0;
+    const int mode = topology_mode(flags, s->base);
+    if (mode != 0 && rtxd::build_topology(s->base, mode == 1, s->topo)) s->rebuilt = true;
+    s->tiered = tier_topology(flags, s->base, s->near_topo);
 }
 
 // The quad table of a scene description (rtx_layout.h): (Q, material), (u, 0), (v, 0), (w, 0).
@@ -877,15 +902,12 @@ int enqueue_on(rtx_scene* s, DeviceCopy* c, const rtx_camera* cam, uint64_t seed
     const uint32_t oct = layout_slot(s, cam);  // the walk's layout (rtx_topology.h, rtx_collapse.h)
     if (int rc = ensure_layout(s, c, cam)) return rc;
     rtxd::Params p = make_params(s, c, oct, cam, seed, r, d_out);
-    // the tiered walk: a camera in the near region, both walks in the LDS copy (not for the
-    // RTX_FLAG_NO_LDS A/B)
-    bool tier = camera_in_near(s, cam) && !(flags & RTX_FLAG_NO_LDS) && p.n_quads == 0 &&
-                !p.has_noise && rtxd::scene_placement(p, flags) == RTX_SCENE_IN_LDS;
+    // the tiered walk: a camera in the near region of a sphere scene (rtx_scene_near_region's rule)
+    bool tier = camera_in_near(s, cam) && p.n_quads == 0 && !p.has_noise;
     rtxd::Params pn;
     if (tier) {
         if (int rc = ensure_layout(s, c, cam, true)) return rc;
-        pn = make_params(s, c, 8u + oct, cam, seed, r, d_out);
-        tier = rtxd::scene_placement(pn, flags) == RTX_SCENE_IN_LDS;
+        pn = make_params(s, c, layout_slot(s, cam, true), cam, seed, r, d_out);
     }
     *tiered = false;
     const uint32_t th = (flags >> 8) & 0x7Fu;  // RTX_FLAG_SHADE_THRESH(n) override
@@ -929,11 +951,13 @@ int enqueue_on(rtx_scene* s, DeviceCopy* c, const rtx_camera* cam, uint64_t seed
             // pass's waves take slots in blocks of 64), at most RTX_DEFER_MB (default 4 GiB) of
             // records; RTX_DEFER_CAP overrides (tests).  A chunk that overflows it is rendered
             // again whole by the redo pass.
+            // A sample whose record does not fit is flagged in a bitmap of the chunk's samples (one bit
+            // per scratch slot) and rendered again from its camera ray by the redo pass.
             const uint64_t items = chunk * (per_sample / 12);
             uint64_t cap = std::max<uint64_t>(items / 8, 1u << 21);
+            if (const char* e = std::getenv("RTX_DEFER_CAP")) cap = std::strtoull(e, nullptr, 10);
             cap = std::min<uint64_t>(cap, ((uint64_t)env_knob("RTX_DEFER_MB", 4096, 1, 1 << 20) << 20) / 64);
             cap = std::min<uint64_t>(cap, 0xFFFFFFFFull / 2);
-            if (const char* e = std::getenv("RTX_DEFER_CAP")) cap = std::strtoull(e, nullptr, 10);
             const size_t need = (size_t)std::max<uint64_t>(cap, 1) * 64;
             if (scr->defer_bytes < need) {
                 HIP_TRY(hipEventSynchronize(scr->last));
@@ -942,6 +966,15 @@ int enqueue_on(rtx_scene* s, DeviceCopy* c, const rtx_camera* cam, uint64_t seed
                 scr->defer_bytes = 0;
                 HIP_TRY(hipMalloc(&scr->defer, need));
                 scr->defer_bytes = need;
+            }
+            const size_t bits = (size_t)(items / 8);  // chunk x tiles x 64 slots, 8 per byte
+            if (scr->redo_bytes < bits) {
+                HIP_TRY(hipEventSynchronize(scr->last));
+                if (scr->redo) HIP_TRY(hipFree(scr->redo));
+                scr->redo = nullptr;
+                scr->redo_bytes = 0;
+                HIP_TRY(hipMalloc(&scr->redo, bits));
+                scr->redo_bytes = bits;
             }
             rtxd::Params lay = pn;  // the near pass: every setting of p, the near walk's layout
             pn = p;
@@ -958,6 +991,7 @@ int enqueue_on(rtx_scene* s, DeviceCopy* c, const rtx_camera* cam, uint64_t seed
             if (!th && !std::getenv("RTX_SHADE_THRESH")) pn.shade_thresh = 56;
             if (!std::getenv("RTX_PRIM_BATCH")) pn.prim_batch = 12;
             pn.defer = p.defer = scr->defer;
+            pn.redo_bits = p.redo_bits = scr->redo;
             pn.defer_cap = p.defer_cap = (uint32_t)cap;
             pn.defer_count = p.defer_count = reinterpret_cast<uint32_t*>(c->counters + 22);  // low: records
             pn.redo_flag = p.redo_flag = reinterpret_cast<uint32_t*>(c->counters + 22) + 1;  // high: overflow
@@ -966,7 +1000,7 @@ int enqueue_on(rtx_scene* s, DeviceCopy* c, const rtx_camera* cam, uint64_t seed
             *tiered = true;
         }
     }
-    c->placement = rtxd::scene_placement(p, flags);
+    c->placement = *tiered ? rtxd::tier_placement(pn, p, flags) : rtxd::scene_placement(p, flags);
     // every stats slot, the unit queue head and the watchdog flag start at 0 for every render
     HIP_TRY(hipMemsetAsync(c->counters, 0, rtxd::COUNTER_SLOTS * sizeof(unsigned long long), stream));
     if (timed) HIP_TRY(hipEventRecord(c->ev0, stream));
@@ -1155,6 +1189,7 @@ int rtx_scene_create_ex(const rtx_scene_desc* d, uint32_t flags, rtx_scene** out
             return rc;
         }
     }
+    rank_spheres(s);
     if (d->n_roots == 1) adopt_topology(s, flags);
     else s->every_box = (flags & RTX_SCENE_EVERY_BOX) != 0;
     return finish_scene(s, d, out);
@@ -1189,6 +1224,7 @@ int rtx_scene_create_spheres(const rtx_sphere* spheres, uint32_t n_spheres, cons
         return fail(e == hipErrorOutOfMemory ? RTX_ERR_OOM : RTX_ERR_HIP, "GPU BVH build: %s", hipGetErrorString(e));
     }
     if (build_ms) *build_ms = ms;
+    rank_spheres(s);
     adopt_topology(s, 0u);
     return finish_scene(s, &d, out);
 }
@@ -1275,9 +1311,8 @@ int rtx_walk_near_region(const rtx_scene_desc* d, uint32_t flags, const rtx_came
     for (uint32_t i = 0; i < d->n_roots; ++i)
         if (int rc = emit(d, d->roots[i], base)) return rc;
     *active = 0;
-    rtxd::Topology t, nt;
-    const int mode = d->n_roots == 1 ? topology_mode(flags, base) : 0;
-    if (mode == 0 || !rtxd::build_topology(base, mode == 1, t) || !tier_topology(flags, mode, base, nt)) return RTX_OK;
+    rtxd::Topology nt;
+    if (d->n_roots != 1 || !tier_topology(flags, base, nt)) return RTX_OK;
     std::memcpy(box, nt.near_box, 6 * sizeof(float));
     bool noise = false;
     for (uint32_t i = 0; i < d->n_textures; ++i) noise |= d->textures[i].type == RTX_TEX_NOISE;
@@ -1324,8 +1359,7 @@ int rtx_walk_tree(const rtx_scene_desc* d, uint32_t flags, uint32_t octant, rtx_
         if (int rc = emit(d, d->roots[i], ref)) return rc;
     rtxd::Topology t;
     const int mode = topology_mode(flags, ref);
-    if (d->n_roots != 1 || mode == 0 || !rtxd::build_topology(ref, mode == 1, t) ||
-        (near && !tier_topology(flags, mode, ref, t))) {
+    if (d->n_roots != 1 || (near ? !tier_topology(flags, ref, t) : (mode == 0 || !rtxd::build_topology(ref, mode == 1, t)))) {
         *n_nodes = 0;
         *root = -1;
         return RTX_OK;
@@ -1354,13 +1388,11 @@ uint64_t rtx_scene_device_bytes(const rtx_scene* s) {
            s->textures.size() * sizeof(rtx_texture) + s->texels.size() * sizeof(uint32_t);
 }
 
-int rtx_render_region_device(rtx_scene* s, const rtx_camera* cam, uint64_t seed, const rtx_region* region,
-                             float* d_out, void* hip_stream, uint32_t flags, rtx_stats* stats) {
-    g_last_error.clear();
-    if (!s || !d_out) return fail(RTX_ERR_INVALID_ARG, "NULL argument");
-    if (int rc = check_camera(cam)) return rc;
-    if (int rc = check_region(cam, region)) return rc;
-    std::lock_guard<std::mutex> lk(s->mu);
+namespace {
+// rtx_render_region_device with s->mu held by the caller.  Lock order everywhere: s->mu, then
+// g_render_mu (rtx_render_ex, rtx_render_ppm), then g_scratch_mu (enqueue_on).
+int render_region_locked(rtx_scene* s, const rtx_camera* cam, uint64_t seed, const rtx_region* region, float* d_out,
+                         void* hip_stream, uint32_t flags, rtx_stats* stats) {
     int cur = 0;
     HIP_TRY(hipGetDevice(&cur));
     DeviceCopy* c = nullptr;
@@ -1376,6 +1408,17 @@ int rtx_render_region_device(rtx_scene* s, const rtx_camera* cam, uint64_t seed,
     const int rc = collect_on(c, count, (uint64_t)region_rows(region) * region->width * cam->samples_per_pixel, chunks, stats);
     stats->walk_layout = walk_layout(s, cam, tiered);
     return rc;
+}
+}  // namespace
+
+int rtx_render_region_device(rtx_scene* s, const rtx_camera* cam, uint64_t seed, const rtx_region* region,
+                             float* d_out, void* hip_stream, uint32_t flags, rtx_stats* stats) {
+    g_last_error.clear();
+    if (!s || !d_out) return fail(RTX_ERR_INVALID_ARG, "NULL argument");
+    if (int rc = check_camera(cam)) return rc;
+    if (int rc = check_region(cam, region)) return rc;
+    std::lock_guard<std::mutex> lk(s->mu);
+    return render_region_locked(s, cam, seed, region, d_out, hip_stream, flags, stats);
 }
 
 int rtx_render(rtx_scene* s, const rtx_camera* cam, uint64_t seed, int n_gpus, float* out_rgb, rtx_stats* stats) {
@@ -1430,9 +1473,14 @@ int rtx_render_ex(rtx_scene* s, const rtx_camera* cam, uint64_t seed, int n_gpus
             break;
         }
         rc = enqueue_on(s, c, cam, seed, &regs[d], bufs[d], streams[d], kflags, true, &chunks[d], &tiered);
+        if (rc == RTX_OK && sim > 1) {  // simulated bands share device 0's counters and events: read each now
+            rtx_stats st;
+            rc = collect_on(c, kflags != 0, (uint64_t)region_rows(&regs[d]) * W * cam->samples_per_pixel, chunks[d], &st);
+            if (rc == RTX_OK) add_stats(&total, st);
+        }
     }
     // 2. Wait for every band (and read its counters), so gather_ms times only the gather.
-    for (int d = 0; d < n && rc == RTX_OK; ++d) {
+    for (int d = 0; d < n && rc == RTX_OK && sim == 1; ++d) {
         if (hipSetDevice(dev_of(d)) != hipSuccess) { rc = fail(RTX_ERR_HIP, "hipSetDevice(%d)", dev_of(d)); break; }
         rtx_stats st;
         uint64_t samples = (uint64_t)region_rows(&regs[d]) * W * cam->samples_per_pixel;
@@ -1638,6 +1686,7 @@ int rtx_render_ppm(rtx_scene* s, const rtx_camera* cam, uint64_t seed, char* out
     const uint64_t need = rtxd::ppm_max_bytes(W, H);
     int dev = 0;
     HIP_TRY(hipGetDevice(&dev));
+    std::lock_guard<std::mutex> lk(s->mu);  // (lock order: the scene, then the render buffers)
     std::lock_guard<std::mutex> bl(g_render_mu);  // the cached image / text buffers and stream
     hipStream_t st = render_stream(dev);
     float* rgb = static_cast<float*>(render_buffer(dev, -3, std::max<size_t>(1, (size_t)W * H * 3 * sizeof(float))));
@@ -1646,7 +1695,7 @@ int rtx_render_ppm(rtx_scene* s, const rtx_camera* cam, uint64_t seed, char* out
     if (!rgb || !text) return fail(RTX_ERR_OOM, "device buffers for a %ux%u PPM", W, H);
     rtx_region reg{0, 0, W, H, 0, 1};
     rtx_stats local;
-    int rc = rtx_render_region_device(s, cam, seed, &reg, rgb, st, 0, stats ? stats : &local);
+    int rc = render_region_locked(s, cam, seed, &reg, rgb, st, 0, stats ? stats : &local);
     uint64_t len = 0;
     if (rc == RTX_OK) rc = rtx_encode_ppm_device(rgb, W, H, text, need, &len, st);
     if (rc == RTX_OK && len > capacity) rc = fail(RTX_ERR_INVALID_ARG, "capacity %llu < PPM length %llu",

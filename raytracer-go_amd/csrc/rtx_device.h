@@ -461,12 +461,14 @@ struct Params {
     // next segment starts outside the near region [near_min, near_max] to the far pass, which walks
     // the guarded tree.  A path is handed over once, as a 64-B record at its segment start.
     uint32_t tier;          // 0: one walk; 1: the near pass; 2: the far pass (resumes the records)
-    uint32_t redo_only;     // 1: render the chunk only if the near pass overflowed its queue
     float near_min[3], near_max[3];
     float4* defer;          // the records: 4 float4 each (origin | pixel, dir | sample, thr | seg, acc | slot)
     uint32_t defer_cap;     // records the queue holds
     uint32_t* defer_count;  // records written (the far pass reads min(count, cap))
-    uint32_t* redo_flag;    // set when a record did not fit: the chunk's redo pass renders it whole
+    uint32_t* redo_flag;    // set when a record did not fit (the redo pass returns at once otherwise)
+    // one bit per scratch slot of the chunk, (k - k0) * n_tiles * 64 + pixel slot: a sample whose
+    // path did not fit the queue, rendered again from its camera ray by the redo pass (zeroed per chunk)
+    uint32_t* redo_bits;
 };
 
 struct Ray {
@@ -766,9 +768,12 @@ __device__ __forceinline__ float div_by(float n, float a, float y) {
 // the tie bvh.go:220-249 resolves for the sphere it meets first (the right subtree is clipped to the
 // left's hit, strictly).  A walk over another tree (rtx_topology.h) meets equal roots in another
 // order; this rule gives every order the reference's answer.  (A no-op on the reference's own order.)
-template <bool COUNT, bool SAFE = false, bool RANKED = false>
+// RANK_WORD (a layout in HBM, whose storage order is the hot set's): the same rule on the rank word
+// every sphere entry carries in b.y (ensure_layout: its place in the reference walk), the current
+// hit's read from bt = the 'b' halves — only on an exact tie.
+template <bool COUNT, bool SAFE = false, bool RANKED = false, bool RANK_WORD = false>
 __device__ __forceinline__ void sphere_test(Trav& t, const Ray& r, const float4 ea, const float4 eb, uint32_t pos,
-                                            Counters& cnt) {
+                                            Counters& cnt, const float4* __restrict__ bt = nullptr) {
     const float tmin = 0.001f;  // ray.go:37
     if (COUNT) ++cnt.prim_tests;
     const float ox = r.o.x - ea.x, oy = r.o.y - ea.y, oz = r.o.z - ea.z;  // :97
@@ -786,6 +791,8 @@ __device__ __forceinline__ void sphere_test(Trav& t, const Ray& r, const float4 
             ok = tmin < tt && tt < t.closest;
         }
         if (RANKED && tt == t.closest && entry_of(pos) < t.hit) ok = true;  // (t.hit = -1: no hit yet)
+        if (RANK_WORD && tt == t.closest && t.hit >= 0 && __float_as_uint(eb.y) < __float_as_uint(bt[t.hit].y))
+            ok = true;
         if (ok) {
             t.closest = tt;
             t.hit = entry_of(pos);
@@ -888,7 +895,7 @@ __device__ __forceinline__ void trav_step(Trav& t, const Ray& r, const SceneRef 
         box_step<COUNT, MED3>(t, r, ea, eb, tag, cnt);
     } else {
         if (QUADS && tag == RTX_E_QUAD) quad_test<COUNT>(t, r, E, ea, eb, t.i, cnt);
-        else sphere_test<COUNT, MED3, FIXED>(t, r, ea, eb, t.i, cnt);
+        else sphere_test<COUNT, MED3, FIXED, !FIXED>(t, r, ea, eb, t.i, cnt, E.b);
         t.i = (uint32_t)__float_as_int(eb.z);  // the primitive's successor
     }
 }
@@ -919,7 +926,7 @@ __device__ __forceinline__ uint32_t trav_step_batched(Trav& t, const Ray& r, con
         if (__builtin_amdgcn_inverse_ballot_w64(pm)) {  // = prim, as the vote's mask (no second compare)
             if (COUNT && HYB && t.i < E.hot) ++cnt.cache_hits;
             if (QUADS && tag == RTX_E_QUAD) quad_test<COUNT>(t, r, E, ea, eb, t.i, cnt);
-            else sphere_test<COUNT, MED3, FIXED>(t, r, ea, eb, t.i, cnt);
+            else sphere_test<COUNT, MED3, FIXED, !FIXED>(t, r, ea, eb, t.i, cnt, E.b);
             t.i = (uint32_t)__float_as_int(eb.z);
         }
     } else if (__builtin_amdgcn_inverse_ballot_w64(bm)) {  // lanes on a node (the sentinel's step is a no-op)

@@ -179,17 +179,18 @@ __device__ __forceinline__ void split_clk(uint64_t& acc, uint64_t& clk) {
 // TIER: 1 = the near pass of a tiered walk: a path whose next segment starts
 // outside the near region is written to the defer queue (its segment start: ray, throughput,
 // colour so far, pixel, sample, segment, scratch slot) and its lane takes a new item; 2 = the far
-// pass: the items are the queue's records, each resumed at its segment start on the guarded tree.
+// pass: the items are the queue's records, each resumed at its segment start on the far tree;
+// 3 = the redo pass: the samples whose record did not fit the queue (flagged in p.redo_bits)
+// rendered again from their camera rays on the far tree — it returns at once when none did.
 // Every sample's Philox blocks are keyed by (pixel, sample, event), so a path resumed in another
 // launch draws exactly what it would have drawn.
 template <bool COUNT, bool USE_LDS, bool QUADS, bool NOISE, int WAVES = 8, int MINW = 0, bool HYB = false,
           bool CLK = false, int TIER = 0>
 __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
     constexpr bool TIME = COUNT || CLK;
-    // the redo pass of a tiered chunk runs only when the near pass's queue overflowed
-    if (p.redo_only) {
+    if constexpr (TIER == 3) {
         if (__builtin_amdgcn_readfirstlane(*(volatile uint32_t*)p.redo_flag) == 0u) return;
-        if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&p.counters[24], 1ull);  // chunks redone
+        if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&p.counters[24], 1ull);  // chunks with a redo
     }
     // walk steps between two wave votes (A/B with primitive batching: 4 +0.7 %, 8 +0.8 %, 12 +1.3 %)
     constexpr uint32_t WAVE_BLOCK = 64 * WAVES, STEPS = RTX_WALK_STEPS;
@@ -243,6 +244,7 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
     if (TIER == 2 && blockIdx.x == 0 && threadIdx.x == 0 && n_rec)
         atomicAdd(&p.counters[23], (unsigned long long)n_rec);  // deferred paths, all chunks
     const size_t tile_floats = (size_t)n_tiles * 64 * 3;  // one sample of every tile (tile-major scratch)
+    const uint64_t* const redo64 = reinterpret_cast<const uint64_t*>(p.redo_bits);  // redo pass: 64 slots a word
 
     // the wave's unit (uniform, kept in SGPRs: every value below is derived from readfirstlane):
     // tile origin (u_x8, u_r8), first sample, items, next item
@@ -258,6 +260,7 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
     Trav t{};
     t.i = 16 * p.n_entries;  // on the sentinel until its first ray
     Counters cnt{0, 0, 0, 0, 0, 0};
+    Counters path0 = cnt;  // COUNT, near pass: the counters when the lane's sample began
     uint64_t wave_iters = 0, lane_steps = 0, shade_phases = 0, shade_lanes = 0;
     uint64_t trav_cycles = 0, shade_cycles = 0, clk = 0, idle_lanes = 0, parked = 0, deferred = 0;  // COUNT only
     uint64_t split[4] = {0, 0, 0, 0};  // COUNT: shading-phase cycles: scatter, shade, claims + camera rays, trav_begin
@@ -278,6 +281,7 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
         uint32_t b = 0;
         if (lane == 0) b = atomicAdd(p.defer_count, (uint32_t)__popcll(fm));
         b = __builtin_amdgcn_readfirstlane(b);
+        bool full = false;
         if (far) {
             const uint32_t slot = b + (uint32_t)__popcll(fm & ((1ull << lane) - 1ull));
             if (slot < p.defer_cap) {
@@ -287,10 +291,16 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
                 q[2] = make_float4(thr.x, thr.y, thr.z, __uint_as_float(seg));
                 q[3] = make_float4(acc.x, acc.y, acc.z, __uint_as_float((uint32_t)pix));
             } else {
-                atomicOr(p.redo_flag, 1u);  // the redo pass renders the chunk again, whole
+                // No room: the redo pass renders this sample again from its camera ray on the far tree
+                // (the same path: its Philox blocks are keyed by (pixel, sample, event)), and counts it.
+                const size_t bit = (size_t)(rng.sample - p.k0) * n_tiles * 64 + pix;
+                atomicOr(p.redo_bits + (bit >> 5), 1u << (uint32_t)(bit & 31u));
+                if (COUNT) cnt = path0;
+                full = true;
             }
             mode = M_CLAIM;
         }
+        if (ballot(full) != 0 && lane == 0) atomicOr(p.redo_flag, 1u);
     };
     auto defer_far = [&](bool& ready) {  // segments that would start outside the near region
         const bool far = ready && !(r.o.x >= p.near_min[0] && r.o.x <= p.near_max[0] && r.o.y >= p.near_min[1] &&
@@ -378,6 +388,10 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
                     const uint32_t cnt_k = min(p.sub, p.k0 + p.kn - u_k0);
                     u_items = 64u * cnt_k;
                     cursor = 0;
+                    if constexpr (TIER == 3) {  // a unit without a flagged sample: the next unit
+                        const bool any = lane < cnt_k && redo64[(size_t)(u_k0 + lane - p.k0) * n_tiles + u_tile] != 0;
+                        if (ballot(any) == 0) cursor = u_items;
+                    }
                 }
             }
             if (exhausted) {
@@ -402,18 +416,23 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
                 const uint32_t j = cursor + rank, l = j & 63u;  // sample-major within the unit
                 const uint32_t lx = u_x8 + (l & 7u);
                 const uint32_t lr = u_r8 + (l >> 3);
-                if (lx < p.width && lr < p.rows) {  // else: outside a ragged tile, claim again
+                const size_t slot = (size_t)((u_r8 >> 3) * tiles_x + (u_x8 >> 3)) * 64 + l;
+                const uint32_t k = u_k0 + (j >> 6);
+                // else: outside a ragged tile (or, redo pass, not flagged), claim again
+                if (lx < p.width && lr < p.rows &&
+                    (TIER != 3 || ((redo64[((size_t)(k - p.k0) * n_tiles * 64 + slot) >> 6] >> l) & 1ull))) {
                     const uint32_t x = p.x0 + lx, y = p.y0 + p.rank + lr * p.world;
                     base = pixel_base(c, x, y);
                     rng.pixel = y * c.image_width + x;
-                    rng.sample = u_k0 + (j >> 6);
-                    pix = (size_t)((u_r8 >> 3) * tiles_x + (u_x8 >> 3)) * 64 + l;
+                    rng.sample = k;
+                    pix = slot;
                     got = true;
                 }
             }
             const uint32_t taken = (uint32_t)__popcll(wm);
             cursor = cursor + taken > u_items ? u_items : cursor + taken;
             if (got) {
+                if (COUNT && TIER == 1) path0 = cnt;
                 r = camera_ray<!COUNT>(c, base, rng, rng.block(0u, 0u), cnt.draws);  // GetRay, camera.go:257
                 thr = v3(1.0f, 1.0f, 1.0f);
                 acc = v3(0.0f, 0.0f, 0.0f);
@@ -557,43 +576,51 @@ hipError_t launch_items(Params p, bool use_lds, hipStream_t stream) {
     return hipSuccess;
 }
 
-// The tiered walk of a sphere scene whose near and guarded layouts are both in
-// the LDS copy: per chunk the near pass (pn), the far pass over its queue (pf), the redo pass (pf
-// over the whole chunk; its waves return at once unless the queue overflowed), the reduction.
-template <bool COUNT, int WAVES, int MINW, bool CLK = false>
+// LDS bytes of a render_items launch: the fixed layout's whole scene (USE_LDS), the hot entries of a
+// scene in HBM (HYB), or none.
+inline size_t items_shmem(const Params& p, bool use_lds, bool hyb) {
+    return use_lds ? lds_fixed_bytes(p.n_entries, p.n_quads, p.n_materials, p.n_textures)
+                   : (hyb ? lds_hot_bytes(p.n_hot) : 0);
+}
+
+// The tiered walk of a sphere scene whose near and far layouts are placed alike —
+// both in the LDS copy (USE_LDS), both in HBM with an LDS cache of their hot entries (HYB), or both
+// in HBM: per chunk the near pass (pn), the far pass over its queue (pf), the redo pass over the
+// samples whose records did not fit (its waves return at once when none), the reduction.
+template <bool COUNT, int WAVES, int MINW, bool CLK = false, bool USE_LDS = true, bool HYB = false>
 hipError_t launch_tiered(Params pn, Params pf, hipStream_t stream) {
-    const auto kn = render_items<COUNT, true, false, false, WAVES, MINW, false, CLK, 1>;
-    const auto kf = render_items<COUNT, true, false, false, WAVES, MINW, false, CLK, 2>;
-    const auto kr = render_items<COUNT, true, false, false, WAVES, MINW, false, false, 0>;
-    const size_t sn = lds_fixed_bytes(pn.n_entries, 0, pn.n_materials, pn.n_textures);
-    const size_t sf = lds_fixed_bytes(pf.n_entries, 0, pf.n_materials, pf.n_textures);
+    const auto kn = render_items<COUNT, USE_LDS, false, false, WAVES, MINW, HYB, CLK, 1>;
+    const auto kf = render_items<COUNT, USE_LDS, false, false, WAVES, MINW, HYB, CLK, 2>;
+    const auto kr = render_items<COUNT, USE_LDS, false, false, WAVES, MINW, HYB, false, 3>;
+    const size_t sn = items_shmem(pn, USE_LDS, HYB), sf = items_shmem(pf, USE_LDS, HYB);
     constexpr int block = 64 * WAVES;
-    int cus = 0, per_n = 0, per_f = 0;
+    int cus = 0, per_n = 0, per_f = 0, per_r = 0;
     hipError_t e = resident_grid((const void*)kn, block, sn, &per_n, &cus);
     if (e == hipSuccess) e = resident_grid((const void*)kf, block, sf, &per_f, &cus);
+    if (e == hipSuccess) e = resident_grid((const void*)kr, block, sf, &per_r, &cus);
     if (e != hipSuccess) return e;
     const uint32_t spp = pn.cam.samples_per_pixel, chunk = pn.kn, sub = pn.sub;
     const uint64_t tiles = (uint64_t)((pn.width + 7) / 8) * ((pn.rows + 7) / 8);
     const uint64_t slots = tiles * 64;
-    Params pr = pf;  // the redo pass: the far layout over the chunk's units
+    Params pr = pf;  // the redo pass: the far layout over the chunk's units, flagged samples only
     pr.tier = 0;
-    pr.redo_only = 1;
-    pf.redo_only = 0;
     for (uint32_t k0 = 0; k0 < spp; k0 += chunk) {
         pn.k0 = pf.k0 = pr.k0 = k0;
         pn.kn = pf.kn = pr.kn = spp - k0 < chunk ? spp - k0 : chunk;
         pn.sub = sub ? sub : unit_samples(tiles, pn.kn, WAVES, per_n, cus);
         pf.sub = pr.sub = pn.sub;
         const uint64_t units = tiles * ((pn.kn + pn.sub - 1) / pn.sub);
-        uint64_t bn = (uint64_t)per_n * cus, br = (uint64_t)per_f * cus;
+        uint64_t bn = (uint64_t)per_n * cus, br = (uint64_t)per_r * cus;
         if (bn > (units + WAVES - 1) / WAVES) bn = (units + WAVES - 1) / WAVES;
         if (br > (units + WAVES - 1) / WAVES) br = (units + WAVES - 1) / WAVES;
         if (pn.debug_launch)
-            fprintf(stderr, "rtx tiered: waves/wg %d, wgs/CU %d / %d, grid %llu, sub %u, units %llu, lds %zu / %zu B, cap %u\n",
-                    WAVES, per_n, per_f, (unsigned long long)bn, pn.sub, (unsigned long long)units, sn, sf, pn.defer_cap);
-        // the unit queue head, and the chunk's record count + overflow flag (one u64 slot)
+            fprintf(stderr, "rtx tiered: waves/wg %d, wgs/CU %d / %d / %d, grid %llu, sub %u, units %llu, lds %zu / %zu B, "
+                    "cap %u\n", WAVES, per_n, per_f, per_r, (unsigned long long)bn, pn.sub, (unsigned long long)units, sn,
+                    sf, pn.defer_cap);
+        // the unit queue head, the chunk's record count + overflow flag (one u64 slot), its redo bits
         if ((e = hipMemsetAsync(pn.tile_counter, 0, sizeof(uint32_t), stream)) != hipSuccess) return e;
         if ((e = hipMemsetAsync(pn.defer_count, 0, 2 * sizeof(uint32_t), stream)) != hipSuccess) return e;
+        if ((e = hipMemsetAsync(pn.redo_bits, 0, (size_t)pn.kn * tiles * 8, stream)) != hipSuccess) return e;
         hipLaunchKernelGGL(kn, dim3((uint32_t)bn), dim3(block), sn, stream, pn);
         if ((e = hipMemsetAsync(pf.tile_counter, 0, sizeof(uint32_t), stream)) != hipSuccess) return e;
         hipLaunchKernelGGL(kf, dim3((uint32_t)per_f * cus), dim3(block), sf, stream, pf);
@@ -639,18 +666,31 @@ uint32_t scene_placement(const Params& p, uint32_t flags) {
     return p.n_hot > 0 && !p.has_noise ? RTX_SCENE_LDS_CACHE : RTX_SCENE_IN_HBM;
 }
 
+uint32_t tier_placement(const Params& near, const Params& far, uint32_t flags) {
+    const uint32_t a = scene_placement(near, flags), b = scene_placement(far, flags);
+    return a == b ? a : 0u;
+}
+
 hipError_t launch_render(const Params& p, uint32_t flags, hipStream_t stream, const Params* far) {
     if (p.width == 0 || p.rows == 0) return hipSuccess;
     if (!p.scratch) return hipErrorInvalidValue;  // the caller sizes the sample scratch
     const bool count = (flags & RTX_FLAG_COUNTERS) != 0;
-    if (far) {  // the caller checked: spheres only, both layouts in the LDS copy, no noise
-        if (p.tier != 1 || far->tier != 2 || !p.defer || !far->defer || p.n_quads || p.has_noise ||
-            scene_placement(p, flags) != RTX_SCENE_IN_LDS || scene_placement(*far, flags) != RTX_SCENE_IN_LDS)
+    if (far) {  // the caller checked: spheres only, both layouts placed alike (tier_placement), no noise
+        const uint32_t place = tier_placement(p, *far, flags);
+        if (p.tier != 1 || far->tier != 2 || !p.defer || !far->defer || !p.redo_bits || p.n_quads || p.has_noise ||
+            place == 0)
             return hipErrorInvalidValue;
-        if (!count && (flags & RTX_FLAG_TIMING))  // diagnostics: the wave-cycle split of both passes
-            return launch_tiered<false, RTX_V3_WAVES, RTX_V3_MINW, true>(p, *far, stream);
-        return count ? launch_tiered<true, RTX_V3_WAVES, 0>(p, *far, stream)
-                     : launch_tiered<false, RTX_V3_WAVES, RTX_V3_MINW>(p, *far, stream);
+        const bool clk = !count && (flags & RTX_FLAG_TIMING);  // diagnostics: the wave-cycle split of the passes
+        if (place == RTX_SCENE_IN_LDS) {
+            if (clk) return launch_tiered<false, RTX_V3_WAVES, RTX_V3_MINW, true>(p, *far, stream);
+            return count ? launch_tiered<true, RTX_V3_WAVES, 0>(p, *far, stream)
+                         : launch_tiered<false, RTX_V3_WAVES, RTX_V3_MINW>(p, *far, stream);
+        }
+        if (place == RTX_SCENE_LDS_CACHE)  // both caches of 64 KB (tier_placement): 12-wave workgroups, two per CU
+            return count ? launch_tiered<true, RTX_HYB_WAVES, 0, false, false, true>(p, *far, stream)
+                         : launch_tiered<false, RTX_HYB_WAVES, RTX_HYB_MINW, false, false, true>(p, *far, stream);
+        return count ? launch_tiered<true, RTX_V3_WAVES, 0, false, false, false>(p, *far, stream)
+                     : launch_tiered<false, RTX_V3_WAVES, RTX_V3_MINW, false, false, false>(p, *far, stream);
     }
     const bool use_lds = scene_placement(p, flags) == RTX_SCENE_IN_LDS;
     if (!count && (flags & RTX_FLAG_TIMING) && !p.has_noise && p.item_waves != 4)  // diagnostics: sphere scenes

@@ -62,15 +62,22 @@ bool build_topology(const std::vector<rtx_entry>& ref, bool guarded, Topology& o
 // the scene has no finite core.
 bool near_region(const std::vector<rtx_entry>& ref, float box[6], double grow = 1.0);
 
-// How far outside a sphere (centre c, radius r) the float32 sphere test can put a hit for a ray
-// origin at distance <= dmax from c: sqrt(r^2 + 2^-17 (dmax^2 + r^2)) - r, plus 2^-20 (dmax + r)
-// for the rounding of the slab test.  (The test's error in |P - c|^2 - r^2 is K eps (dmax^2 + r^2)
-// with K <= 9.5 measured over 4e7 near-tangent rays; 2^-17 = 128 eps.)
+// How far outside a sphere (centre c, radius r) the float32 sphere test (hittables.go:96-116) can
+// put a hit for a ray origin at distance <= dmax from c, with room for the slab test's rounding:
+// rho - r + 2^-20 (dmax + rho), rho = sqrt(r^2 + 24u (dmax^2 + r^2)), u = 2^-24 — the forward-error
+// bound derived in DESIGN.md §14 (the computed discriminant is within 24u |d|^2 (D^2 + r^2) of the
+// exact one; the measured worst case over 4e7 near-tangent rays is 9.5u).
 double sphere_margin(double r, double dmax);
 
 // Whether the scene's spheres are small against the float32 sphere test's error (see the .hip):
 // the gate of the default (guarded) rebuild.
 bool precise_enough(const std::vector<rtx_entry>& ref);
+
+// Whether every node box of the caller's walk `ref` contains the own box (NewSphere's NewAabb,
+// hittables.go:85-94) of every sphere below it, and the scene holds spheres only: the tiered walk's
+// hit check accepts a near-tree hit by testing the sphere's own box in place of every
+// box the far walk would test above it.  NewBVH's nodes always qualify (NewAabbFromBoxes, bvh.go:44-50).
+bool own_boxes_nested(const std::vector<rtx_entry>& ref);
 
 // The node table of `t` as walked for camera octant `oct` (bit k: the viewing direction is
 // negative along axis k): at every SAH node the child on the near side of its split along the

@@ -228,6 +228,30 @@ bool precise_enough(const std::vector<rtx_entry>& ref) {
     return rmin > 0.0 && std::ldexp(d2, -24) / (rmin * rmin) < std::ldexp(1.0, -7);
 }
 
+bool own_boxes_nested(const std::vector<rtx_entry>& ref) {
+    std::vector<uint32_t> open;  // the nodes whose subtree holds entry i (host layout: a[3] = escape index)
+    bool any = false;
+    for (uint32_t i = 0; i < ref.size(); ++i) {
+        while (!open.empty() && (uint32_t)word(&ref[open.back()].a[3]) <= i) open.pop_back();
+        const int32_t tag = tag_of(ref[i]);
+        if (tag == RTX_E_NODE) {
+            open.push_back(i);
+            continue;
+        }
+        if (tag < 0) return false;  // a quad
+        any = true;
+        const rtx_entry& e = ref[i];
+        for (int k = 0; k < 3; ++k) {
+            const float p1 = e.a[k] + (e.a[3] * -1.0f), p2 = e.a[k] + e.a[3];
+            const float mn = go_min(p1, p2), mx = go_max(p1, p2);
+            if (!(mn == mn) || !(mx == mx)) return false;
+            for (uint32_t n : open)
+                if (!(ref[n].a[k] <= mn && ref[n].b[k] >= mx)) return false;
+        }
+    }
+    return any;
+}
+
 bool near_region(const std::vector<rtx_entry>& ref, float box[6], double grow) {
     Box b;
     double rmin = 0.0;
@@ -243,8 +267,12 @@ bool near_region(const std::vector<rtx_entry>& ref, float box[6], double grow) {
     return true;
 }
 
+// The forward-error bound of DESIGN.md §14 (u = 2^-24): a computed disc >= 0 puts the ray's line
+// within rho = sqrt(r^2 + 24u (D^2 + r^2)) of the centre, and the reported root's point within
+// rho + 11u D + 7u rho of it; the slab test of the grown box passes it with 3u (D + r + m) to spare.
 double sphere_margin(double r, double dmax) {
-    return std::sqrt(r * r + std::ldexp(dmax * dmax + r * r, -17)) - r + std::ldexp(dmax + r, -20);
+    const double rho = std::sqrt(r * r + 3.0 * std::ldexp(dmax * dmax + r * r, -21));  // 24u = 3 * 2^-21
+    return rho - r + std::ldexp(dmax + rho, -20);                                      // + 16u (D + rho)
 }
 
 bool build_topology(const std::vector<rtx_entry>& ref, bool guarded, Topology& out, const float* near_box) {

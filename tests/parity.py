@@ -82,7 +82,7 @@ def oracle_checks(desc, walk, cam, seed, reg, skip=None, tier=None):
 
 def check_scene(torch, dev, desc, cam, seed, reg, flags=0, kernels=("timed", "counting")):
     """Checks 1-3 for both kernels on one region; returns (timed image, counting stats, oracle counters)."""
-    tier = tier_of(dev, desc, cam) if not flags & rtx.RTX_FLAG_NO_LDS else None
+    tier = tier_of(dev, desc, cam)
     if tier is not None:
         walk, skip, tw = tier
     else:

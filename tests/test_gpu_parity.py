@@ -390,38 +390,86 @@ def test_every_camera_octant(torch_cuda, spheres, dev_spheres, octant):
     assert st.walk_layout & ~rtx.RTX_LAYOUT_TIERED == octant
 
 
-@pytest.mark.parametrize("name,stride", [("C2", 36), ("C4", 36)])
-def test_config_rows_vs_oracle(torch_cuda, built, name, stride):
-    """Every `stride`-th row of the whole BASELINE frame (C2: 1920x1080x500 on the rebuilt tree; C4:
-    1920x1080x100 on the reference's), rendered by the timed kernel as part of the full frame, against
-    the oracle walking the CALLER's tree (iterative colour order): bit-identical."""
-    scene, width, spp, _ = CONFIGS[name]
+# BASELINE configs at their own parameters: (scene, width, spp, row stride, pixels of the sampled rows
+# allowed to differ from the caller's tree).  C5's rebuilt (guarded) tree differs from the caller's at
+# paths trapped inside the r = 1000 ground sphere (one pixel of 8.3 M on the whole frame,
+# by 3.0e-8); every such pixel must still be the walked tree's oracle value bit for bit.
+ROW_CONFIGS = {
+    "C1": ("random_spheres", 400, 100, 1, 0),
+    "C2": ("random_spheres", 1920, 500, 36, 0),
+    "C3": ("random_spheres", 1920, 2000, 72, 0),
+    "C4": ("stress_100k", 1920, 100, 36, 0),
+    "C5": ("earth_dielectric", 3840, 1000, 72, 4),
+}
+
+
+@pytest.mark.parametrize("name", list(ROW_CONFIGS))
+def test_config_rows_vs_oracle(torch_cuda, built, name):
+    """Every `stride`-th row (C1: every row) of the whole BASELINE frame at its own parameters — C1
+    400x225x100, C2 1920x1080x500, C3 1920x1080x2000 (>= 3 sample chunks), C4 1920x1080x100 (100k
+    spheres), C5 3840x2160x1000 (image texture, 35 % Dielectric, defocus, 6 sample chunks) — rendered by
+    the timed kernel as part of the full frame and held to the oracle walking the CALLER's tree (16
+    threads): bit-identical to its iterative colour order (but for C5's documented trapped-path class,
+    counted and each equal to the walked tree's oracle), and within 1e-4 of the reference order."""
+    scene, width, spp, stride, allowed = ROW_CONFIGS[name]
     s = rtx.HostScene(scene, 1)
     dev = rtx.DeviceScene(s.desc)
     cam = s.camera(width=width, spp=spp)
-    H = cam.image_height
-    gpu, _ = gpu_region(torch_cuda, dev, cam, 2024, rtx.Region(0, 0, width, H, 0, 1), counters=False)
-    rows = rtx.Region(0, 0, width, H, 7 % stride, stride)  # rows 7, 7 + stride, ...
-    it, _ = ob.render(s.desc, cam, 2024, rows, ob.ORDER_ITERATIVE)
+    W, H = cam.image_width, cam.image_height
+    assert cam.samples_per_pixel == spp and cam.max_depth == 50
+    gpu, st = gpu_region(torch_cuda, dev, cam, 2024, rtx.Region(0, 0, W, H, 0, 1), counters=False)
+    assert st.redo_chunks == 0
+    if name == "C3":
+        assert st.sample_chunks >= 3, st.sample_chunks
+    if name == "C5":
+        assert st.sample_chunks >= 6, st.sample_chunks
+    rows = rtx.Region(0, 0, W, H, 7 % stride, stride)  # rows 7, 7 + stride, ... (C1: all)
     want = gpu[rows.rank::stride]
+    it, _ = ob.render(s.desc, cam, 2024, rows, ob.ORDER_ITERATIVE, threads=16)
     bad = np.argwhere((want != it).any(axis=2))
-    assert len(bad) == 0, (len(bad), bad[:8].tolist(), float(np.abs(want - it).max()))
+    assert len(bad) <= allowed, (len(bad), bad[:8].tolist(), float(np.abs(want - it).max()))
+    if len(bad):
+        from parity import tier_of, walk_of
+
+        tier = tier_of(dev, s.desc, cam)
+        walk, skip, tw = tier if tier is not None else (*walk_of(dev, s.desc, cam), None)
+        rank = ob.sphere_ranks(s.desc)
+        for i, x in bad.tolist():
+            y = rows.rank + i * stride
+            px, _ = ob.render(walk, cam, 2024, rtx.Region(int(x), y, 1, 1, 0, 1), ob.ORDER_ITERATIVE, skip=skip,
+                              tier=tw, rank=rank)
+            assert np.array_equal(px[0, 0], want[i, x]), ((x, y), px[0, 0], want[i, x])
+            assert float(np.abs(want[i, x] - it[i, x]).max()) <= 1e-6
+    ref, _ = ob.render(s.desc, cam, 2024, rows, ob.ORDER_REFERENCE, threads=16)
+    d = float(np.abs(want - ref).max())
+    assert d <= TOL, d
+    print(f"{name}: {want.shape[0]} rows x {W} px x {spp} spp vs the oracle, {len(bad)} trapped-path pixels, "
+          f"max |delta| vs the reference order {d:.2e}")
 
 
-@pytest.mark.parametrize("cap", [0, 64])
+@pytest.mark.parametrize("cap", [0, 64, 1000])
 def test_tier_queue_overflow_redo(torch_cuda, spheres, dev_spheres, monkeypatch, cap):
     """The tiered walk's queue of deferred paths too small for the chunk
-    (RTX_DEFER_CAP): the redo pass renders the chunk again, whole, on the guarded tree — the same
-    image, bit for bit, as the oracle on the caller's tree and as the render with room."""
+    (RTX_DEFER_CAP): the samples whose records do not fit are flagged and rendered again from their
+    camera rays on the guarded tree by the redo pass — the same image, bit for bit, as the oracle on
+    the caller's tree and as the render with room, from both kernels; the counting kernel's path
+    counters (samples, segments, hits, texel fetches, draws) equal the oracle's: the near pass's work
+    on a flagged sample is taken back and the redo pass counts it."""
     cam = spheres.camera(width=160, spp=12, depth=50)
     reg = rtx.Region(0, 0, cam.image_width, cam.image_height, 0, 1)
-    want, _ = gpu_region(torch_cuda, dev_spheres, cam, 21, reg, counters=False)
-    it, _ = ob.render(spheres.desc, cam, 21, reg, ob.ORDER_ITERATIVE)
+    want, st0 = gpu_region(torch_cuda, dev_spheres, cam, 21, reg, counters=True)
+    it, cnt = ob.render(spheres.desc, cam, 21, reg, ob.ORDER_ITERATIVE)
     assert np.array_equal(want, it)
+    assert st0.redo_chunks == 0 and st0.deferred_paths > 1000
     monkeypatch.setenv("RTX_DEFER_CAP", str(cap))
-    got, st = gpu_region(torch_cuda, dev_spheres, cam, 21, reg, counters=False)
-    assert st.walk_layout & rtx.RTX_LAYOUT_TIERED and st.redo_chunks == 1
-    assert np.array_equal(got, want)
+    for counters in (False, True):
+        got, st = gpu_region(torch_cuda, dev_spheres, cam, 21, reg, counters=counters)
+        assert st.walk_layout & rtx.RTX_LAYOUT_TIERED and st.redo_chunks == 1
+        assert np.array_equal(got, want), (counters, int((got != want).any(axis=2).sum()))
+        if counters:
+            for k in ("samples", "segments", "hits", "texel_fetches", "rng_draws"):
+                assert getattr(st, k) == cnt[k], (k, getattr(st, k), cnt[k])
+            assert st.deferred_paths == min(cap, st0.deferred_paths)
 
 
 def test_tier_deferred_paths_c2_crop(torch_cuda, spheres, dev_spheres):

@@ -146,11 +146,13 @@ def test_band_assembly_index_math_one_gpu(built, bands):
         "s = rtx.HostScene('random_spheres', 1); d = rtx.DeviceScene(s.desc)\n"
         "cam = s.camera(width=200, spp=3)\n"
         "assert cam.image_height == 112\n"
-        "a, sa = d.render_host(cam, 9, stats=True)\n"
+        "a, sa = d.render_host(cam, 9, counters=True)\n"
         "os.environ['RTX_SIM_BANDS'] = str(k)\n"
-        "b, sb = d.render_host(cam, 9, stats=True)\n"
+        "b, sb = d.render_host(cam, 9, counters=True)\n"
         "assert np.array_equal(a, b), 'device gather differs'\n"
-        "assert sb.gather_kind == rtx.RTX_GATHER_DEVICE and sb.samples == sa.samples, sb.gather_kind\n"
+        "assert sb.gather_kind == rtx.RTX_GATHER_DEVICE, sb.gather_kind\n"
+        "for f in ('samples', 'segments', 'node_visits', 'prim_tests', 'hits', 'rng_draws'):  # every band's\n"
+        "    assert getattr(sa, f) == getattr(sb, f), (f, getattr(sa, f), getattr(sb, f))\n"
         "os.environ['RTX_NO_RCCL'] = '1'\n"
         "c, sc = d.render_host(cam, 9, stats=True)\n"
         "assert np.array_equal(a, c), 'host band copies differ'\n"
@@ -188,3 +190,30 @@ def test_rtx_render_stats_run_the_timed_kernel(built):
         "assert abs(free1 - free0) < (16 << 20), (free0, free1)  # no new buffers per call\n"
         "print('ok', k, min(t), sb.kernel_ms)\n")
     assert out.split()[0] == "ok"
+
+
+def test_render_and_ppm_concurrently(built):
+    """rtx_render and rtx_render_ppm on one scene from two threads at once (both take the scene's lock,
+    then the render buffers' lock, in that order): no deadlock, and every result is the one a lone call
+    gives."""
+    out = child(
+        "import threading\n"
+        "s = rtx.HostScene('random_spheres', 1); d = rtx.DeviceScene(s.desc)\n"
+        "cam = s.camera(width=160, spp=2)\n"
+        "img0, _ = d.render_host(cam, 3)\n"
+        "ppm0 = d.render_ppm(cam, 3)\n"
+        "bad = []\n"
+        "def a():\n"
+        "    for _ in range(25):\n"
+        "        img, _ = d.render_host(cam, 3)\n"
+        "        bad.append(not np.array_equal(img, img0))\n"
+        "def b():\n"
+        "    for _ in range(25):\n"
+        "        bad.append(d.render_ppm(cam, 3) != ppm0)\n"
+        "ts = [threading.Thread(target=a), threading.Thread(target=b)]\n"
+        "[t.start() for t in ts]\n"
+        "[t.join(60) for t in ts]\n"
+        "assert not any(t.is_alive() for t in ts), 'deadlock'\n"
+        "assert len(bad) == 50 and not any(bad)\n"
+        "print('ok')\n", timeout=100)
+    assert out.strip().endswith("ok")
