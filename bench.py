@@ -52,8 +52,17 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0, help="0: the host's CPU share per GPU")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-hash", action="store_true", help="skip the framebuffer hash")
-    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_r03.json"))
-    ap.add_argument("--valu", default=os.path.join(ROOT, "profiles", "valu_r03.json"))
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_r04.jsonl"),
+                    help="PMC HBM-traffic summaries (scripts/pmc_traffic.py): a .json, or a .jsonl of one per workload")
+    ap.add_argument("--valu", default=os.path.join(ROOT, "profiles", "valu_r04.jsonl"),
+                    help="PMC VALU summaries (scripts/pmc_valu.py): a .json, or a .jsonl of one per workload")
+    ap.add_argument("--shard", default="", help="R/N: one process renders only rank R's rows of N (a rank's "
+                    "workload of the N-GPU run, for its PMC profile); not a scaling number")
+    ap.add_argument("--in-process", action="store_true",
+                    help="one process drives --gpus N devices through rtx_render(n_gpus = N): the C-ABI's own "
+                         "band render + ncclGather + de-interleave + copy into a host buffer (what a Go host calls)")
+    ap.add_argument("--no-in-process", action="store_true",
+                    help="N > 1 under torch.distributed: skip rank 0's in-process leg after the timed steps")
     # launcher self-test on the CPU (tests/test_bench_launcher.py): gloo, no GPU, shards filled
     # with a known function of the global pixel instead of rendered
     ap.add_argument("--rehearse-one-gpu", action="store_true",
@@ -196,13 +205,19 @@ def load_profile(path: str, workload: str, lib: str):
     if not os.path.exists(path):
         return None, f"{os.path.relpath(path, ROOT)} missing"
     with open(path) as f:
-        d = json.load(f)
-    if d.get("workload") != workload:
-        return None, f"{os.path.relpath(path, ROOT)} is for {d.get('workload')}, not {workload}"
-    if d.get("librtx_sha256_16") != lib:
-        return None, (f"{os.path.relpath(path, ROOT)} was measured on librtx {d.get('librtx_sha256_16')}, "
-                      f"this run loads {lib}: stale, frac not derived")
-    return d, None
+        if path.endswith(".jsonl"):
+            entries = [json.loads(ln) for ln in f if ln.strip()]
+        else:
+            entries = [json.load(f)]
+    same = [d for d in entries if d.get("workload") == workload]
+    if not same:
+        return None, f"{os.path.relpath(path, ROOT)} has no profile of {workload}"
+    for d in same:
+        if d.get("librtx_sha256_16") == lib:
+            return d, None
+    return None, (f"{os.path.relpath(path, ROOT)} profiled {workload} on librtx "
+                  f"{', '.join(sorted({str(d.get('librtx_sha256_16')) for d in same}))}, this run loads {lib}: "
+                  "stale, frac not derived")
 
 
 def served_from(st: dict) -> str:
@@ -286,6 +301,8 @@ def framebuffer_hash(img) -> str:
 # ---- the run -------------------------------------------------------------------------------
 def main():
     args = parse()
+    if args.in_process:
+        return main_in_process(args)
     if args.gpus > 1 and "RANK" not in os.environ:
         sys.exit(launch_ranks(args.gpus))  # before anything touches a GPU
     import torch
@@ -319,8 +336,12 @@ def main():
     dev = rtx.DeviceScene(scene.desc)  # one-time upload to this rank's HBM
     skips = dev.walk_skip(cam)  # the walk's plan for this camera (rtx_collapse.h), made before timing
     near_skips = dev.near_skip(cam) if dev.near_region(cam)[1] else None  # the tiered walk's near tree (§14)
-    reg = rtx.Region(0, 0, W, H, rank, world)
-    R = max_shard_rows(H, world)
+    # the rows this process renders: its rank's of the world, or (--shard R/N) one rank's of N alone
+    srank, sworld = (int(v) for v in args.shard.split("/")) if args.shard else (rank, world)
+    if world > 1 and args.shard:
+        raise SystemExit("--shard is a one-process run")
+    reg = rtx.Region(0, 0, W, H, srank, sworld)
+    R = max_shard_rows(H, sworld)
     shard = torch.zeros((R, W, 3), dtype=torch.float32, device="cuda")
     stream = torch.cuda.current_stream().cuda_stream
 
@@ -342,7 +363,8 @@ def main():
         s = dev.render_region(cam, args.seed, reg, shard.data_ptr(), stream, counters=False, timed=True)
         times.append(s.kernel_ms)
         g0 = time.perf_counter()  # (render_region waited for this rank's kernel)
-        out = gather_image(shard.cpu() if shared else shard, H, rank, world)
+        out = shard[:rtx.region_rows(reg)] if args.shard else gather_image(shard.cpu() if shared else shard, H, rank,
+                                                                                world)
         if world > 1 and out is not None and not shared:
             torch.cuda.synchronize()
         gathers.append((time.perf_counter() - g0) * 1e3)
@@ -370,7 +392,7 @@ def main():
     rank_kms = [float(x.item()) for x in per_rank]
 
     if rank == 0:
-        assert img is not None and tuple(img.shape) == (H, W, 3)
+        assert img is not None and tuple(img.shape) == ((rtx.region_rows(reg), W, 3) if args.shard else (H, W, 3))
         ms_step = elapsed / args.steps * 1e3
         mray = tot["segments"] * args.steps / elapsed / 1e6
         samples_s = tot["samples"] * args.steps / elapsed
@@ -382,7 +404,11 @@ def main():
         tag = " (configs[1])" if headline else (" (configs[2])" if c3 else "")
         if shared:
             metric = f"rehearsal: {world} ranks sharing one GPU, gloo gather (not a scaling number); " + metric
-        profile_workload = f"{args.scene}:{W}x{H}x{S}"
+        if args.shard:
+            metric = f"shard {srank}/{sworld} alone (rank {srank}'s rows of an {sworld}-GPU run; not a scaling number); " + metric
+        # the PMC profile of this process's own workload: the frame, or its rank's rows of an N-way run
+        # (profiled alone with --shard R/N)
+        profile_workload = f"{args.scene}:{W}x{H}x{S}" + (f"/rows{srank}of{sworld}" if sworld > 1 else "")
         out = {
             "metric": metric,
             "value": round(mray, 3),
@@ -414,21 +440,93 @@ def main():
             "walk_layout": walk_desc(st, skips, near_skips),
             "prim_tests_per_segment": round(tot["prim_tests"] / tot["segments"], 3),
             "schedule": schedule(st),
-            "roofline": roofline(st, my_rows * W, avg_kernel_s, profile_workload if world == 1 else "-",
-                                 args.traffic, args.valu),
+            "roofline": roofline(st, my_rows * W, avg_kernel_s, profile_workload, args.traffic, args.valu),
         }
+        if sworld > 1:
+            out["roofline"]["scope"] = (f"rank {srank}'s kernel on its own rows ({my_rows} of {H}), against the PMC "
+                                        f"profile of that shard rendered alone (bench.py --shard {srank}/{sworld})")
         if world > 1:  # rank 0's wall time in the gather (incl. waiting for the slowest rank)
             out["gather_ms_avg"] = round(sum(gms) / len(gms), 3)
             out["kernel_ms_per_rank"] = {"min": round(min(rank_kms), 3), "max": round(max(rank_kms), 3),
                                          "all": [round(x, 3) for x in rank_kms]}
         if not args.no_hash:
             out["framebuffer_sha256_16"] = framebuffer_hash(img)  # bitwise-comparable across N
-        if world == 1 and not args.no_cpu:
+        if world == 1 and not args.no_cpu and not args.shard:
             out["cpu_baseline"] = cpu_baseline(scene, cam, args.seed, args.cpu_target_s, args.cpu_threads)
-        print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+    if rank == 0:
+        if world > 1 and not shared and not args.no_in_process:
+            out["in_process"] = in_process_leg(args, world)
+        print(json.dumps(out), flush=True)
+
+
+def in_process_leg(args, n: int) -> dict:
+    """Rank 0, after the ranks' timed steps: the same workload through the C-ABI's own N-device path
+    (rtx_render(n_gpus = N): bands on devices 0..N-1, one ncclGather to device 0, the de-interleave
+    kernel, the copy into a host buffer) in a child process with a time limit — the path a Go host
+    takes, timed by the same driver run."""
+    keep = ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK", "MASTER_ADDR",
+            "MASTER_PORT", "TORCHELASTIC_RUN_ID")
+    env = {k: v for k, v in os.environ.items() if k not in keep}
+    cmd = [sys.executable, os.path.abspath(__file__), "--in-process", "--gpus", str(n), "--steps", str(args.steps),
+           "--warmup", str(max(1, args.warmup)), "--width", str(args.width), "--spp", str(args.spp), "--depth",
+           str(args.depth), "--scene", args.scene, "--scene-seed", str(args.scene_seed), "--seed", str(args.seed)]
+    try:
+        res = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
+        lines = [ln for ln in res.stdout.splitlines() if ln.startswith("{")]
+        if res.returncode != 0 or not lines:
+            return {"error": f"exit {res.returncode}: {(res.stderr or res.stdout)[-400:]}"}
+        return json.loads(lines[-1])
+    except subprocess.TimeoutExpired:
+        return {"error": "timed out after 600 s"}
+
+
+def main_in_process(args):
+    """--in-process: one process, --gpus N devices, rtx_render(n_gpus = N) timed per step (render of
+    every band + RCCL gather + de-interleave + copy into this process's host buffer).  Counts come from
+    one untimed rtx_render_ex(RTX_FLAG_COUNTERS) over the same devices."""
+    import numpy as np
+    import torch  # (before librtx.so: one HIP runtime per process, DESIGN.md §6)
+
+    import rtx
+
+    n = args.gpus
+    assert torch.cuda.device_count() >= n, f"--in-process --gpus {n}: {torch.cuda.device_count()} devices visible"
+    scene = rtx.HostScene(args.scene, seed=args.scene_seed)
+    cam = scene.camera(width=args.width, spp=args.spp, depth=args.depth)
+    W, H, S = cam.image_width, cam.image_height, cam.samples_per_pixel
+    dev = rtx.DeviceScene(scene.desc)
+    buf = np.zeros((H, W, 3), dtype=np.float32)
+    _, st = dev.render_host(cam, args.seed, n_gpus=n, counters=True, out=buf)
+    for _ in range(args.warmup):
+        dev.render_host(cam, args.seed, n_gpus=n, stats=True, out=buf)
+    kms, gms = [], []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        _, s = dev.render_host(cam, args.seed, n_gpus=n, stats=True, out=buf)
+        kms.append(s.kernel_ms)
+        gms.append(s.gather_ms)
+    elapsed = time.perf_counter() - t0
+    out = {
+        "metric": f"Mray/s on {W}x{H}x{S}spp {args.scene}, one process driving {n} GPUs (rtx_render)",
+        "value": round(st.segments * args.steps / elapsed / 1e6, 3),
+        "unit": "Mray/s",
+        "n_gpus": n,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "gsamples_per_s": round(st.samples * args.steps / elapsed / 1e9, 4),
+        "kernel_ms_max_band_avg": round(sum(kms) / len(kms), 3),
+        "gather_ms_avg": round(sum(gms) / len(gms), 3),
+        "gather_kind": {rtx.RTX_GATHER_NONE: "none", rtx.RTX_GATHER_RCCL: "rccl", rtx.RTX_GATHER_HOST: "host copies",
+                        rtx.RTX_GATHER_DEVICE: "device copies"}.get(s.gather_kind, str(s.gather_kind)),
+        "step": "every band's render on its device + ncclGather to device 0 + de-interleave + copy to the host "
+                "buffer (24.9 MB at 1920x1080 over PCIe)",
+        "framebuffer_sha256_16": hashlib.sha256(np.ascontiguousarray(buf).tobytes()).hexdigest()[:16],
+    }
+    print(json.dumps(out), flush=True)
 
 
 def selftest_gloo(args, rank: int, world: int) -> None:

@@ -416,10 +416,14 @@ class DeviceScene:
         check(rc, "rtx_render_region_device")
         return st
 
-    def render_host(self, cam: Camera, seed: int, n_gpus: int = 1, stats: bool = False, counters: bool = False):
-        """rtx_render (counters=False: the timed kernel) or rtx_render_ex(RTX_FLAG_COUNTERS) into a host array."""
+    def render_host(self, cam: Camera, seed: int, n_gpus: int = 1, stats: bool = False, counters: bool = False,
+                    out=None):
+        """rtx_render (counters=False: the timed kernel) or rtx_render_ex(RTX_FLAG_COUNTERS) into a host array
+        (`out`: a C-contiguous float32 [H, W, 3] to reuse, else a new one)."""
         import numpy as np
-        out = np.zeros((cam.image_height, cam.image_width, 3), dtype=np.float32)
+        if out is None:
+            out = np.zeros((cam.image_height, cam.image_width, 3), dtype=np.float32)
+        assert out.dtype == np.float32 and out.shape == (cam.image_height, cam.image_width, 3) and out.flags.c_contiguous
         st = Stats() if (stats or counters) else None
         if counters:
             rc = load().rtx_render_ex(self._h, ctypes.byref(cam), seed, n_gpus, RTX_FLAG_COUNTERS,

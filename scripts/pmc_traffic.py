@@ -50,6 +50,16 @@ out = {
     "method": "rocprofv3 --kernel-trace --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes); "
               "KiB units; FETCH_SIZE x2 (gfx950 16-B/lane read correction)",
 }
-with open(args.out, "w") as fh:
-    json.dump(out, fh, indent=1)
+if args.out.endswith(".jsonl"):  # one line per (workload, library): replace this one's, keep the others
+    keep = []
+    if os.path.exists(args.out):
+        with open(args.out) as fh:
+            keep = [ln for ln in fh.read().splitlines() if ln.strip() and
+                    (json.loads(ln).get("workload"), json.loads(ln).get("librtx_sha256_16")) !=
+                    (out["workload"], out["librtx_sha256_16"])]
+    with open(args.out, "w") as fh:
+        fh.write("\n".join(keep + [json.dumps(out)]) + "\n")
+else:
+    with open(args.out, "w") as fh:
+        json.dump(out, fh, indent=1)
 print(json.dumps(out))

@@ -69,3 +69,39 @@ def test_rank_processes_render_the_same_image_on_one_gpu():
     assert three["n_gpus"] == 3 and three["config"]["world_size"] == 3 and three["config"]["backend"] == "gloo"
     assert three["metric"].startswith("rehearsal")
     assert one["framebuffer_sha256_16"] == three["framebuffer_sha256_16"]
+
+
+def _bench_line_env(args, extra):
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(extra)
+    res = subprocess.run([sys.executable, "-u", "bench.py"] + args, cwd=ROOT, env=env, capture_output=True, text=True,
+                         timeout=240)
+    assert res.returncode == 0, res.stderr[-3000:]
+    lines = [ln for ln in res.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, res.stdout
+    return json.loads(lines[0])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("env,kind", [({"RTX_SIM_BANDS": "3"}, "device copies"), ({"RTX_FORCE_RCCL": "1"}, "rccl")])
+def test_in_process_leg_on_one_gpu(env, kind):
+    """`bench.py --in-process`: one process timing rtx_render(n_gpus) — the C-ABI's own N-device path
+    (bands, gather to device 0, de-interleave, copy to the host) that rank 0 of an N-GPU run also times
+    after its ranks' steps.  On one GPU: RTX_SIM_BANDS=3 renders three bands on device 0 and assembles
+    them as the gather does; RTX_FORCE_RCCL=1 runs the ncclGather as a 1-rank gather.  Same framebuffer as
+    the one-rank bench, the gather timed."""
+    common = ["--width", "192", "--spp", "8", "--steps", "2", "--warmup", "1", "--no-cpu"]
+    one = _bench_line(["--gpus", "1"] + common)
+    got = _bench_line_env(["--in-process", "--gpus", "1"] + common, env)
+    assert got["gather_kind"] == kind and got["gather_ms_avg"] > 0
+    assert got["framebuffer_sha256_16"] == one["framebuffer_sha256_16"]
+    assert got["value"] > 0 and got["kernel_ms_max_band_avg"] > 0
+
+
+@pytest.mark.gpu
+def test_shard_run_renders_its_rows():
+    """`bench.py --shard 1/3`: rank 1's rows of a 3-way run rendered alone (its PMC profile's workload):
+    the metric says so, and the roofline looks up that shard's own profile."""
+    got = _bench_line(["--shard", "1/3", "--width", "192", "--spp", "8", "--steps", "1", "--warmup", "0", "--no-cpu"])
+    assert got["metric"].startswith("shard 1/3")
+    assert "rows1of3" in str(got["roofline"].get("stale", "")) or got["roofline"].get("frac") is not None
