@@ -1,17 +1,23 @@
-// render_gpu.go — the Go side of the drop-in boundary: (*Camera).RenderGPU, a cgo binding of
+// render_gpu.go — the Go side of the drop-in boundary: Render on the MI355X path, a cgo binding of
 // librtx.so (include/rtx.h) for TwFlem/raytracer-go.
 //
 // A maintainer copies this file into the reference's package `internal` (next to
 // internal/camera.go; the Hittable/Material/Texture fields it flattens are unexported, so it
-// must live in that package) and points cgo at a build of this repository (`make -C
-// raytracer-go_amd`) through the environment, wherever it is checked out:
+// must live in that package), adds the three-line hook at the top of Render (INTEGRATION.md:
+// `if done, err := c.renderGPU(world, writer); done { return err }`) and points cgo at a build of
+// this repository (`make -C raytracer-go_amd`) through the environment, wherever it is checked out:
 //   CGO_CFLAGS="-I$RTX/include" CGO_LDFLAGS="-L$RTX/raytracer-go_amd -Wl,-rpath,$RTX/raytracer-go_amd" go build
-// ($RTX = this repository's root).  It replaces nothing: Render (internal/camera.go:180) stays as
-// the CPU path, and RenderGPU falls back to it for anything the GPU path does not carry.
+// ($RTX = this repository's root).  main.go then changes only its camera options:
+//   internal.NewCamera(16.0/9.0, 1920, ..., internal.WithGPUs(1), internal.WithSeed(2024))
+// (or RTX_GPUS=1 in the environment, with no change at all), and, to build a World of spheres'
+// BVH on the GPU instead of NewBVHFromWorld's host recursion (bvh.go:138-185; 100k spheres),
+// internal.NewBVHFromWorldGPU(world) in place of internal.NewBVHFromWorld(world).
+// Render keeps its CPU path for every scene part, device or option the GPU path does not carry.
 //
 // Go is not installed in the image this repository is built in, so this file has not been
-// compiled; the same flattening is built and tested in C++ (raytracer-go_amd/host/flatten.cpp)
-// and through ctypes (tests/).
+// compiled; tests/test_go_binding.py checks every C identifier and struct field it names against
+// include/rtx.h and drives the exact C-ABI call sequences it issues through ctypes, and the same
+// flattening is built and tested in C++ (raytracer-go_amd/host/flatten.cpp).
 package internal
 
 /*
@@ -26,11 +32,78 @@ import (
 	"fmt"
 	"io"
 	"math"
+	"os"
 	"runtime"
 	"strconv"
 	"strings"
+	"sync"
+	"sync/atomic"
 	"unsafe"
 )
+
+// gpuConfig holds a Camera's GPU options (WithGPUs, WithSeed).  The Camera struct is camera.go's,
+// so they are kept beside it, keyed by the *Camera (a Camera lives as long as its program).
+type gpuConfig struct {
+	gpus     int
+	seed     uint64
+	fallback atomic.Bool // RenderGPU is running the CPU Render: the hook stays out of the way
+}
+
+var gpuConfigs sync.Map // *Camera -> *gpuConfig
+
+func (c *Camera) gpuConfig() *gpuConfig {
+	if v, ok := gpuConfigs.Load(c); ok {
+		return v.(*gpuConfig)
+	}
+	cfg := &gpuConfig{seed: 1}
+	if n, err := strconv.Atoi(os.Getenv("RTX_GPUS")); err == nil { // the default without WithGPUs
+		cfg.gpus = n
+	}
+	v, _ := gpuConfigs.LoadOrStore(c, cfg)
+	return v.(*gpuConfig)
+}
+
+// WithGPUs renders on n MI355X devices of this process: Render runs the megakernel on row-
+// interleaved bands of the image, one per device, gathered to device 0 over RCCL (n > 1).  0 keeps
+// the reference's CPU path.  Without this option the RTX_GPUS environment variable decides.
+func WithGPUs(n int) CameraOpt {
+	return func(c *Camera) {
+		c.gpuConfig().gpus = n
+	}
+}
+
+// WithSeed keys the GPU path's counter-based RNG (Philox4x32-10; DESIGN.md §3): the same seed
+// gives the same image on any number of devices.  (The CPU path seeds its workers from the clock,
+// camera.go:170.)  It also seeds NewBVHFromWorldGPU's axis draws.
+func WithSeed(seed uint64) CameraOpt {
+	return func(c *Camera) {
+		c.gpuConfig().seed = seed
+	}
+}
+
+// gpuBVH is the tree NewBVHFromWorld would build over a World of spheres, built on the GPU by
+// rtx_scene_create_spheres (NewBVH restated, bvh.go:142-185: the same sort and median split per
+// node, the axis drawn from the render seed's stream instead of the global rand).  The CPU path
+// (Hit, GetBounds) builds the reference's tree on first use.
+type gpuBVH struct {
+	world *World
+	once  sync.Once
+	tree  *BVH
+}
+
+// NewBVHFromWorldGPU stands in for NewBVHFromWorld (bvh.go:138-140) when the World holds only
+// spheres: Render on the GPU path builds the tree on the device (10 ms for 100k spheres, where the
+// host recursion takes about 0.5 s), and any CPU use builds the reference's tree.
+func NewBVHFromWorldGPU(w *World) Hittable { return &gpuBVH{world: w} }
+
+func (g *gpuBVH) cpu() *BVH {
+	g.once.Do(func() { g.tree = NewBVHFromWorld(g.world) })
+	return g.tree
+}
+
+func (g *gpuBVH) Hit(r *Ray, rayT Interval) (HitInfo, bool) { return g.cpu().Hit(r, rayT) }
+
+func (g *gpuBVH) GetBounds() Aabb { return g.cpu().GetBounds() }
 
 // gpuTables is the flattened Hittable tree (rtx.h).  The slices hold no Go pointers, so
 // passing them to C is legal under the cgo rules; librtx copies them and never keeps them.
@@ -217,9 +290,15 @@ func (t *gpuTables) ref(h Hittable) (C.int32_t, error) {
 	}
 }
 
-func rtxErr(rc C.int) error {
-	return fmt.Errorf("rtx error %d: %s", int(rc), C.GoString(C.rtx_last_error()))
+// rtxError is a library error code with rtx_last_error's message (Render's error return).
+type rtxError struct {
+	code C.int
+	msg  string
 }
+
+func (e *rtxError) Error() string { return fmt.Sprintf("rtx error %d: %s", int(e.code), e.msg) }
+
+func rtxErr(rc C.int) error { return &rtxError{code: rc, msg: C.GoString(C.rtx_last_error())} }
 
 // gpuMissing: the library cannot run this render at all (no device, a feature it reports as
 // unsupported): RenderGPU then renders on the CPU.  (RCCL trouble is not among them: rtx_render
@@ -249,22 +328,85 @@ func flatten(world Hittable) (*gpuTables, error) {
 	return t, nil
 }
 
-// RenderGPU is Render (camera.go:180) on the MI355X path: same P3 bytes to writer, same
-// error return.  seed keys the counter-based RNG (the GPU path is reproducible); gpus > 1
-// row-interleaves the image over that many devices of this process (RCCL gather, rtx.h).
+// errFallback: the GPU path cannot carry this render (a scene part it does not flatten, no
+// device, a feature the library reports unsupported): the CPU path renders it instead.
+var errFallback = errors.New("rtx: render on the CPU path")
+
+// renderGPU is the hook at the top of Render (camera.go:180, INTEGRATION.md): with WithGPUs(n > 0)
+// (or RTX_GPUS) it renders on the devices and reports done; otherwise, or when the GPU path cannot
+// carry the render, Render continues on its CPU path.
+func (c *Camera) renderGPU(world Hittable, writer io.Writer) (bool, error) {
+	cfg := c.gpuConfig()
+	if cfg.gpus <= 0 || cfg.fallback.Load() {
+		return false, nil
+	}
+	err := c.renderOnDevices(world, writer, cfg.seed, cfg.gpus)
+	if errors.Is(err, errFallback) {
+		return false, nil
+	}
+	return true, err
+}
+
+// RenderGPU is Render (camera.go:180) on the MI355X path with an explicit seed and device count,
+// whatever the camera's options: same P3 bytes to writer, same error return; the CPU Render for
+// anything the GPU path does not carry.
 func (c *Camera) RenderGPU(world Hittable, writer io.Writer, seed uint64, gpus int) error {
-	c.init() // Camera.init (idempotent, sync.Once): the derived state below (camera.go:128-165)
-	t, err := flatten(world)
-	if errors.Is(err, errUnsupported) {
+	err := c.renderOnDevices(world, writer, seed, max(gpus, 1))
+	if errors.Is(err, errFallback) {
+		cfg := c.gpuConfig()
+		cfg.fallback.Store(true)
+		defer cfg.fallback.Store(false)
 		return c.Render(world, writer)
 	}
-	if err != nil {
-		return err
-	}
-	// desc holds pointers into Go slices: pinned for the call (cgo: Go memory passed to C may
-	// not contain unpinned Go pointers; runtime.Pinner, Go 1.21).
+	return err
+}
+
+// sceneOf uploads the world once (rtx_scene_create, or rtx_scene_create_spheres for a
+// NewBVHFromWorldGPU tree): the caller destroys the scene.  Go slices stay pinned only for the
+// call; librtx copies them and keeps no pointer into Go memory.
+func sceneOf(world Hittable, seed uint64) (*C.rtx_scene, error) {
 	var pin runtime.Pinner
 	defer pin.Unpin()
+	var scene *C.rtx_scene
+	if g, ok := world.(*gpuBVH); ok {
+		t := &gpuTables{matIdx: map[Material]C.uint32_t{}, texIdx: map[Texture]C.uint32_t{}}
+		for _, h := range g.world.hittables { // spheres in Add order: NewBVH's input list
+			s, ok := h.(*Sphere)
+			if !ok {
+				return nil, errFallback
+			}
+			mi, err := t.material(s.Material)
+			if err != nil {
+				return nil, err
+			}
+			t.spheres = append(t.spheres, C.rtx_sphere{center: vec(s.Center), radius: C.float(s.Radius), material: mi})
+		}
+		if len(t.spheres) == 0 {
+			return nil, errFallback
+		}
+		pin.Pin(&t.spheres[0])
+		pin.Pin(&t.materials[0])
+		var tex *C.rtx_texture
+		var texels *C.uint32_t
+		if len(t.textures) > 0 {
+			pin.Pin(&t.textures[0])
+			tex = &t.textures[0]
+		}
+		if len(t.texels) > 0 {
+			pin.Pin(&t.texels[0])
+			texels = &t.texels[0]
+		}
+		if rc := C.rtx_scene_create_spheres(&t.spheres[0], C.uint32_t(len(t.spheres)), &t.materials[0],
+			C.uint32_t(len(t.materials)), tex, C.uint32_t(len(t.textures)), texels, C.uint64_t(len(t.texels)),
+			C.uint64_t(seed), 0, &scene, nil); rc != 0 {
+			return nil, rtxErr(rc)
+		}
+		return scene, nil
+	}
+	t, err := flatten(world)
+	if err != nil {
+		return nil, err
+	}
 	var desc C.rtx_scene_desc
 	if len(t.nodes) > 0 {
 		pin.Pin(&t.nodes[0])
@@ -298,12 +440,23 @@ func (c *Camera) RenderGPU(world Hittable, writer io.Writer, seed uint64, gpus i
 		pin.Pin(&t.listRefs[0])
 		desc.list_refs, desc.n_list_refs = &t.listRefs[0], C.uint32_t(len(t.listRefs))
 	}
-	var scene *C.rtx_scene
 	if rc := C.rtx_scene_create(&desc, &scene); rc != 0 {
-		if gpuMissing(rc) {
-			return c.Render(world, writer)
-		}
-		return rtxErr(rc)
+		return nil, rtxErr(rc)
+	}
+	return scene, nil
+}
+
+// renderOnDevices renders on `gpus` devices and writes Render's P3 bytes; errFallback when the GPU
+// path cannot carry the render (nothing has been written then).
+func (c *Camera) renderOnDevices(world Hittable, writer io.Writer, seed uint64, gpus int) error {
+	c.init() // Camera.init (idempotent, sync.Once): the derived state below (camera.go:128-165)
+	scene, err := sceneOf(world, seed)
+	var re *rtxError
+	if errors.Is(err, errUnsupported) || (errors.As(err, &re) && gpuMissing(re.code)) {
+		return errFallback
+	}
+	if err != nil {
+		return err
 	}
 	// Destroying the last scene on a device also frees the library's sample scratch there, so
 	// nothing stays pinned in HBM after Render returns.
@@ -324,7 +477,7 @@ func (c *Camera) RenderGPU(world Hittable, writer io.Writer, seed uint64, gpus i
 		if rc := C.rtx_render_ppm(scene, &cam, C.uint64_t(seed), (*C.char)(unsafe.Pointer(&text[0])),
 			C.uint64_t(len(text)), &n, nil); rc != 0 {
 			if gpuMissing(rc) {
-				return c.Render(world, writer)
+				return errFallback
 			}
 			return rtxErr(rc)
 		}
@@ -334,7 +487,7 @@ func (c *Camera) RenderGPU(world Hittable, writer io.Writer, seed uint64, gpus i
 	rgb := make([]float32, w*h*3) // several GPUs: float32 image gathered to device 0, text here
 	if rc := C.rtx_render(scene, &cam, C.uint64_t(seed), C.int(gpus), (*C.float)(unsafe.Pointer(&rgb[0])), nil); rc != 0 {
 		if gpuMissing(rc) {
-			return c.Render(world, writer)
+			return errFallback
 		}
 		return rtxErr(rc)
 	}
