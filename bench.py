@@ -245,7 +245,8 @@ def roofline(st: dict, pixels: int, kernel_s: float, workload: str, traffic_path
     tr, tr_why = load_profile(traffic_path, workload, lib)
     vr, vr_why = load_profile(valu_path, workload, lib)
     out = {"bound": "valu", "achieved": None, "peak": round(VALU_PEAK_GINST, 1), "unit": "Gwave-inst/s",
-           "frac": None, "traffic": tr.get("hbm_bytes_per_launch") if tr else None, "librtx_sha256_16": lib}
+           "frac": None, "traffic": tr.get("hbm_bytes_per_launch") if tr else None, "librtx_sha256_16": lib,
+           "workload": workload}
     if vr:
         achieved = vr["valu_insts_per_launch"] / kernel_s / 1e9
         out.update(achieved=round(achieved, 1), frac=round(achieved / VALU_PEAK_GINST, 4),
@@ -272,7 +273,7 @@ def roofline(st: dict, pixels: int, kernel_s: float, workload: str, traffic_path
     return out
 
 
-def walk_desc(st, skips, near_skips) -> str:
+def walk_desc(st, skips, near_skips, cam) -> str:
     """The walked layout(s) of a render, from its stats and the plans' skip masks."""
     import rtx
 
@@ -283,11 +284,12 @@ def walk_desc(st, skips, near_skips) -> str:
     def col(m):
         return f"collapsed: {int(m.sum())} of {len(m)} node tests left out" if m.any() else "every box test"
 
+    if tiered:
+        far = "the caller's tree" if lay == rtx.RTX_LAYOUT_REFERENCE else "guarded tree"
+        return (f"tiered: near tree ({col(near_skips)}), {far} for {st.get('deferred_paths', 0)} deferred "
+                f"paths ({col(skips)}), camera octant {rtx.camera_octant(cam)}")
     if lay == rtx.RTX_LAYOUT_REFERENCE:
         return "reference tree, " + col(skips)
-    if tiered:
-        return (f"tiered: near tree ({col(near_skips)}), guarded tree for {st.get('deferred_paths', 0)} deferred "
-                f"paths ({col(skips)}), camera octant {lay}")
     return f"rebuilt tree, camera octant {lay}, " + col(skips)
 
 
@@ -437,7 +439,7 @@ def main():
             "segments_per_sample": round(tot["segments"] / tot["samples"], 4),
             "node_visits_per_segment": round(tot["node_visits"] / tot["segments"], 3),
             "kernel_ms_avg": round(avg_kernel_s * 1e3, 3),
-            "walk_layout": walk_desc(st, skips, near_skips),
+            "walk_layout": walk_desc(st, skips, near_skips, cam),
             "prim_tests_per_segment": round(tot["prim_tests"] / tot["segments"], 3),
             "schedule": schedule(st),
             "roofline": roofline(st, my_rows * W, avg_kernel_s, profile_workload, args.traffic, args.valu),

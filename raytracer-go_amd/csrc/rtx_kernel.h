@@ -14,6 +14,6 @@ struct Params;
 hipError_t launch_render(const Params& p, uint32_t flags, hipStream_t stream, const Params* far = nullptr);
 // Where a launch reads the scene (RTX_SCENE_IN_LDS / LDS_CACHE / IN_HBM, rtx.h).
 uint32_t scene_placement(const Params& p, uint32_t flags);
-// Where a tiered walk reads both layouts: their common placement, or 0 when they differ.
+// Where a tiered walk reads both layouts: their common placement, or RTX_SCENE_IN_HBM when they differ.
 uint32_t tier_placement(const Params& near, const Params& far, uint32_t flags);
 }  // namespace rtxd

@@ -668,7 +668,7 @@ uint32_t scene_placement(const Params& p, uint32_t flags) {
 
 uint32_t tier_placement(const Params& near, const Params& far, uint32_t flags) {
     const uint32_t a = scene_placement(near, flags), b = scene_placement(far, flags);
-    return a == b ? a : 0u;
+    return a == b ? a : RTX_SCENE_IN_HBM;  // placed unalike: both passes read their layouts from HBM
 }
 
 hipError_t launch_render(const Params& p, uint32_t flags, hipStream_t stream, const Params* far) {
@@ -677,8 +677,7 @@ hipError_t launch_render(const Params& p, uint32_t flags, hipStream_t stream, co
     const bool count = (flags & RTX_FLAG_COUNTERS) != 0;
     if (far) {  // the caller checked: spheres only, both layouts placed alike (tier_placement), no noise
         const uint32_t place = tier_placement(p, *far, flags);
-        if (p.tier != 1 || far->tier != 2 || !p.defer || !far->defer || !p.redo_bits || p.n_quads || p.has_noise ||
-            place == 0)
+        if (p.tier != 1 || far->tier != 2 || !p.defer || !far->defer || !p.redo_bits || p.n_quads || p.has_noise)
             return hipErrorInvalidValue;
         const bool clk = !count && (flags & RTX_FLAG_TIMING);  // diagnostics: the wave-cycle split of the passes
         if (place == RTX_SCENE_IN_LDS) {

@@ -95,7 +95,8 @@ def check_scene(torch, dev, desc, cam, seed, reg, flags=0, kernels=("timed", "co
         assert np.array_equal(gpu, it), f"{k} kernel not bit-identical to the oracle: max {np.abs(gpu - it).max()}"
         d = float(np.abs(gpu - ref).max()) if gpu.size else 0.0
         assert d <= TOL, f"{k} kernel: max |delta| = {d} > {TOL} vs the reference-order oracle"
-        want = rtx.camera_octant(cam) if walk is not desc else rtx.RTX_LAYOUT_REFERENCE
+        far = tw[1] if tier is not None else walk  # the tree the walk falls back on: rebuilt, or the caller's
+        want = rtx.camera_octant(cam) if far is not desc else rtx.RTX_LAYOUT_REFERENCE
         if tier is not None:
             want |= rtx.RTX_LAYOUT_TIERED
         assert s.walk_layout == want, (k, s.walk_layout, want)

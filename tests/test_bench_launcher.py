@@ -104,4 +104,4 @@ def test_shard_run_renders_its_rows():
     the metric says so, and the roofline looks up that shard's own profile."""
     got = _bench_line(["--shard", "1/3", "--width", "192", "--spp", "8", "--steps", "1", "--warmup", "0", "--no-cpu"])
     assert got["metric"].startswith("shard 1/3")
-    assert "rows1of3" in str(got["roofline"].get("stale", "")) or got["roofline"].get("frac") is not None
+    assert got["roofline"]["workload"].endswith("/rows1of3") and "rank 1's kernel" in got["roofline"]["scope"]

@@ -106,13 +106,31 @@ def test_oracle_list_equivalences(built, order):
 
 
 @pytest.mark.gpu
-def test_nested_worlds_gpu_bitexact(built):
+def test_nested_worlds_gpu_tiered(built):
+    """The nested-World scene under the tiered walk (its node boxes hold every sphere's own box, so it
+    gets a near tree; the caller's tree with its Worlds is the far tree): both kernels bit-exact, with
+    the tiered oracle's counters (tests/parity.py)."""
     import torch
 
     assert torch.cuda.is_available()
     torch.cuda.set_device(0)
     sc = rtx.HostScene("nested_worlds", seed=1)
     dev = rtx.DeviceScene(sc.desc)
+    cam = sc.camera(width=192, spp=6, depth=50)
+    reg = rtx.Region(0, 0, cam.image_width, cam.image_height, 0, 1)
+    _, st, _ = parity.check_scene(torch, dev, sc.desc, cam, 11, reg)
+    assert st.walk_layout == rtx.RTX_LAYOUT_REFERENCE | rtx.RTX_LAYOUT_TIERED
+
+
+@pytest.mark.gpu
+def test_nested_worlds_gpu_bitexact(built):
+    """The caller's tree with Worlds nested in it, walked as it is (RTX_SCENE_NO_TIER)."""
+    import torch
+
+    assert torch.cuda.is_available()
+    torch.cuda.set_device(0)
+    sc = rtx.HostScene("nested_worlds", seed=1)
+    dev = rtx.DeviceScene(sc.desc, no_tier=True)
     cam = sc.camera(width=192, spp=6, depth=50)
     reg = rtx.Region(0, 0, cam.image_width, cam.image_height, 0, 1)
     out = torch.full((cam.image_height, cam.image_width, 3), float("nan"), device="cuda")

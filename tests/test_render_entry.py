@@ -120,7 +120,7 @@ def test_watchdog_stops_v3(built):
     """A render whose per-wave time limit (RTX_WATCHDOG_S) is exceeded stops claiming work and
     reports RTX_ERR_HIP instead of keeping the GPU busy."""
     out = child(
-        "s = rtx.HostScene('random_spheres', 1); d = rtx.DeviceScene(s.desc); c = s.camera(width=400, spp=2000)\n"
+        "s = rtx.HostScene('random_spheres', 1); d = rtx.DeviceScene(s.desc); c = s.camera(width=400, spp=8000)\n"
         "o = torch.empty((225, 400, 3), device='cuda')\n"
         "try:\n"
         "    d.render_region(c, 1, rtx.Region(0, 0, 400, 225, 0, 1), o.data_ptr(), 0, timed=True)\n"
@@ -130,7 +130,7 @@ def test_watchdog_stops_v3(built):
         "st = d.render_region(s.camera(width=64, spp=1), 1, rtx.Region(0, 0, 64, 36, 0, 1), o.data_ptr(), 0,"
         " timed=True)\n"
         "print('next render ok')\n",
-        env={"RTX_WATCHDOG_S": "0.02"})
+        env={"RTX_WATCHDOG_S": "0.005"})
     assert f"ERR {rtx.RTX_ERR_HIP}" in out and "next render ok" in out, out
 
 
