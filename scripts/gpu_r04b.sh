@@ -5,7 +5,7 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT="$PWD/gpurun_out/r04b"; mkdir -p "$OUT"; export TMPDIR=/tmp
 timeout -k 10 600 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread \
-    -k "shard_run or kernel_variant or stress_100k or nested_world or watchdog or ties or walk_layout" > "$OUT/pytest_gpu.log" 2>&1
+    -k "shard_run or kernel_variant or stress_100k or nested_world or watchdog or ties or walk_layout or go_sequence" > "$OUT/pytest_gpu.log" 2>&1
 rc=$?
 grep -E "passed|failed|error" "$OUT/pytest_gpu.log" | tail -8
 [ $rc -le 1 ] && \
