@@ -967,14 +967,16 @@ int enqueue_on(rtx_scene* s, DeviceCopy* c, const rtx_camera* cam, uint64_t seed
                 HIP_TRY(hipMalloc(&scr->defer, need));
                 scr->defer_bytes = need;
             }
-            const size_t bits = (size_t)(items / 8);  // chunk x tiles x 64 slots, 8 per byte
-            if (scr->redo_bytes < bits) {
+            // the bits (chunk x tiles x 64 slots, 8 per byte), then as many bytes of 4-byte sample ids: the
+            // redo pass's compacted list holds up to 1/32 of the chunk's samples (C2 defers 0.9 %)
+            const size_t bits = (size_t)(items / 8);
+            if (scr->redo_bytes < 2 * bits) {
                 HIP_TRY(hipEventSynchronize(scr->last));
                 if (scr->redo) HIP_TRY(hipFree(scr->redo));
                 scr->redo = nullptr;
                 scr->redo_bytes = 0;
-                HIP_TRY(hipMalloc(&scr->redo, bits));
-                scr->redo_bytes = bits;
+                HIP_TRY(hipMalloc(&scr->redo, 2 * bits));
+                scr->redo_bytes = 2 * bits;
             }
             rtxd::Params lay = pn;  // the near pass: every setting of p, the near walk's layout
             pn = p;
@@ -992,6 +994,9 @@ int enqueue_on(rtx_scene* s, DeviceCopy* c, const rtx_camera* cam, uint64_t seed
             if (!std::getenv("RTX_PRIM_BATCH")) pn.prim_batch = 12;
             pn.defer = p.defer = scr->defer;
             pn.redo_bits = p.redo_bits = scr->redo;
+            pn.redo_ids = p.redo_ids = scr->redo + bits / 4;
+            pn.redo_cap = p.redo_cap = (uint32_t)std::min<uint64_t>(bits / 4, 0xFFFFFFFFull);
+            pn.redo_count = p.redo_count = reinterpret_cast<uint32_t*>(c->counters + 25);
             pn.defer_cap = p.defer_cap = (uint32_t)cap;
             pn.defer_count = p.defer_count = reinterpret_cast<uint32_t*>(c->counters + 22);  // low: records
             pn.redo_flag = p.redo_flag = reinterpret_cast<uint32_t*>(c->counters + 22) + 1;  // high: overflow

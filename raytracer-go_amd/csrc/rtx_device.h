@@ -469,6 +469,11 @@ struct Params {
     // one bit per scratch slot of the chunk, (k - k0) * n_tiles * 64 + pixel slot: a sample whose
     // path did not fit the queue, rendered again from its camera ray by the redo pass (zeroed per chunk)
     uint32_t* redo_bits;
+    // the flagged bits' indices, compacted (compact_redo) for the redo pass: up to redo_cap of them, the
+    // count in *redo_count (beyond redo_cap the redo pass scans the bits instead)
+    uint32_t* redo_ids;
+    uint32_t redo_cap;
+    uint32_t* redo_count;
 };
 
 struct Ray {

@@ -240,7 +240,11 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
     // far pass: units of 64 queue records
     const uint32_t n_rec = TIER == 2 ? min(__builtin_amdgcn_readfirstlane(*(volatile uint32_t*)p.defer_count), p.defer_cap)
                                      : 0u;
-    const uint64_t n_units = TIER == 2 ? (uint64_t)((n_rec + 63u) / 64u) : (uint64_t)n_tiles * nsub;
+    // redo pass: the compacted list of flagged samples when it held them all (else the bits, unit by unit)
+    const uint32_t n_ids = TIER == 3 ? __builtin_amdgcn_readfirstlane(*(volatile uint32_t*)p.redo_count) : 0u;
+    const bool listed = TIER == 3 && n_ids <= p.redo_cap;
+    const uint64_t n_units = TIER == 2 ? (uint64_t)((n_rec + 63u) / 64u)
+                                       : (listed ? (uint64_t)((n_ids + 63u) / 64u) : (uint64_t)n_tiles * nsub);
     if (TIER == 2 && blockIdx.x == 0 && threadIdx.x == 0 && n_rec)
         atomicAdd(&p.counters[23], (unsigned long long)n_rec);  // deferred paths, all chunks
     const size_t tile_floats = (size_t)n_tiles * 64 * 3;  // one sample of every tile (tile-major scratch)
@@ -376,9 +380,9 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
                 if (lane == 0) un = atomicAdd(p.tile_counter, 1u);
                 const uint32_t uu = __builtin_amdgcn_readfirstlane(un);  // the whole wave is here: lane 0's
                 exhausted = uu >= n_units;
-                if (!exhausted && TIER == 2) {
-                    u_k0 = 64u * uu;  // the unit's first record
-                    u_items = min(64u, n_rec - u_k0);
+                if (!exhausted && (TIER == 2 || listed)) {
+                    u_k0 = 64u * uu;  // the unit's first record / listed sample
+                    u_items = min(64u, (TIER == 2 ? n_rec : n_ids) - u_k0);
                     cursor = 0;
                 } else if (!exhausted) {
                     const uint32_t u_tile = uu / nsub;
@@ -388,7 +392,7 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
                     const uint32_t cnt_k = min(p.sub, p.k0 + p.kn - u_k0);
                     u_items = 64u * cnt_k;
                     cursor = 0;
-                    if constexpr (TIER == 3) {  // a unit without a flagged sample: the next unit
+                    if (TIER == 3 && !listed) {  // a unit without a flagged sample: the next unit
                         const bool any = lane < cnt_k && redo64[(size_t)(u_k0 + lane - p.k0) * n_tiles + u_tile] != 0;
                         if (ballot(any) == 0) cursor = u_items;
                     }
@@ -413,14 +417,24 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
                 mode = M_START;
                 ready = true;
             } else if (TIER != 2 && mode == M_CLAIM && rank < u_items - cursor) {
-                const uint32_t j = cursor + rank, l = j & 63u;  // sample-major within the unit
-                const uint32_t lx = u_x8 + (l & 7u);
-                const uint32_t lr = u_r8 + (l >> 3);
-                const size_t slot = (size_t)((u_r8 >> 3) * tiles_x + (u_x8 >> 3)) * 64 + l;
-                const uint32_t k = u_k0 + (j >> 6);
+                uint32_t j = cursor + rank, l = j & 63u;  // sample-major within the unit
+                uint32_t lx = u_x8 + (l & 7u);
+                uint32_t lr = u_r8 + (l >> 3);
+                size_t slot = (size_t)((u_r8 >> 3) * tiles_x + (u_x8 >> 3)) * 64 + l;
+                uint32_t k = u_k0 + (j >> 6);
+                if (TIER == 3 && listed) {  // a listed sample: its bit index in the chunk
+                    const uint32_t id = p.redo_ids[u_k0 + j];
+                    const uint32_t per_k = n_tiles * 64u;
+                    k = p.k0 + id / per_k;
+                    slot = id - (k - p.k0) * per_k;
+                    l = (uint32_t)slot & 63u;
+                    const uint32_t tile = (uint32_t)(slot >> 6);
+                    lx = (tile % tiles_x) * 8u + (l & 7u);
+                    lr = (tile / tiles_x) * 8u + (l >> 3);
+                }
                 // else: outside a ragged tile (or, redo pass, not flagged), claim again
                 if (lx < p.width && lr < p.rows &&
-                    (TIER != 3 || ((redo64[((size_t)(k - p.k0) * n_tiles * 64 + slot) >> 6] >> l) & 1ull))) {
+                    (TIER != 3 || listed || ((redo64[((size_t)(k - p.k0) * n_tiles * 64 + slot) >> 6] >> l) & 1ull))) {
                     const uint32_t x = p.x0 + lx, y = p.y0 + p.rank + lr * p.world;
                     base = pixel_base(c, x, y);
                     rng.pixel = y * c.image_width + x;
@@ -471,6 +485,20 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
         }
         atomicAdd(&p.counters[13], (unsigned long long)shade_cycles);
     }
+}
+
+// The redo pass's list: the indices of the chunk's flagged samples (p.redo_bits), in no particular
+// order (every sample is rendered on its own).  One thread per 64-bit word, one atomic per word that
+// has a flag; nothing to do (a return) when no record overflowed.  The ids stop at p.redo_cap; the
+// count keeps growing, and a count past the cap tells the redo pass to scan the bits instead.
+__global__ __launch_bounds__(256) void compact_redo(Params p, uint64_t n_words) {
+    if (__builtin_amdgcn_readfirstlane(*(volatile uint32_t*)p.redo_flag) == 0u) return;
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n_words) return;
+    uint64_t w = reinterpret_cast<const uint64_t*>(p.redo_bits)[i];
+    if (w == 0) return;
+    uint32_t at = atomicAdd(p.redo_count, (uint32_t)__popcll(w));
+    for (; w != 0 && at < p.redo_cap; w &= w - 1, ++at) p.redo_ids[at] = (uint32_t)(i * 64 + (uint64_t)__builtin_ctzll(w));
 }
 
 // GetPixelColor's sum over the stored colours of samples [k0, k0 + kn), in k order
@@ -617,13 +645,16 @@ hipError_t launch_tiered(Params pn, Params pf, hipStream_t stream) {
             fprintf(stderr, "rtx tiered: waves/wg %d, wgs/CU %d / %d / %d, grid %llu, sub %u, units %llu, lds %zu / %zu B, "
                     "cap %u\n", WAVES, per_n, per_f, per_r, (unsigned long long)bn, pn.sub, (unsigned long long)units, sn,
                     sf, pn.defer_cap);
-        // the unit queue head, the chunk's record count + overflow flag (one u64 slot), its redo bits
+        // the unit queue head, the chunk's record count + overflow flag (one u64 slot), its redo bits and list
         if ((e = hipMemsetAsync(pn.tile_counter, 0, sizeof(uint32_t), stream)) != hipSuccess) return e;
         if ((e = hipMemsetAsync(pn.defer_count, 0, 2 * sizeof(uint32_t), stream)) != hipSuccess) return e;
+        if ((e = hipMemsetAsync(pn.redo_count, 0, sizeof(uint32_t), stream)) != hipSuccess) return e;
         if ((e = hipMemsetAsync(pn.redo_bits, 0, (size_t)pn.kn * tiles * 8, stream)) != hipSuccess) return e;
         hipLaunchKernelGGL(kn, dim3((uint32_t)bn), dim3(block), sn, stream, pn);
         if ((e = hipMemsetAsync(pf.tile_counter, 0, sizeof(uint32_t), stream)) != hipSuccess) return e;
         hipLaunchKernelGGL(kf, dim3((uint32_t)per_f * cus), dim3(block), sf, stream, pf);
+        const uint64_t words = (uint64_t)pn.kn * tiles;  // 64 slots each
+        hipLaunchKernelGGL(compact_redo, dim3((uint32_t)((words + 255) / 256)), dim3(256), 0, stream, pn, words);
         if ((e = hipMemsetAsync(pr.tile_counter, 0, sizeof(uint32_t), stream)) != hipSuccess) return e;
         hipLaunchKernelGGL(kr, dim3((uint32_t)br), dim3(block), sf, stream, pr);
         hipLaunchKernelGGL(reduce_samples, dim3((uint32_t)((slots + 255) / 256)), dim3(256), 0, stream, pn,
