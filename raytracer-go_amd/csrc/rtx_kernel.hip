@@ -304,7 +304,8 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
             }
             mode = M_CLAIM;
         }
-        if (ballot(full) != 0 && lane == 0) atomicOr(p.redo_flag, 1u);
+        // (one flag for the chunk: set once, read before — same-address atomics from every wave serialise)
+        if (ballot(full) != 0 && lane == 0 && *(volatile uint32_t*)p.redo_flag == 0u) atomicOr(p.redo_flag, 1u);
     };
     auto defer_far = [&](bool& ready) {  // segments that would start outside the near region
         const bool far = ready && !(r.o.x >= p.near_min[0] && r.o.x <= p.near_max[0] && r.o.y >= p.near_min[1] &&

@@ -137,12 +137,21 @@ def render_ppm(L, h, cam, seed):
     return buf[: n.value].tobytes()
 
 
-def desc_from_export(entries: bytes, base_desc, spheres, n_spheres):
-    """The node table of a scene's threaded entries (rtx_scene_export: the reference walk's pre-order, a
-    node's escape after its subtree; a one-element split's child once) over `spheres` (the sphere indices
-    the entries name), with base_desc's materials and textures."""
+def desc_from_export(entries: bytes, base_desc):
+    """The scene description of a scene's threaded entries (rtx_scene_export: the reference walk's
+    pre-order, a node's escape after its subtree; a one-element split's child once): its node table, and
+    its sphere table rebuilt from the sphere entries (centre, radius, material; the GPU build numbers the
+    spheres in pre-order, as the flattener does), with base_desc's materials and textures."""
     e = np.frombuffer(entries, np.uint32).reshape(-1, 8)
     fl = e.view(np.float32)
+    sph = e[e[:, 7].view(np.int32) != -1]
+    spheres = (rtx.Sphere * len(sph))()
+    for row in sph:
+        i = int(row[5])
+        spheres[i].center = (ctypes.c_float * 3)(*[float(v) for v in row[:3].view(np.float32)])
+        spheres[i].radius = float(row[3:4].view(np.float32)[0])
+        spheres[i].material = int(row[7])
+    n_spheres = len(sph)
     nodes = []
 
     def build(i):  # -> (ref, next entry)
@@ -220,7 +229,7 @@ def test_go_sequence_gpu_bvh(gpu, scene):
     dev = rtx.DeviceScene(handle=h)
     try:
         text = render_ppm(L, h, cam, 2024)
-        tree = desc_from_export(dev.export(), host.desc, arr, n)
+        tree = desc_from_export(dev.export(), host.desc)
     finally:
         dev.close()
     reg = rtx.Region(0, 0, cam.image_width, cam.image_height, 0, 1)
