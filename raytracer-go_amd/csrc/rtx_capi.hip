@@ -968,7 +968,7 @@ int enqueue_on(rtx_scene* s, DeviceCopy* c, const rtx_camera* cam, uint64_t seed
                 scr->defer_bytes = need;
             }
             // the bits (chunk x tiles x 64 slots, 8 per byte), then as many bytes of 4-byte sample ids: the
-            // redo pass's compacted list holds up to 1/32 of the chunk's samples (C2 defers 0.9 %)
+            // redo list holds up to 1/32 of the chunk's samples (C2 defers 0.9 % of its paths)
             const size_t bits = (size_t)(items / 8);
             if (scr->redo_bytes < 2 * bits) {
                 HIP_TRY(hipEventSynchronize(scr->last));
@@ -995,11 +995,12 @@ int enqueue_on(rtx_scene* s, DeviceCopy* c, const rtx_camera* cam, uint64_t seed
             pn.defer = p.defer = scr->defer;
             pn.redo_bits = p.redo_bits = scr->redo;
             pn.redo_ids = p.redo_ids = scr->redo + bits / 4;
-            pn.redo_cap = p.redo_cap = (uint32_t)std::min<uint64_t>(bits / 4, 0xFFFFFFFFull);
+            uint64_t rcap = std::min<uint64_t>(bits / 4, 0xFFFFFFFFull);
+            if (const char* e = std::getenv("RTX_REDO_CAP")) rcap = std::min<uint64_t>(rcap, std::strtoull(e, nullptr, 10));
+            pn.redo_cap = p.redo_cap = (uint32_t)rcap;  // (RTX_REDO_CAP: tests of the bits' path)
             pn.redo_count = p.redo_count = reinterpret_cast<uint32_t*>(c->counters + 25);
             pn.defer_cap = p.defer_cap = (uint32_t)cap;
             pn.defer_count = p.defer_count = reinterpret_cast<uint32_t*>(c->counters + 22);  // low: records
-            pn.redo_flag = p.redo_flag = reinterpret_cast<uint32_t*>(c->counters + 22) + 1;  // high: overflow
             std::memcpy(pn.near_min, s->near_topo.near_box, 3 * sizeof(float));
             std::memcpy(pn.near_max, s->near_topo.near_box + 3, 3 * sizeof(float));
             *tiered = true;

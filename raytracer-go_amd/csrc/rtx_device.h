@@ -465,15 +465,15 @@ struct Params {
     float4* defer;          // the records: 4 float4 each (origin | pixel, dir | sample, thr | seg, acc | slot)
     uint32_t defer_cap;     // records the queue holds
     uint32_t* defer_count;  // records written (the far pass reads min(count, cap))
-    uint32_t* redo_flag;    // set when a record did not fit (the redo pass returns at once otherwise)
-    // one bit per scratch slot of the chunk, (k - k0) * n_tiles * 64 + pixel slot: a sample whose
-    // path did not fit the queue, rendered again from its camera ray by the redo pass (zeroed per chunk)
-    uint32_t* redo_bits;
-    // the flagged bits' indices, compacted (compact_redo) for the redo pass: up to redo_cap of them, the
-    // count in *redo_count (beyond redo_cap the redo pass scans the bits instead)
+    // The samples whose records did not fit, by id = (k - k0) * n_tiles * 64 + pixel slot: rendered again
+    // from their camera rays by the redo pass.  The near pass lists up to redo_cap ids in redo_ids (the
+    // count, all of them, in *redo_count) and sets the bits of the others in redo_bits, one per scratch
+    // slot of the chunk (zeroed per chunk); past redo_cap the list joins the bits (spill_redo_list) and
+    // the redo pass scans them.
     uint32_t* redo_ids;
     uint32_t redo_cap;
     uint32_t* redo_count;
+    uint32_t* redo_bits;
 };
 
 struct Ray {

@@ -189,7 +189,7 @@ template <bool COUNT, bool USE_LDS, bool QUADS, bool NOISE, int WAVES = 8, int M
 __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
     constexpr bool TIME = COUNT || CLK;
     if constexpr (TIER == 3) {
-        if (__builtin_amdgcn_readfirstlane(*(volatile uint32_t*)p.redo_flag) == 0u) return;
+        if (__builtin_amdgcn_readfirstlane(*(volatile uint32_t*)p.redo_count) == 0u) return;
         if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&p.counters[24], 1ull);  // chunks with a redo
     }
     // walk steps between two wave votes (A/B with primitive batching: 4 +0.7 %, 8 +0.8 %, 12 +1.3 %)
@@ -295,17 +295,25 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
                 q[2] = make_float4(thr.x, thr.y, thr.z, __uint_as_float(seg));
                 q[3] = make_float4(acc.x, acc.y, acc.z, __uint_as_float((uint32_t)pix));
             } else {
-                // No room: the redo pass renders this sample again from its camera ray on the far tree
-                // (the same path: its Philox blocks are keyed by (pixel, sample, event)), and counts it.
-                const size_t bit = (size_t)(rng.sample - p.k0) * n_tiles * 64 + pix;
-                atomicOr(p.redo_bits + (bit >> 5), 1u << (uint32_t)(bit & 31u));
-                if (COUNT) cnt = path0;
                 full = true;
             }
             mode = M_CLAIM;
         }
-        // (one flag for the chunk: set once, read before — same-address atomics from every wave serialise)
-        if (ballot(full) != 0 && lane == 0 && *(volatile uint32_t*)p.redo_flag == 0u) atomicOr(p.redo_flag, 1u);
+        // No room: the redo pass renders the sample again from its camera ray on the far tree (the same
+        // path: its Philox blocks are keyed by (pixel, sample, event)), and counts it.  Its id goes to the
+        // redo list (one reservation per wave, coalesced stores); past the list's end, to the redo bits.
+        const uint64_t om = ballot(full);
+        if (om == 0) return;
+        uint32_t b2 = 0;
+        if (lane == 0) b2 = atomicAdd(p.redo_count, (uint32_t)__popcll(om));
+        b2 = __builtin_amdgcn_readfirstlane(b2);
+        if (full) {
+            const uint32_t at = b2 + (uint32_t)__popcll(om & ((1ull << lane) - 1ull));
+            const uint32_t id = (rng.sample - p.k0) * n_tiles * 64u + (uint32_t)pix;
+            if (at < p.redo_cap) p.redo_ids[at] = id;
+            else atomicOr(p.redo_bits + (id >> 5), 1u << (id & 31u));
+            if (COUNT) cnt = path0;
+        }
     };
     auto defer_far = [&](bool& ready) {  // segments that would start outside the near region
         const bool far = ready && !(r.o.x >= p.near_min[0] && r.o.x <= p.near_max[0] && r.o.y >= p.near_min[1] &&
@@ -488,18 +496,14 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
     }
 }
 
-// The redo pass's list: the indices of the chunk's flagged samples (p.redo_bits), in no particular
-// order (every sample is rendered on its own).  One thread per 64-bit word, one atomic per word that
-// has a flag; nothing to do (a return) when no record overflowed.  The ids stop at p.redo_cap; the
-// count keeps growing, and a count past the cap tells the redo pass to scan the bits instead.
-__global__ __launch_bounds__(256) void compact_redo(Params p, uint64_t n_words) {
-    if (__builtin_amdgcn_readfirstlane(*(volatile uint32_t*)p.redo_flag) == 0u) return;
-    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= n_words) return;
-    uint64_t w = reinterpret_cast<const uint64_t*>(p.redo_bits)[i];
-    if (w == 0) return;
-    uint32_t at = atomicAdd(p.redo_count, (uint32_t)__popcll(w));
-    for (; w != 0 && at < p.redo_cap; w &= w - 1, ++at) p.redo_ids[at] = (uint32_t)(i * 64 + (uint64_t)__builtin_ctzll(w));
+// The redo list overflowed (more samples than p.redo_cap): its ids join the ones the near pass set in
+// p.redo_bits, and the redo pass scans the bits.  A return when it did not.
+__global__ __launch_bounds__(256) void spill_redo_list(Params p) {
+    if (__builtin_amdgcn_readfirstlane(*(volatile uint32_t*)p.redo_count) <= p.redo_cap) return;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < p.redo_cap; i += (uint64_t)gridDim.x * 256) {
+        const uint32_t id = p.redo_ids[i];
+        atomicOr(p.redo_bits + (id >> 5), 1u << (id & 31u));
+    }
 }
 
 // GetPixelColor's sum over the stored colours of samples [k0, k0 + kn), in k order
@@ -646,16 +650,15 @@ hipError_t launch_tiered(Params pn, Params pf, hipStream_t stream) {
             fprintf(stderr, "rtx tiered: waves/wg %d, wgs/CU %d / %d / %d, grid %llu, sub %u, units %llu, lds %zu / %zu B, "
                     "cap %u\n", WAVES, per_n, per_f, per_r, (unsigned long long)bn, pn.sub, (unsigned long long)units, sn,
                     sf, pn.defer_cap);
-        // the unit queue head, the chunk's record count + overflow flag (one u64 slot), its redo bits and list
+        // the unit queue head, the chunk's record count, its redo list count and bits
         if ((e = hipMemsetAsync(pn.tile_counter, 0, sizeof(uint32_t), stream)) != hipSuccess) return e;
-        if ((e = hipMemsetAsync(pn.defer_count, 0, 2 * sizeof(uint32_t), stream)) != hipSuccess) return e;
+        if ((e = hipMemsetAsync(pn.defer_count, 0, sizeof(uint32_t), stream)) != hipSuccess) return e;
         if ((e = hipMemsetAsync(pn.redo_count, 0, sizeof(uint32_t), stream)) != hipSuccess) return e;
         if ((e = hipMemsetAsync(pn.redo_bits, 0, (size_t)pn.kn * tiles * 8, stream)) != hipSuccess) return e;
         hipLaunchKernelGGL(kn, dim3((uint32_t)bn), dim3(block), sn, stream, pn);
         if ((e = hipMemsetAsync(pf.tile_counter, 0, sizeof(uint32_t), stream)) != hipSuccess) return e;
         hipLaunchKernelGGL(kf, dim3((uint32_t)per_f * cus), dim3(block), sf, stream, pf);
-        const uint64_t words = (uint64_t)pn.kn * tiles;  // 64 slots each
-        hipLaunchKernelGGL(compact_redo, dim3((uint32_t)((words + 255) / 256)), dim3(256), 0, stream, pn, words);
+        hipLaunchKernelGGL(spill_redo_list, dim3((uint32_t)cus * 4), dim3(256), 0, stream, pn);
         if ((e = hipMemsetAsync(pr.tile_counter, 0, sizeof(uint32_t), stream)) != hipSuccess) return e;
         hipLaunchKernelGGL(kr, dim3((uint32_t)br), dim3(block), sf, stream, pr);
         hipLaunchKernelGGL(reduce_samples, dim3((uint32_t)((slots + 255) / 256)), dim3(256), 0, stream, pn,

@@ -4,7 +4,7 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT="$PWD/gpurun_out/r04d"; mkdir -p "$OUT"; export TMPDIR=/tmp
-timeout -k 10 300 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread -k "go_sequence or overflow" > "$OUT/pytest_gpu.log" 2>&1
+timeout -k 10 300 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread -k "go_sequence or overflow or ties or stress_100k_crop" > "$OUT/pytest_gpu.log" 2>&1
 rc=$?
 grep -E "passed|failed|error" "$OUT/pytest_gpu.log" | tail -4
 [ $rc -le 1 ] && \

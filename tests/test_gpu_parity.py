@@ -447,14 +447,15 @@ def test_config_rows_vs_oracle(torch_cuda, built, name):
           f"max |delta| vs the reference order {d:.2e}")
 
 
-@pytest.mark.parametrize("cap", [0, 64, 1000])
-def test_tier_queue_overflow_redo(torch_cuda, spheres, dev_spheres, monkeypatch, cap):
+@pytest.mark.parametrize("cap,redo_cap", [(0, None), (64, None), (1000, None), (64, 100), (0, 0)])
+def test_tier_queue_overflow_redo(torch_cuda, spheres, dev_spheres, monkeypatch, cap, redo_cap):
     """The tiered walk's queue of deferred paths too small for the chunk
     (RTX_DEFER_CAP): the samples whose records do not fit are flagged and rendered again from their
     camera rays on the guarded tree by the redo pass — the same image, bit for bit, as the oracle on
     the caller's tree and as the render with room, from both kernels; the counting kernel's path
     counters (samples, segments, hits, texel fetches, draws) equal the oracle's: the near pass's work
-    on a flagged sample is taken back and the redo pass counts it."""
+    on a flagged sample is taken back and the redo pass counts it.  RTX_REDO_CAP shortens the redo list
+    so that the samples past it take the bits' path (spill_redo_list, the redo pass scanning the bits)."""
     cam = spheres.camera(width=160, spp=12, depth=50)
     reg = rtx.Region(0, 0, cam.image_width, cam.image_height, 0, 1)
     want, st0 = gpu_region(torch_cuda, dev_spheres, cam, 21, reg, counters=True)
@@ -462,6 +463,8 @@ def test_tier_queue_overflow_redo(torch_cuda, spheres, dev_spheres, monkeypatch,
     assert np.array_equal(want, it)
     assert st0.redo_chunks == 0 and st0.deferred_paths > 1000
     monkeypatch.setenv("RTX_DEFER_CAP", str(cap))
+    if redo_cap is not None:
+        monkeypatch.setenv("RTX_REDO_CAP", str(redo_cap))
     for counters in (False, True):
         got, st = gpu_region(torch_cuda, dev_spheres, cam, 21, reg, counters=counters)
         assert st.walk_layout & rtx.RTX_LAYOUT_TIERED and st.redo_chunks == 1
