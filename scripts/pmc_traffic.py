@@ -26,6 +26,9 @@ ap.add_argument("--kernel", default="render_items<false")
 ap.add_argument("--lib", default=os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                                               "raytracer-go_amd", "librtx.so"),
                 help="the library the profiled run loaded: its hash ties the profile to the code (bench.py checks it)")
+ap.add_argument("--renders", type=int, default=0,
+                help="renders in the profiled run: every dispatch summed and divided by it (a render of several "
+                     "sample chunks dispatches each pass per chunk); 0: the median dispatch of each kernel")
 args = ap.parse_args()
 
 # Per counter and kernel, the median over its dispatches; summed over the matching kernels (a
@@ -37,8 +40,9 @@ for f in glob.glob(os.path.join(args.pmc_dir, "**", "*counter_collection.csv"), 
             if args.kernel in r["Kernel_Name"] and r["Counter_Name"] in vals:
                 vals[r["Counter_Name"]].setdefault(r["Kernel_Name"], []).append(float(r["Counter_Value"]))
 assert vals["FETCH_SIZE"] and vals["WRITE_SIZE"], f"no {args.kernel} rows with FETCH_SIZE/WRITE_SIZE under {args.pmc_dir}"
-fetch = sum(statistics.median(v) for v in vals["FETCH_SIZE"].values()) * 1024 * 2  # KiB -> B, x2 gfx950
-write = sum(statistics.median(v) for v in vals["WRITE_SIZE"].values()) * 1024
+agg = (lambda v: sum(v) / args.renders) if args.renders else statistics.median
+fetch = sum(agg(v) for v in vals["FETCH_SIZE"].values()) * 1024 * 2  # KiB -> B, x2 gfx950
+write = sum(agg(v) for v in vals["WRITE_SIZE"].values()) * 1024
 out = {
     "workload": args.workload,
     "kernel": args.kernel,

@@ -23,6 +23,10 @@ ap.add_argument("--simds", type=int, default=1024)
 ap.add_argument("--lib", default=os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                                               "raytracer-go_amd", "librtx.so"),
                 help="the library the profiled run loaded: its hash ties the profile to the code (bench.py checks it)")
+ap.add_argument("--renders", type=int, default=0,
+                help="renders in the profiled run (bench.py --steps 1 --warmup 0: 1); every dispatch of the "
+                     "matching kernels (each pass of each sample chunk) is summed and divided by it.  0: the "
+                     "dispatches of one kernel (a one-chunk render)")
 args = ap.parse_args()
 
 # Per counter: the sum over every dispatch of the matching kernels (a tiered render launches its
@@ -40,7 +44,7 @@ for f in sorted(glob.glob(os.path.join(args.pmc_dir, "**", "*counter_collection.
         disp.setdefault((f, r["Counter_Name"], r["Kernel_Name"]), set()).add(r.get("Dispatch_Id", ""))
     break
 assert all(k in vals for k in need), f"missing {need} for {args.kernel} under {args.pmc_dir}"
-renders = {c: max(len(d) for (f, cc, k), d in disp.items() if cc == c) for c in need}
+renders = {c: args.renders or max(len(d) for (f, cc, k), d in disp.items() if cc == c) for c in need}
 insts = vals["SQ_INSTS_VALU"] / renders["SQ_INSTS_VALU"]
 cycles = vals["GRBM_GUI_ACTIVE"] / renders["GRBM_GUI_ACTIVE"] / 8.0
 thread_cycles = vals["SQ_THREAD_CYCLES_VALU"] / renders["SQ_THREAD_CYCLES_VALU"]
