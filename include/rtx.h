@@ -246,8 +246,9 @@ typedef struct rtx_stats {
     uint64_t gather_kind;   /* ABI 6, rtx_render: how the bands were assembled (RTX_GATHER_*)    */
     uint64_t scene_placement; /* ABI 6: where the walk read the scene (RTX_SCENE_IN_LDS / ...)    */
     uint64_t deferred_paths;  /* ABI 8, tiered walk: paths the near pass handed to the far pass  */
-    uint64_t redo_chunks;     /* ABI 8, tiered walk: sample chunks rendered again whole by the far
-                                 walk because the queue of deferred paths overflowed             */
+    uint64_t redo_chunks;     /* ABI 8, tiered walk: sample chunks whose queue of deferred paths
+                                 overflowed: the samples that did not fit were rendered again from
+                                 their camera rays on the far tree (the rest of the chunk is not) */
 } rtx_stats;
 #define RTX_SCENE_IN_HBM 0u    /* entries from HBM (through L2)                                   */
 #define RTX_SCENE_IN_LDS 1u    /* the whole scene and its materials copied into LDS per workgroup */
@@ -308,16 +309,19 @@ int rtx_scene_create(const rtx_scene_desc* desc, rtx_scene** out);
  * rtx_stats.node_visits.  RTX_SCENE_EVERY_BOX (or RTX_COLLAPSE=0 in the environment) keeps
  * every box test, as bvh.go:220-249 makes them. */
 #define RTX_SCENE_EVERY_BOX 2u
-/* ABI 8.  The tiered walk.  A scene walked over the library's own tree also
- * gets a NEAR tree: the spheres themselves as leaves, each behind its own box grown by the
- * float32 sphere test's error bound for ray origins inside a NEAR REGION (the box of the
- * scene's non-huge spheres grown by its largest extent).  A render whose camera lies in
- * the region walks every segment that starts there on the near tree (3.9x fewer sphere
- * tests on randSpheres); a path whose segment starts outside it is handed, once, to a
- * second pass that continues it on the guarded tree (the reference's leaves).  The closest
- * hit of every segment is the one bvh.go:220-249 returns (DESIGN.md §14 states why and what
- * the tests check).  RTX_SCENE_NO_TIER (or RTX_TIER=0 in the environment) walks the guarded
- * tree alone. */
+/* ABI 8.  The tiered walk.  A scene of spheres under one tree whose node
+ * boxes contain the boxes of the spheres below them (every NewBVH tree) also gets a NEAR tree:
+ * the spheres themselves as leaves, each behind its own box grown by the float32 sphere test's
+ * derived error bound for ray origins inside a NEAR REGION (the box of the scene's non-huge
+ * spheres, grown by its largest extent — by 1 % of it for scenes the rebuild's precision gate
+ * refuses, config 4).  A render whose camera lies in the region walks every segment that starts
+ * there on the near tree, and accepts a near hit only when the sphere's own box passes with the
+ * bound just past it; a path whose segment starts outside the region, or whose near hit fails
+ * that check, is handed, once, to a second pass that continues it on the FAR tree: the guarded
+ * rebuild (the reference's leaves) when the scene has one, else the caller's own tree.  The
+ * closest hit of every segment is the one bvh.go:220-249 returns, ties included (DESIGN.md §15
+ * states why and what the tests check).  RTX_SCENE_NO_TIER (or RTX_TIER=0 in the environment)
+ * walks the far tree alone; RTX_SCENE_REFERENCE_BVH keeps the caller's tree alone. */
 #define RTX_SCENE_NO_TIER 4u
 int rtx_scene_create_ex(const rtx_scene_desc* desc, uint32_t flags, rtx_scene** out);
 
@@ -352,9 +356,8 @@ int rtx_walk_skip(const rtx_scene_desc* desc, uint32_t flags, const rtx_camera* 
 /* ABI 8.  The near region of a tiered scene (box = min xyz, max xyz; a segment whose origin o
  * has box[k] <= o[k] <= box[3 + k] for every k starts in it, a NaN origin does not; box is left
  * alone when the scene has no near tree), and *active = whether renders with `cam` qualify:
- * the camera's rays start in the region, spheres only, no Perlin texture.  (A render also
- * needs both walks in the LDS copy; rtx_stats.walk_layout & RTX_LAYOUT_TIERED says whether it
- * walked in two tiers.)  For tests and tools. */
+ * the camera's rays start in the region, spheres only, no Perlin texture (rtx_stats.walk_layout
+ * & RTX_LAYOUT_TIERED says that a render walked in two tiers).  For tests and tools. */
 int rtx_scene_near_region(rtx_scene* scene, const rtx_camera* cam, float box[6], uint32_t* active);
 /* ABI 8.  rtx_scene_walk_skip of the near walk for `cam` (over rtx_scene_topology's
  * octant | RTX_TREE_NEAR tree). */
