@@ -454,6 +454,47 @@ static int aabb_hit(const rtx_bvh_node* n, const ray_t* r, float tmin, float tma
     return 0;
 }
 
+/* The near walk's slab test (rtx_device.h box_step FMA): the slab distances as
+ * fmaf(b, 1/d, -(o * (1/d))) — one rounding instead of two — for a ray whose 1/d components are
+ * within 2^64 and whose origin is within 2^32 (near_fma_ok); other rays take the reference's form.
+ * The near tree's boxes carry the slack for both forms, and the near walk's result is the
+ * reference's by the hit check whichever boxes pass: only the work counts differ. */
+static int aabb_hit_near(const rtx_bvh_node* n, const ray_t* r, float tmin, float tmax) {
+    const float inv[3] = {1.0f / r->dir.x, 1.0f / r->dir.y, 1.0f / r->dir.z};
+    const float o[3] = {r->origin.x, r->origin.y, r->origin.z};
+    for (int k = 0; k < 3; ++k)
+        if (!(fabsf(inv[k]) <= 0x1p64f && fabsf(o[k]) <= 0x1p32f)) return aabb_hit(n, r, tmin, tmax);
+    for (int k = 0; k < 3; ++k) {
+        const float no = -(o[k] * inv[k]);
+        float t0 = fmaf(n->bmin[k], inv[k], no), t1 = fmaf(n->bmax[k], inv[k], no);
+        if (inv[k] < 0.0f) {
+            const float t = t0;
+            t0 = t1;
+            t1 = t;
+        }
+        if (t0 > tmin) tmin = t0;
+        if (t1 < tmax) tmax = t1;
+        if (!(tmin < tmax)) return 0;
+    }
+    return 1;
+}
+
+/* Test hook: the near walk's slab test (aabb_hit_near) of n rays against n boxes with intervals. */
+void oracle_near_slab_pass(const float* o, const float* d, const float* mn, const float* mx, const float* lo,
+                           const float* hi, uint8_t* out, uint64_t n) {
+    for (uint64_t i = 0; i < n; ++i) {
+        ray_t r;
+        r.origin = v3(o[3 * i], o[3 * i + 1], o[3 * i + 2]);
+        r.dir = v3(d[3 * i], d[3 * i + 1], d[3 * i + 2]);
+        rtx_bvh_node b;
+        for (int k = 0; k < 3; ++k) {
+            b.bmin[k] = mn[3 * i + k];
+            b.bmax[k] = mx[3 * i + k];
+        }
+        out[i] = (uint8_t)aabb_hit_near(&b, &r, lo[i], hi[i]);
+    }
+}
+
 static int hit_ref(const ctx_t* cx, int32_t ref, const ray_t* r, float tmin, float tmax, hit_t* out, int dup,
                    uint32_t trank);
 
@@ -496,7 +537,8 @@ static int bvh_hit(const ctx_t* cx, const rtx_bvh_node* n, const ray_t* r, float
     if (!skip || !skip[id]) {
         cx->c->node_visits++;
         if (g_node_tested && !far) __atomic_fetch_add(&g_node_tested[id], 1, __ATOMIC_RELAXED);
-        if (!aabb_hit(n, r, tmin, tmax)) return 0;                          /* :221 */
+        /* :221; the tiered walk's near tree in its own form */
+        if (!(g_tier_far && !far ? aabb_hit_near(n, r, tmin, tmax) : aabb_hit(n, r, tmin, tmax))) return 0;
         if (g_node_passed && !far) __atomic_fetch_add(&g_node_passed[id], 1, __ATOMIC_RELAXED);
     }
     hit_t hl, hr;

@@ -129,6 +129,12 @@ void oracle_ycbcr_rgba_all(uint32_t* out);
 int oracle_ycbcr_texels(const uint8_t* Y, const uint8_t* Cb, const uint8_t* Cr, int64_t w, int64_t h,
                         int64_t ystride, int64_t cstride, int ratio, uint32_t* out);
 
+/* Test hook: the tiered walk's near-tree slab test (its FMA form) of ray i
+ * (origin o[3i..], direction d[3i..]) against box i (mn, mx) with the interval (lo[i], hi[i]):
+ * out[i] = 1 when it passes. */
+void oracle_near_slab_pass(const float* o, const float* d, const float* mn, const float* mx, const float* lo,
+                           const float* hi, uint8_t* out, uint64_t n);
+
 /* Independent recompute of rtx_region_rows. */
 uint32_t oracle_region_rows(const rtx_region* r);
 

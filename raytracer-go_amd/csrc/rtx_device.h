@@ -661,6 +661,16 @@ struct Trav {
     bool safe;  // 1/dir and the origin finite, a in [2^-60, 2^60]: the SAFE step forms are exact
 };
 
+// The near walk's FMA slab form (box_step FMA) needs products that cannot overflow:
+// |1/d| <= 2^64 per axis and an origin within 2^32 (the near tree's boxes lie within 2^32, topology).
+// Rays outside these bounds take the reference's form, ray by ray (oracle.c restates the rule).
+__device__ __forceinline__ bool near_fma_ok(const Ray& r, const Trav& t) {
+    return __builtin_fabsf(t.ix) <= 0x1p64f && __builtin_fabsf(t.iy) <= 0x1p64f && __builtin_fabsf(t.iz) <= 0x1p64f &&
+           __builtin_fabsf(r.o.x) <= 0x1p32f && __builtin_fabsf(r.o.y) <= 0x1p32f && __builtin_fabsf(r.o.z) <= 0x1p32f;
+}
+
+// FMA (the near pass): a ray is `safe` for the walk's fast forms only when the FMA form applies too.
+template <bool FMA = false>
 __device__ __forceinline__ void trav_begin(Trav& t, const Ray& r, uint32_t start) {
     // InBoundary computes 1/dir per node; hoisting it is bit-identical.
     if (__builtin_amdgcn_ballot_w64(!(rcp_fast_ok(r.d.x) && rcp_fast_ok(r.d.y) && rcp_fast_ok(r.d.z))) == 0) {
@@ -680,6 +690,7 @@ __device__ __forceinline__ void trav_begin(Trav& t, const Ray& r, uint32_t start
     t.safe = __builtin_isfinite(t.ix) && __builtin_isfinite(t.iy) && __builtin_isfinite(t.iz) &&
              __builtin_isfinite(r.o.x) && __builtin_isfinite(r.o.y) && __builtin_isfinite(r.o.z) &&
              t.a >= 0x1p-60f && t.a <= 0x1p60f;
+    if (FMA) t.safe = t.safe && near_fma_ok(r, t);
     t.closest = __builtin_inff();
     t.hit = -1;
     t.i = start;
@@ -844,15 +855,28 @@ __device__ __forceinline__ bool own_box_pass(const Trav& t, const Ray& r, const 
     return lo < hi;
 }
 
-template <bool COUNT, bool MED3 = false>
+// FMA (the near walk): the slab distances as fma(b, 1/d, no) with no = -(o * (1/d))
+// per axis (the caller's, once per phase) — one rounding of b/d - o/d instead of two of (b - o) * (1/d).
+// The near tree's boxes carry the slack for either form (sphere_margin), and its walk is exact by the hit
+// check whatever boxes pass (§14-15), so only the work counts change — as the oracle's near walk restates.
+// Rays outside near_fma_ok take the reference's form (per lane in the select form; the MED3 form runs
+// only when every walking lane's ray is safe, which for the near pass includes near_fma_ok).
+template <bool COUNT, bool MED3 = false, bool FMA = false>
 __device__ __forceinline__ void box_step(Trav& t, const Ray& r, const float4 ea, const float4 eb, int32_t tag,
-                                         Counters& cnt) {
+                                         Counters& cnt, const V3 no = V3{0.0f, 0.0f, 0.0f}) {
     const float tmin = 0.001f;  // ray.go:37
     if (COUNT && __float_as_int(ea.w) != tag) ++cnt.node_visits;  // (not the sentinel: escape == next)
     if constexpr (MED3) {
-        const float tax = (ea.x - r.o.x) * t.ix, tbx = (eb.x - r.o.x) * t.ix;
-        const float tay = (ea.y - r.o.y) * t.iy, tby = (eb.y - r.o.y) * t.iy;
-        const float taz = (ea.z - r.o.z) * t.iz, tbz = (eb.z - r.o.z) * t.iz;
+        float tax, tbx, tay, tby, taz, tbz;
+        if constexpr (FMA) {
+            tax = __builtin_fmaf(ea.x, t.ix, no.x), tbx = __builtin_fmaf(eb.x, t.ix, no.x);
+            tay = __builtin_fmaf(ea.y, t.iy, no.y), tby = __builtin_fmaf(eb.y, t.iy, no.y);
+            taz = __builtin_fmaf(ea.z, t.iz, no.z), tbz = __builtin_fmaf(eb.z, t.iz, no.z);
+        } else {
+            tax = (ea.x - r.o.x) * t.ix, tbx = (eb.x - r.o.x) * t.ix;
+            tay = (ea.y - r.o.y) * t.iy, tby = (eb.y - r.o.y) * t.iy;
+            taz = (ea.z - r.o.z) * t.iz, tbz = (eb.z - r.o.z) * t.iz;
+        }
         const float lo = med3(med3(med3(tmin, tax, tbx), tay, tby), taz, tbz);
         const float hi = med3(med3(med3(t.closest, tax, tbx), tay, tby), taz, tbz);
         const uint32_t take = 0u - (uint32_t)(lo < hi);
@@ -862,12 +886,20 @@ __device__ __forceinline__ void box_step(Trav& t, const Ray& r, const float4 ea,
     // Per axis: t0 = (min - o) * invD, t1 = (max - o) * invD, swapped if invD < 0.
     // (Scalar FP32 throughout: a v_pk_mul_f32 / v_pk_add_f32 issues at a quarter of
     // v_mul_f32's rate on gfx950, scripts/micro/pk_rate.hip, so packing loses 2x.)
-    const float t0x = ((t.nx ? eb.x : ea.x) - r.o.x) * t.ix;
-    const float t1x = ((t.nx ? ea.x : eb.x) - r.o.x) * t.ix;
-    const float t0y = ((t.ny ? eb.y : ea.y) - r.o.y) * t.iy;
-    const float t1y = ((t.ny ? ea.y : eb.y) - r.o.y) * t.iy;
-    const float t0z = ((t.nz ? eb.z : ea.z) - r.o.z) * t.iz;
-    const float t1z = ((t.nz ? ea.z : eb.z) - r.o.z) * t.iz;
+    float t0x = ((t.nx ? eb.x : ea.x) - r.o.x) * t.ix;
+    float t1x = ((t.nx ? ea.x : eb.x) - r.o.x) * t.ix;
+    float t0y = ((t.ny ? eb.y : ea.y) - r.o.y) * t.iy;
+    float t1y = ((t.ny ? ea.y : eb.y) - r.o.y) * t.iy;
+    float t0z = ((t.nz ? eb.z : ea.z) - r.o.z) * t.iz;
+    float t1z = ((t.nz ? ea.z : eb.z) - r.o.z) * t.iz;
+    if (FMA && near_fma_ok(r, t)) {
+        t0x = __builtin_fmaf(t.nx ? eb.x : ea.x, t.ix, no.x);
+        t1x = __builtin_fmaf(t.nx ? ea.x : eb.x, t.ix, no.x);
+        t0y = __builtin_fmaf(t.ny ? eb.y : ea.y, t.iy, no.y);
+        t1y = __builtin_fmaf(t.ny ? ea.y : eb.y, t.iy, no.y);
+        t0z = __builtin_fmaf(t.nz ? eb.z : ea.z, t.iz, no.z);
+        t1z = __builtin_fmaf(t.nz ? ea.z : eb.z, t.iz, no.z);
+    }
     // `if t0 > min { min = t0 }` keeps min on NaN (0 * inf): fmaxf's NaN rule.  The
     // bound only shrinks, so one min < max test after all three axes equals the
     // reference's per-axis early exit.
@@ -889,15 +921,16 @@ __device__ __forceinline__ void box_step(Trav& t, const Ray& r, const float4 ea,
 // running bound `closest` = the closest hit so far (bvh.go:227-232).
 // QUADS: the scene holds quads (a third entry kind); false compiles the sphere-only step.
 // FIXED: E is v3's LDS layout at LDS address 0 (scene_ref_fixed).
-template <bool COUNT, bool QUADS = false, bool FIXED = false, bool HYB = false, bool MED3 = false>
-__device__ __forceinline__ void trav_step(Trav& t, const Ray& r, const SceneRef E, Counters& cnt) {
+template <bool COUNT, bool QUADS = false, bool FIXED = false, bool HYB = false, bool MED3 = false, bool FMA = false>
+__device__ __forceinline__ void trav_step(Trav& t, const Ray& r, const SceneRef E, Counters& cnt,
+                                          const V3 no = V3{0.0f, 0.0f, 0.0f}) {
     float4 ea, eb;
     load_entry<FIXED, HYB>(E, t.i, ea, eb);
     if (COUNT && HYB && t.i < E.hot) ++cnt.cache_hits;
     const int32_t tag = __float_as_int(eb.w);  // device recoding, rtx_layout.h
     // (tag > -2, not tag >= 0: a sign test became a 64-bit compare of eb.z:eb.w)
     if (tag > -2) {  // a node (or the sentinel)
-        box_step<COUNT, MED3>(t, r, ea, eb, tag, cnt);
+        box_step<COUNT, MED3, FMA>(t, r, ea, eb, tag, cnt, no);
     } else {
         if (QUADS && tag == RTX_E_QUAD) quad_test<COUNT>(t, r, E, ea, eb, t.i, cnt);
         else sphere_test<COUNT, MED3, FIXED, !FIXED>(t, r, ea, eb, t.i, cnt, E.b);
@@ -915,9 +948,10 @@ __device__ __forceinline__ void trav_step(Trav& t, const Ray& r, const SceneRef 
 // Returns (COUNT only) the lanes whose entry the step processed, wave-uniform; `idle` gets the
 // lanes parked on the sentinel (low 16 bits) and the lanes whose entry kind the step did not
 // run (high 16 bits).
-template <bool COUNT, bool QUADS, bool FIXED, bool HYB, bool MED3>
+template <bool COUNT, bool QUADS, bool FIXED, bool HYB, bool MED3, bool FMA = false>
 __device__ __forceinline__ uint32_t trav_step_batched(Trav& t, const Ray& r, const SceneRef E, Counters& cnt,
-                                                      uint32_t end, uint32_t kmin, uint32_t& idle) {
+                                                      uint32_t end, uint32_t kmin, uint32_t& idle,
+                                                      const V3 no = V3{0.0f, 0.0f, 0.0f}) {
     float4 ea, eb;
     load_entry<FIXED, HYB>(E, t.i, ea, eb);
     const int32_t tag = __float_as_int(eb.w);
@@ -936,7 +970,7 @@ __device__ __forceinline__ uint32_t trav_step_batched(Trav& t, const Ray& r, con
         }
     } else if (__builtin_amdgcn_inverse_ballot_w64(bm)) {  // lanes on a node (the sentinel's step is a no-op)
         if (COUNT && HYB && t.i < E.hot) ++cnt.cache_hits;
-        box_step<COUNT, MED3>(t, r, ea, eb, tag, cnt);
+        box_step<COUNT, MED3, FMA>(t, r, ea, eb, tag, cnt, no);
     }
     if (COUNT) {
         const uint32_t walking = (uint32_t)__popcll(pm | bm);
@@ -1010,17 +1044,9 @@ __device__ __forceinline__ uint32_t trav_step_batched(Trav& t, const Ray& r, con
 #else
 #define RTX_PRIM_RUN_TAIL(K, WAIT) ""
 #endif
-#define RTX_WALK_STEP_PF(K, LOAD, WAIT, BEND)                                      \
-        "v_cmp_gt_u32_e64 %[pm], %[pe], %[pos]\n\t" /* primitive: pos < prim_end */\
-        "s_bcnt1_i32_b64 %[cnt], %[pm]\n\t"                                  \
-        "s_cmp_ge_u32 %[cnt], %[kmin]\n\t"                                   \
-        "s_cbranch_scc1 LP%=_" #K "\n\t"                                     \
-        "s_andn2_b64 %[wm], %[wk], %[pm]\n\t" /* scc: a node lane */         \
-        "s_cbranch_scc0 LP%=_" #K "\n\t"                                     \
-        /* ---- box tests on the node lanes, then their next entries */      \
-        "s_and_saveexec_b64 %[save], %[wm]\n\t"                              \
-        "LB%=_" #K ":\n\t" /* a box run continues here, exec = its node lanes */\
-        WAIT                                                                 \
+// A box step's slab distances, lo / hi clamped by v_med3 (box_step MED3): the reference's
+// (b - o) * (1/d), or the near walk's fma(b, 1/d, -(o/d)) (box_step FMA: 12 VALU instead of 18).
+#define RTX_SLABS_SUBMUL \
         "v_sub_f32 v0, v0, %[ox]\n\t"                                        \
         "v_sub_f32 v4, v4, %[ox]\n\t"                                        \
         "v_sub_f32 v1, v1, %[oy]\n\t"                                        \
@@ -1038,7 +1064,32 @@ __device__ __forceinline__ uint32_t trav_step_batched(Trav& t, const Ray& r, con
         "v_med3_f32 v8, v8, v1, v5\n\t"                                      \
         "v_med3_f32 v9, v9, v1, v5\n\t"                                      \
         "v_med3_f32 v8, v8, v2, v6\n\t"                                      \
-        "v_med3_f32 v9, v9, v2, v6\n\t"                                      \
+        "v_med3_f32 v9, v9, v2, v6\n\t"
+#define RTX_SLABS_FMA                                                        \
+        "v_fma_f32 v0, v0, %[ix], %[nox]\n\t"                                \
+        "v_fma_f32 v4, v4, %[ix], %[nox]\n\t"                                \
+        "v_fma_f32 v1, v1, %[iy], %[noy]\n\t"                                \
+        "v_fma_f32 v5, v5, %[iy], %[noy]\n\t"                                \
+        "v_med3_f32 v8, %[tmin], v0, v4\n\t"                                 \
+        "v_med3_f32 v9, %[cl], v0, v4\n\t"                                   \
+        "v_fma_f32 v2, v2, %[iz], %[noz]\n\t"                                \
+        "v_fma_f32 v6, v6, %[iz], %[noz]\n\t"                                \
+        "v_med3_f32 v8, v8, v1, v5\n\t"                                      \
+        "v_med3_f32 v9, v9, v1, v5\n\t"                                      \
+        "v_med3_f32 v8, v8, v2, v6\n\t"                                      \
+        "v_med3_f32 v9, v9, v2, v6\n\t"
+#define RTX_WALK_STEP_PF(K, LOAD, WAIT, BEND, SLABS)                               \
+        "v_cmp_gt_u32_e64 %[pm], %[pe], %[pos]\n\t" /* primitive: pos < prim_end */\
+        "s_bcnt1_i32_b64 %[cnt], %[pm]\n\t"                                  \
+        "s_cmp_ge_u32 %[cnt], %[kmin]\n\t"                                   \
+        "s_cbranch_scc1 LP%=_" #K "\n\t"                                     \
+        "s_andn2_b64 %[wm], %[wk], %[pm]\n\t" /* scc: a node lane */         \
+        "s_cbranch_scc0 LP%=_" #K "\n\t"                                     \
+        /* ---- box tests on the node lanes, then their next entries */      \
+        "s_and_saveexec_b64 %[save], %[wm]\n\t"                              \
+        "LB%=_" #K ":\n\t" /* a box run continues here, exec = its node lanes */\
+        WAIT                                                                 \
+        SLABS                                                                \
         "v_cmp_lt_f32_e32 vcc, v8, v9\n\t"                                   \
         "s_nop 1\n\t"                                                        \
         "v_cndmask_b32_e32 %[pos], v3, v7, vcc\n\t"                          \
@@ -1106,7 +1157,7 @@ __device__ __forceinline__ uint32_t trav_step_batched(Trav& t, const Ray& r, con
         "LR%=_" #K ":\n\t"                                                   \
         "s_mov_b64 exec, %[save]\n"                                          \
         "LE%=_" #K ":\n\t"
-#define RTX_WALK_STEP_PFQ(K, LOAD, WAIT, BEND)                                      \
+#define RTX_WALK_STEP_PFQ(K, LOAD, WAIT, BEND, SLABS)                               \
         "v_cmp_gt_u32_e64 %[pm], %[pe], %[pos]\n\t" /* primitive: pos < prim_end */\
         "s_bcnt1_i32_b64 %[cnt], %[pm]\n\t"                                  \
         "s_cmp_ge_u32 %[cnt], %[kmin]\n\t"                                   \
@@ -1117,24 +1168,7 @@ __device__ __forceinline__ uint32_t trav_step_batched(Trav& t, const Ray& r, con
         "s_and_saveexec_b64 %[save], %[wm]\n\t"                              \
         "LB%=_" #K ":\n\t" /* a box run continues here, exec = its node lanes */\
         WAIT                                                                 \
-        "v_sub_f32 v0, v0, %[ox]\n\t"                                        \
-        "v_sub_f32 v4, v4, %[ox]\n\t"                                        \
-        "v_sub_f32 v1, v1, %[oy]\n\t"                                        \
-        "v_sub_f32 v5, v5, %[oy]\n\t"                                        \
-        "v_mul_f32 v0, v0, %[ix]\n\t"                                        \
-        "v_mul_f32 v4, v4, %[ix]\n\t"                                        \
-        "v_sub_f32 v2, v2, %[oz]\n\t"                                        \
-        "v_sub_f32 v6, v6, %[oz]\n\t"                                        \
-        "v_mul_f32 v1, v1, %[iy]\n\t"                                        \
-        "v_mul_f32 v5, v5, %[iy]\n\t"                                        \
-        "v_med3_f32 v8, %[tmin], v0, v4\n\t"                                 \
-        "v_med3_f32 v9, %[cl], v0, v4\n\t"                                   \
-        "v_mul_f32 v2, v2, %[iz]\n\t"                                        \
-        "v_mul_f32 v6, v6, %[iz]\n\t"                                        \
-        "v_med3_f32 v8, v8, v1, v5\n\t"                                      \
-        "v_med3_f32 v9, v9, v1, v5\n\t"                                      \
-        "v_med3_f32 v8, v8, v2, v6\n\t"                                      \
-        "v_med3_f32 v9, v9, v2, v6\n\t"                                      \
+        SLABS                                                                \
         "v_cmp_lt_f32_e32 vcc, v8, v9\n\t"                                   \
         "s_nop 1\n\t"                                                        \
         "v_cndmask_b32_e32 %[pos], v3, v7, vcc\n\t"                          \
@@ -1368,16 +1402,18 @@ __device__ __forceinline__ uint32_t trav_step_batched(Trav& t, const Ray& r, con
 #define RTX_COLD_BLOCK_(n) RTX_COLD_##n
 #define RTX_COLD_BLOCK(n) RTX_COLD_BLOCK_(n)
 // QUADS: the scene holds quads (RTX_WALK_STEP_PFQ; the quad table at LDS byte qbase).
-template <bool QUADS = false>
+// FMA: the near walk's slab form (box_step FMA), no = -(o * (1/d)) per axis (sphere scenes).
+template <bool QUADS = false, bool FMA = false>
 __device__ __forceinline__ uint64_t walk_phase_asm(Trav& t, const Ray& r, uint32_t end, uint32_t kmin, float tmin,
                                                    uint64_t W, uint64_t P0, uint32_t thresh, uint32_t prim_end,
-                                                   uint32_t qbase = 0) {
+                                                   uint32_t qbase = 0, const V3 no = V3{0.0f, 0.0f, 0.0f}) {
     static_assert(LDS_B == 32768, "the asm reads the 'b' halves at offset:32768");
+    static_assert(!(QUADS && FMA), "the FMA form is the near walk's: sphere scenes");
     uint64_t pm, wm, save, g1, l1, l2, wk;
     uint32_t cnt;
     if constexpr (QUADS) {
         uint64_t qm, qs;
-#define S(K, BEND) RTX_WALK_STEP_PFQ(K, RTX_LOAD_LDS, RTX_WAIT_LDS, BEND)
+#define S(K, BEND) RTX_WALK_STEP_PFQ(K, RTX_LOAD_LDS, RTX_WAIT_LDS, BEND, RTX_SLABS_SUBMUL)
         asm volatile(RTX_LOAD_LDS "v_cmp_lt_u32_e64 %[wk], %[pos], %[end]\nLW%=:\n\t" RTX_WALK_BLOCK(RTX_ASM_BLOCK_Q) RTX_WALK_VOTE
                      "\n\ts_branch LZ%=\n" RTX_COLD_BLOCK(RTX_ASM_BLOCK_Q) "LZ%=:\n\ts_waitcnt lgkmcnt(0)"
                      : RTX_WALK_OUTS, [qm] "=&s"(qm), [qs] "=&s"(qs)
@@ -1385,8 +1421,16 @@ __device__ __forceinline__ uint64_t walk_phase_asm(Trav& t, const Ray& r, uint32
                      : RTX_WALK_CLOBBERS, "v17", "v18", "v19", "v20", "v21", "v22", "v23", "v24", "v25", "v26", "v27",
                        "v28", "v29", "v30", "v31", "v32", "v33", "v34");
 #undef S
+    } else if constexpr (FMA) {
+#define S(K, BEND) RTX_WALK_STEP_PF(K, RTX_LOAD_LDS, RTX_WAIT_LDS, BEND, RTX_SLABS_FMA)
+        asm volatile(RTX_LOAD_LDS "v_cmp_lt_u32_e64 %[wk], %[pos], %[end]\nLW%=:\n\t" RTX_WALK_BLOCK(RTX_ASM_BLOCK) RTX_WALK_VOTE
+                     "\n\ts_branch LZ%=\n" RTX_COLD_BLOCK(RTX_ASM_BLOCK) "LZ%=:\n\ts_waitcnt lgkmcnt(0)"
+                     : RTX_WALK_OUTS
+                     : RTX_WALK_INS, [nox] "v"(no.x), [noy] "v"(no.y), [noz] "v"(no.z)
+                     : RTX_WALK_CLOBBERS);
+#undef S
     } else {
-#define S(K, BEND) RTX_WALK_STEP_PF(K, RTX_LOAD_LDS, RTX_WAIT_LDS, BEND)
+#define S(K, BEND) RTX_WALK_STEP_PF(K, RTX_LOAD_LDS, RTX_WAIT_LDS, BEND, RTX_SLABS_SUBMUL)
         asm volatile(RTX_LOAD_LDS "v_cmp_lt_u32_e64 %[wk], %[pos], %[end]\nLW%=:\n\t" RTX_WALK_BLOCK(RTX_ASM_BLOCK) RTX_WALK_VOTE
                      "\n\ts_branch LZ%=\n" RTX_COLD_BLOCK(RTX_ASM_BLOCK) "LZ%=:\n\ts_waitcnt lgkmcnt(0)"
                      : RTX_WALK_OUTS
@@ -1398,6 +1442,8 @@ __device__ __forceinline__ uint64_t walk_phase_asm(Trav& t, const Ray& r, uint32
 }
 #undef RTX_WALK_STEP_PF
 #undef RTX_WALK_STEP_PFQ
+#undef RTX_SLABS_SUBMUL
+#undef RTX_SLABS_FMA
 #undef RTX_PRIM_RUN_TAIL
 #undef RTX_WALK_4
 #undef RTX_WALK_5

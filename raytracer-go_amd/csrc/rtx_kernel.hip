@@ -33,6 +33,9 @@
 #ifndef RTX_ASM_STEP  // 1: the timed kernel's walk step in assembly (trav_step_asm); 0 for A/B
 #define RTX_ASM_STEP 1
 #endif
+#ifndef RTX_NEAR_FMA  // 1: the near pass's slab tests in the FMA form (box_step FMA); 0 for A/B
+#define RTX_NEAR_FMA 1
+#endif
 
 namespace rtxd {
 
@@ -65,7 +68,7 @@ __device__ __forceinline__ void flush_sched(const Params& p, uint64_t wi, uint64
 // STEPS > 1 takes up to STEPS entries per lane between two wave votes.  (A branch-free
 // step that evaluates the box and the sphere test on every lane measured 8 % slower:
 // most waves hold only box entries at a step, and the branch skips the sphere test.)
-template <bool COUNT, int STEPS, bool QUADS, bool FIXED, bool HYB, bool BATCH, bool MED3>
+template <bool COUNT, int STEPS, bool QUADS, bool FIXED, bool HYB, bool BATCH, bool MED3, bool FMA = false>
 __device__ __forceinline__ void traverse_loop(uint32_t& mode, Trav& t, const Ray& r, const SceneRef E,
                                               uint32_t n_entries, uint32_t thresh, Counters& cnt,
                                               uint64_t& wave_iters, uint64_t& lane_steps, uint64_t& shade_phases,
@@ -76,12 +79,14 @@ __device__ __forceinline__ void traverse_loop(uint32_t& mode, Trav& t, const Ray
     // lanes P0, lanes without an item D; per iteration only `at_end` is voted.
     const uint64_t W = ballot(mode == 0), P0 = ballot(mode - 1u < 2u);
     const uint64_t D = COUNT ? ballot(mode == 3) : 0ull;
+    // FMA (the near pass): the slab form's -(o / d) per axis, once per phase (box_step FMA)
+    const V3 no = FMA ? v3(-(r.o.x * t.ix), -(r.o.y * t.iy), -(r.o.z * t.iz)) : v3(0.0f, 0.0f, 0.0f);
     // The asm walk (walk_phase_asm) for scenes in LDS (spheres, and quads).  (For config 4's scene in HBM with
     // its top levels in LDS an asm walk lost to this C++ one: +9 % batched, +23 % running both
     // kinds per step)
     if constexpr (RTX_ASM_STEP && BATCH && !COUNT && FIXED && !HYB && MED3) {
-        const uint64_t at_end = walk_phase_asm<QUADS>(t, r, 16 * n_entries, prim_batch, 0.001f, W, P0, thresh,
-                                                      E.prim_end, LDS_B + 16 * (n_entries + 1));  // quad table
+        const uint64_t at_end = walk_phase_asm<QUADS, FMA>(t, r, 16 * n_entries, prim_batch, 0.001f, W, P0, thresh,
+                                                           E.prim_end, LDS_B + 16 * (n_entries + 1), no);  // quad table
         if (__builtin_amdgcn_inverse_ballot_w64(W & at_end)) mode = 1;  // walked to the end
         return;
     }
@@ -94,8 +99,8 @@ __device__ __forceinline__ void traverse_loop(uint32_t& mode, Trav& t, const Ray
         if constexpr (BATCH) {
 #pragma unroll
             for (int s = 0; s < STEPS; ++s)
-                done += trav_step_batched<COUNT, QUADS, FIXED, HYB, MED3>(t, r, E, cnt, 16 * n_entries, prim_batch,
-                                                                         idle);
+                done += trav_step_batched<COUNT, QUADS, FIXED, HYB, MED3, FMA>(t, r, E, cnt, 16 * n_entries,
+                                                                              prim_batch, idle, no);
         } else {
 #pragma unroll
             for (int s = 0; s < STEPS; ++s) {
@@ -104,7 +109,7 @@ __device__ __forceinline__ void traverse_loop(uint32_t& mode, Trav& t, const Ray
                     done += w;
                     idle += 64u - w;
                 }
-                trav_step<COUNT, QUADS, FIXED, HYB, MED3>(t, r, E, cnt);
+                trav_step<COUNT, QUADS, FIXED, HYB, MED3, FMA>(t, r, E, cnt, no);
             }
         }
         const uint64_t at_end = ballot(t.i >= 16 * n_entries);
@@ -132,20 +137,23 @@ __device__ __forceinline__ void traverse_loop(uint32_t& mode, Trav& t, const Ray
 // 1/dir and origin — all but a handful of rays per frame —, else the select form for the whole
 // phase.  (A lane's ray is fixed for the phase; lanes parked on the sentinel do not matter: a
 // step there changes nothing either way.)
-template <bool COUNT, int STEPS = 1, bool QUADS = false, bool FIXED = false, bool HYB = false, bool BATCH = false>
+template <bool COUNT, int STEPS = 1, bool QUADS = false, bool FIXED = false, bool HYB = false, bool BATCH = false,
+          bool FMA = false>
 __device__ __forceinline__ void traverse_phase(uint32_t& mode, Trav& t, const Ray& r, const SceneRef E,
                                                uint32_t n_entries, uint32_t thresh, Counters& cnt,
                                                uint64_t& wave_iters, uint64_t& lane_steps, uint64_t& shade_phases,
                                                uint64_t& shade_lanes, uint64_t& idle_lanes, uint64_t& parked,
                                                uint64_t& deferred, uint32_t prim_batch = 0) {
     if (ballot(!t.safe && t.i < 16 * n_entries) == 0)
-        traverse_loop<COUNT, STEPS, QUADS, FIXED, HYB, BATCH, true>(mode, t, r, E, n_entries, thresh, cnt, wave_iters,
-                                                                  lane_steps, shade_phases, shade_lanes, idle_lanes,
-                                                                  parked, deferred, prim_batch);
+        traverse_loop<COUNT, STEPS, QUADS, FIXED, HYB, BATCH, true, FMA>(mode, t, r, E, n_entries, thresh, cnt,
+                                                                       wave_iters, lane_steps, shade_phases,
+                                                                       shade_lanes, idle_lanes, parked, deferred,
+                                                                       prim_batch);
     else
-        traverse_loop<COUNT, STEPS, QUADS, FIXED, HYB, BATCH, false>(mode, t, r, E, n_entries, thresh, cnt,
-                                                                   wave_iters, lane_steps, shade_phases, shade_lanes,
-                                                                   idle_lanes, parked, deferred, prim_batch);
+        traverse_loop<COUNT, STEPS, QUADS, FIXED, HYB, BATCH, false, FMA>(mode, t, r, E, n_entries, thresh, cnt,
+                                                                        wave_iters, lane_steps, shade_phases,
+                                                                        shade_lanes, idle_lanes, parked, deferred,
+                                                                        prim_batch);
 }
 
 enum : uint32_t { M_TRAV = 0, M_SHADE = 1, M_START = 2, M_DONE = 3, M_CLAIM = 4 };
@@ -335,7 +343,7 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
         if (TIME) clk = __builtin_amdgcn_s_memtime();
         // primitive batching only for a scene in LDS: a lane that waits re-reads its entry, which
         // from HBM cost config 4 +34 %
-        traverse_phase<COUNT, STEPS, QUADS, USE_LDS, HYB, USE_LDS || (RTX_HYB_BATCH && HYB)>(
+        traverse_phase<COUNT, STEPS, QUADS, USE_LDS, HYB, USE_LDS || (RTX_HYB_BATCH && HYB), TIER == 1 && RTX_NEAR_FMA>(
             mode, t, r, E, n_entries, thresh, cnt, wave_iters,
                                                               lane_steps, shade_phases, shade_lanes, idle_lanes,
                                                               parked, deferred, p.prim_batch);
@@ -472,7 +480,7 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
         if (TIME) split_clk(split[2], clk);
         if (ready) {  // begin a segment: world.Hit (ray.go:36)
             if (COUNT) ++cnt.segments;
-            trav_begin(t, r, p.start);
+            trav_begin<TIER == 1 && RTX_NEAR_FMA>(t, r, p.start);
             mode = n_entries > 0 ? M_TRAV : M_SHADE;
         }
         if (TIME) split_clk(split[3], clk);

@@ -63,11 +63,12 @@ bool build_topology(const std::vector<rtx_entry>& ref, bool guarded, Topology& o
 bool near_region(const std::vector<rtx_entry>& ref, float box[6], double grow = 1.0);
 
 // How far outside a sphere (centre c, radius r) the float32 sphere test (hittables.go:96-116) can
-// put a hit for a ray origin at distance <= dmax from c, with room for the slab test's rounding:
-// rho - r + 2^-20 (dmax + rho), rho = sqrt(r^2 + 24u (dmax^2 + r^2)), u = 2^-24 — the forward-error
-// bound derived in DESIGN.md §14 (the computed discriminant is within 24u |d|^2 (D^2 + r^2) of the
-// exact one; the measured worst case over 4e7 near-tangent rays is 9.5u).
-double sphere_margin(double r, double dmax);
+// put a hit for a ray origin at distance <= dmax from c (its coordinates <= omax in magnitude), with
+// room for the slab test's rounding in either form (the reference's and the near walk's FMA form):
+// rho - r + 2^-20 (dmax + rho) + 2^-23 omax, rho = sqrt(r^2 + 24u (dmax^2 + r^2)), u = 2^-24 — the
+// forward-error bound derived in DESIGN.md §15.1 (the computed discriminant is within
+// 24u |d|^2 (D^2 + r^2) of the exact one; the adversarial test meets at most 8.1u).
+double sphere_margin(double r, double dmax, double omax);
 
 // Whether the scene's spheres are small against the float32 sphere test's error (see the .hip):
 // the gate of the default (guarded) rebuild.

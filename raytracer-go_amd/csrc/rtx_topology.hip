@@ -267,12 +267,14 @@ bool near_region(const std::vector<rtx_entry>& ref, float box[6], double grow) {
     return true;
 }
 
-// The forward-error bound of DESIGN.md §14 (u = 2^-24): a computed disc >= 0 puts the ray's line
+// The forward-error bound of DESIGN.md §15.1 (u = 2^-24): a computed disc >= 0 puts the ray's line
 // within rho = sqrt(r^2 + 24u (D^2 + r^2)) of the centre, and the reported root's point within
-// rho + 11u D + 7u rho of it; the slab test of the grown box passes it with 3u (D + r + m) to spare.
-double sphere_margin(double r, double dmax) {
+// rho + 11u D + 7u rho of it; the slab test of the grown box passes it with 3u (D + r + m) to spare,
+// and its FMA form (fma(b, 1/d, -(o/d)), the near walk's: §15.5) with 2u (D + r + m) + u omax, omax
+// bounding the origin's coordinates.
+double sphere_margin(double r, double dmax, double omax) {
     const double rho = std::sqrt(r * r + 3.0 * std::ldexp(dmax * dmax + r * r, -21));  // 24u = 3 * 2^-21
-    return rho - r + std::ldexp(dmax + rho, -20);                                      // + 16u (D + rho)
+    return rho - r + std::ldexp(dmax + rho, -20) + std::ldexp(omax, -23);              // + 16u (D + rho) + 2u omax
 }
 
 bool build_topology(const std::vector<rtx_entry>& ref, bool guarded, Topology& out, const float* near_box) {
@@ -323,16 +325,18 @@ bool build_topology(const std::vector<rtx_entry>& ref, bool guarded, Topology& o
             item_ref[u] = (int32_t)(t.n_internal + u);
         } else if (near_box) {  // the sphere's box grown by its margin for origins in the near region
             const double r = std::fabs((double)h.a[3]);
-            double d2 = 0.0;  // farthest corner of the region from the centre
+            double d2 = 0.0, omax = 0.0;  // farthest corner of the region from the centre; its largest coordinate
             for (int k = 0; k < 3; ++k) {
                 const double lo = (double)near_box[k] - h.a[k], hi = (double)near_box[3 + k] - h.a[k];
                 d2 += std::max(lo * lo, hi * hi);
+                omax = std::max({omax, std::fabs((double)near_box[k]), std::fabs((double)near_box[3 + k])});
             }
-            const double m = sphere_margin(r, std::sqrt(d2));
+            const double m = sphere_margin(r, std::sqrt(d2), omax);
             for (int k = 0; k < 3; ++k) {  // rounded outward
                 boxes[u].mn[k] = std::nextafter((float)((double)h.a[k] - r - m), -INFINITY);
                 boxes[u].mx[k] = std::nextafter((float)((double)h.a[k] + r + m), INFINITY);
-                if (!std::isfinite(boxes[u].mn[k]) || !std::isfinite(boxes[u].mx[k])) return false;
+                // finite, and within 2^32: the near walk's FMA slab form cannot overflow (§15.5)
+                if (!(std::fabs(boxes[u].mn[k]) <= 0x1p32f) || !(std::fabs(boxes[u].mx[k]) <= 0x1p32f)) return false;
             }
             item_ref[u] = RTX_REF_PRIM(RTX_PRIM_SPHERE, word(&h.b[1]));
         } else {  // the sphere's box: NewSphere's NewAabb(center - r, center + r), hittables.go:85-94

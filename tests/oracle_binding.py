@@ -93,6 +93,8 @@ def load():
     L.oracle_tier.restype = None
     L.oracle_sphere_rank.argtypes = [c_void_p]
     L.oracle_sphere_rank.restype = None
+    L.oracle_near_slab_pass.argtypes = [c_void_p] * 7 + [c_uint64]
+    L.oracle_near_slab_pass.restype = None
     _lib = L
     return L
 
@@ -274,3 +276,11 @@ def rand_spheres_camera(width: int = 400, spp: int = 500, depth: int = 50) -> rt
     return camera(np.float32(16.0) / np.float32(9.0), width, samples_per_pixel=spp, max_depth=depth,
                   look_from=(13, 2, 3), look_at=(0, 0, 0), fov_degrees=20, defocus_degrees=0.6,
                   focus_dist=10, background=(0.7, 0.8, 1.0))
+
+
+def near_slab_pass(o, d, mn, mx, lo, hi):
+    """The near walk's slab test (oracle_near_slab_pass: the FMA form for rays within its bounds), elementwise."""
+    arrs = [np.ascontiguousarray(a, np.float32) for a in (o, d, mn, mx, lo, hi)]
+    out = np.zeros(len(arrs[0]), np.uint8)
+    load().oracle_near_slab_pass(*[a.ctypes.data_as(c_void_p) for a in arrs], out.ctypes.data_as(c_void_p), len(out))
+    return out.astype(bool)

@@ -40,11 +40,11 @@ def sphere_index(ref):
     return p & 0x0FFFFFFF
 
 
-def margin(r, dmax):
-    """rtx_topology.h sphere_margin, restated: rho - r + 2^-20 (dmax + rho), rho = sqrt(r^2 + 24u (dmax^2 + r^2)),
-    u = 2^-24 (the forward-error bound of DESIGN.md §14)."""
+def margin(r, dmax, omax):
+    """rtx_topology.h sphere_margin, restated: rho - r + 2^-20 (dmax + rho) + 2^-23 omax, rho = sqrt(r^2 + 24u
+    (dmax^2 + r^2)), u = 2^-24 (the forward-error bound of DESIGN.md §15.1)."""
     rho = math.sqrt(r * r + 3.0 * math.ldexp(dmax * dmax + r * r, -21))
-    return rho - r + math.ldexp(dmax + rho, -20)
+    return rho - r + math.ldexp(dmax + rho, -20) + math.ldexp(omax, -23)
 
 
 def spheres_of(desc):
@@ -113,7 +113,7 @@ def test_near_tree_shape(built, scene):
             seen_sph[j] += 1
             rr = abs(float(r[j]))
             dmax = float(np.sqrt(((corners - c[j].astype(np.float64)) ** 2).sum(1)).max())
-            m = margin(rr, dmax)
+            m = margin(rr, dmax, float(np.abs(corners).max()))
             for k in range(3):
                 assert nd.bmin[k] <= float(c[j][k]) - rr - m and nd.bmax[k] >= float(c[j][k]) + rr + m
     assert (seen_nodes == 1).all() and (seen_sph == 1).all()
@@ -274,7 +274,7 @@ def test_margin_bound_adversarial(built, scene, n_spheres):
         D = np.linalg.norm(oh - ch, axis=1)
         dist = np.linalg.norm(oh + th[:, None] * dh - ch, axis=1)
         rho = np.sqrt(rh * rh + 3.0 * np.ldexp(D * D + rh * rh, -21))  # margin(), vectorised
-        m = rho - rh + np.ldexp(D + rho, -20)
+        m = rho - rh + np.ldexp(D + rho, -20) + np.ldexp(np.abs(corners).max(), -23)
         assert (dist <= rh + m).all(), int((dist > rh + m).sum())
         k_max = max(k_max, float(((dist * dist - rh * rh) / (u * (D * D + rh * rh))).max()))
         bound = np.nextafter(t[hit], F(np.inf))
@@ -284,9 +284,11 @@ def test_margin_bound_adversarial(built, scene, n_spheres):
             if not sel.any():
                 break
             nodes = chain[sel, lev]
-            ok = slab_pass(o[hit][sel], d[hit][sel], bmin[nodes], bmax[nodes], np.full(int(sel.sum()), F(0.001)),
-                           bound[sel])
+            args = (o[hit][sel], d[hit][sel], bmin[nodes], bmax[nodes], np.full(int(sel.sum()), F(0.001)), bound[sel])
+            ok = slab_pass(*args)  # the reference's form
             assert ok.all(), (lev, int((~ok).sum()))
+            ok = ob.near_slab_pass(*args)  # the near walk's FMA form (§15.5)
+            assert ok.all(), ("fma", lev, int((~ok).sum()))
     assert n_hits > 10_000
     assert k_max < 24.0, k_max
     print(f"{scene}: {n_hits} reported hits, largest K = {k_max:.2f} (the margin assumes 24)")
