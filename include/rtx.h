@@ -313,8 +313,8 @@ int rtx_scene_create(const rtx_scene_desc* desc, rtx_scene** out);
  * boxes contain the boxes of the spheres below them (every NewBVH tree) also gets a NEAR tree:
  * the spheres themselves as leaves, each behind its own box grown by the float32 sphere test's
  * derived error bound for ray origins inside a NEAR REGION (the box of the scene's non-huge
- * spheres, grown by its largest extent — by 1 % of it for scenes the rebuild's precision gate
- * refuses, config 4).  A render whose camera lies in the region walks every segment that starts
+ * spheres, grown by 1.5 times its largest extent — by 1 % of it for scenes the rebuild's precision
+ * gate refuses, config 4).  A render whose camera lies in the region walks every segment that starts
  * there on the near tree, and accepts a near hit only when the sphere's own box passes with the
  * bound just past it; a path whose segment starts outside the region, or whose near hit fails
  * that check, is handed, once, to a second pass that continues it on the FAR tree: the guarded

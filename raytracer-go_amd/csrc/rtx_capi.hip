@@ -731,17 +731,18 @@ int topology_mode(uint32_t flags, const std::vector<rtx_entry>& ref) {
 // RTX_SCENE_REFERENCE_BVH or RTX_TIER=0, or a node box does not contain the boxes of the spheres
 // below it (the hit check's argument needs that; NewBVH's always do).  Its far tree is the walk's
 // other tree: the guarded rebuild, or the caller's.  The region is the core box grown by
-// RTX_NEAR_GROW percent of its largest extent: 100 for scenes that pass precise_enough (randSpheres:
-// C2 at 100 spp 10 / 25 / 40 / 60 / 100 % -> 23.73 / 23.43 / 23.21 / 22.89 / 22.67 ms, 3.6 / 3.2 / 2.6 /
-// 1.8 / 0.9 % of the paths deferred), 1 for the others (config 4's 316-unit slab: its far spheres'
-// margins already set the boxes; the region need only hold the camera and the slab).
+// RTX_NEAR_GROW percent of its largest extent: 150 for scenes that pass precise_enough (randSpheres,
+// C2 at 100 spp, round 4's margins and FMA walk: 50 / 100 / 150 / 200 / 300 % -> 21.73 / 21.02 / 20.65 /
+// 20.73 / 21.05 ms; round 3: 10 / 25 / 40 / 60 / 100 % -> 23.73 / 23.43 / 23.21 / 22.89 / 22.67 ms),
+// 1 for the others (config 4's 316-unit slab, whose far corners set every margin anyway: 0 (untiered) /
+// 1 / 2 / 5 % -> 100.9 / 76.6 / 77.2 / 78.9 ms).
 bool tier_topology(uint32_t flags, const std::vector<rtx_entry>& base, rtxd::Topology& near) {
     if (flags & (RTX_SCENE_NO_TIER | RTX_SCENE_REFERENCE_BVH)) return false;
     const char* e = std::getenv("RTX_TIER");
     if (e && std::strcmp(e, "0") == 0) return false;
     if (!rtxd::own_boxes_nested(base)) return false;
     float box[6];
-    const double grow = env_knob("RTX_NEAR_GROW", rtxd::precise_enough(base) ? 100 : 1, 0, 1000) / 100.0;
+    const double grow = env_knob("RTX_NEAR_GROW", rtxd::precise_enough(base) ? 150 : 1, 0, 1000) / 100.0;
     return rtxd::near_region(base, box, grow) && rtxd::build_topology(base, false, near, box);
 }
 
