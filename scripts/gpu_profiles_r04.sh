@@ -16,6 +16,9 @@ add c3 "random_spheres:1920x1080x2000" "--spp 2000"
 add c4 "stress_100k:1920x1080x100" "--scene stress_100k --spp 100"
 add c5 "earth_dielectric:3840x2160x1000" "--scene earth_dielectric --width 3840 --spp 1000"
 add cornell "cornell_box:600x600x200" "--scene cornell_box --width 600 --spp 200"
+add quad "quad_demo:400x225x100" "--scene quad_demo --width 400 --spp 100"
+add perlin "perlin_demo:400x225x100" "--scene perlin_demo --width 400 --spp 100"
+add light "simple_light_demo:400x225x500" "--scene simple_light_demo --width 400 --spp 500"
 add c2_r0of2 "random_spheres:1920x1080x500/rows0of2" "--shard 0/2"
 add c2_r0of4 "random_spheres:1920x1080x500/rows0of4" "--shard 0/4"
 add c2_r0of8 "random_spheres:1920x1080x500/rows0of8" "--shard 0/8"
