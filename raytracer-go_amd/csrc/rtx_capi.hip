@@ -881,6 +881,9 @@ rtxd::Params make_params(const rtx_scene* s, const DeviceCopy* c, uint32_t oct, 
     p.rows = region_rows(r);
     p.rank = r->rank;
     p.world = r->world;
+    // RTX_TILE_W = 8 / 16 / 32 overrides the tile width (A/B)
+    const uint32_t tw = env_knob("RTX_TILE_W", 0, 0, 32);
+    p.tile_w_log2 = tw >= 32 ? 5u : (tw >= 16 ? 4u : (tw >= 8 ? 3u : rtxd::tile_w_log2_for(r->world)));
     p.out = d_out;
     p.counters = c->counters;
     p.tile_counter = reinterpret_cast<uint32_t*>(c->counters + 7);  // slot 7 low: unit queue head
@@ -923,8 +926,9 @@ int enqueue_on(rtx_scene* s, DeviceCopy* c, const rtx_camera* cam, uint64_t seed
     if (p.width > 0 && p.rows > 0) {
         // Sample scratch: up to RTX_SCRATCH_MB (default 16 GiB of the 288 GB HBM) of sample
         // colours, 12 B each; the samples run in chunks that fit.
-        // tile-major: every 8x8 tile whole (render_items / reduce_samples), 12 B per pixel
-        const uint64_t per_sample = (uint64_t)((p.width + 7) / 8) * ((p.rows + 7) / 8) * 64 * 12;
+        // tile-major: every tile of 64 pixels whole (render_items / reduce_samples), 12 B per pixel
+        const uint64_t per_sample =
+            (uint64_t)rtxd::tiles_x_of(p.width, p.tile_w_log2) * rtxd::tiles_y_of(p.rows, p.tile_w_log2) * 64 * 12;
         const uint64_t budget = (uint64_t)env_knob("RTX_SCRATCH_MB", 16384, 1, 1 << 20) << 20;
         uint64_t chunk = budget / per_sample;
         if (chunk > cam->samples_per_pixel) chunk = cam->samples_per_pixel;

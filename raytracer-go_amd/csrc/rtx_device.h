@@ -438,6 +438,7 @@ struct Params {
     rtx_camera cam;
     uint64_t seed;
     uint32_t x0, y0, width, rows, rank, world;
+    uint32_t tile_w_log2;  // a tile of 64 pixels is (1 << tile_w_log2) wide (8 or 16) and 64 >> tile_w_log2 rows tall
     float* out;
     unsigned long long* counters;  // rtx_stats order when counting (COUNTER_SLOTS x u64)
     uint32_t shade_thresh;         // shade once this many lanes of a wave wait (1..64)
@@ -479,6 +480,17 @@ struct Params {
 struct Ray {
     V3 o, d;
 };
+
+// The tiles of a region's rows (64 pixels each, tile_w_log2 wide): the work units' pixels and the
+// sample scratch's blocks.  Square 8 x 8 tiles for one or two shards; from four row-interleaved
+// shards on, 16 x 4: a shard's 4 consecutive rows lie 4 N image rows apart, so a tile then spans
+// 16 x 16 (N = 4) or 16 x 32 (N = 8) image pixels instead of 8 x 32 or 8 x 64 (coherent rays).
+__host__ __device__ __forceinline__ uint32_t tile_w_log2_for(uint32_t world) { return world >= 4 ? 4u : 3u; }
+__host__ __device__ __forceinline__ uint32_t tiles_x_of(uint32_t width, uint32_t twl) { return (width + (1u << twl) - 1u) >> twl; }
+__host__ __device__ __forceinline__ uint32_t tiles_y_of(uint32_t rows, uint32_t twl) {
+    const uint32_t th = 64u >> twl;
+    return (rows + th - 1u) / th;
+}
 
 struct Counters {
     uint32_t segments, node_visits, prim_tests, hits, texel_fetches, draws;

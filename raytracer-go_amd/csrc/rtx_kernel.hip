@@ -242,8 +242,9 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
     const uint32_t thresh = p.shade_thresh;
     const uint32_t lane = threadIdx.x & 63u;
     const rtx_camera& c = p.cam;
-    const uint32_t tiles_x = (p.width + 7u) / 8u;
-    const uint32_t n_tiles = tiles_x * ((p.rows + 7u) / 8u);
+    const uint32_t twl = p.tile_w_log2, tw_mask = (1u << twl) - 1u, th = 64u >> twl;  // tile: (1 << twl) x th
+    const uint32_t tiles_x = tiles_x_of(p.width, twl);
+    const uint32_t n_tiles = tiles_x * tiles_y_of(p.rows, twl);
     const uint32_t nsub = (p.kn + p.sub - 1u) / p.sub;
     // far pass: units of 64 queue records
     const uint32_t n_rec = TIER == 2 ? min(__builtin_amdgcn_readfirstlane(*(volatile uint32_t*)p.defer_count), p.defer_cap)
@@ -259,8 +260,8 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
     const uint64_t* const redo64 = reinterpret_cast<const uint64_t*>(p.redo_bits);  // redo pass: 64 slots a word
 
     // the wave's unit (uniform, kept in SGPRs: every value below is derived from readfirstlane):
-    // tile origin (u_x8, u_r8), first sample, items, next item
-    uint32_t u_x8 = 0, u_r8 = 0, u_k0 = 0, u_items = 0, cursor = 0;
+    // tile (index, origin u_x, u_r), first sample, items, next item
+    uint32_t u_tile = 0, u_x = 0, u_r = 0, u_k0 = 0, u_items = 0, cursor = 0;
     bool exhausted = false;
 
     uint32_t mode = M_CLAIM, seg = 0, items_done = 0;
@@ -402,9 +403,9 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
                     u_items = min(64u, (TIER == 2 ? n_rec : n_ids) - u_k0);
                     cursor = 0;
                 } else if (!exhausted) {
-                    const uint32_t u_tile = uu / nsub;
-                    u_x8 = (u_tile % tiles_x) * 8u;
-                    u_r8 = (u_tile / tiles_x) * 8u;
+                    u_tile = uu / nsub;
+                    u_x = (u_tile % tiles_x) << twl;
+                    u_r = (u_tile / tiles_x) * th;
                     u_k0 = p.k0 + (uu - u_tile * nsub) * p.sub;
                     const uint32_t cnt_k = min(p.sub, p.k0 + p.kn - u_k0);
                     u_items = 64u * cnt_k;
@@ -435,9 +436,9 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
                 ready = true;
             } else if (TIER != 2 && mode == M_CLAIM && rank < u_items - cursor) {
                 uint32_t j = cursor + rank, l = j & 63u;  // sample-major within the unit
-                uint32_t lx = u_x8 + (l & 7u);
-                uint32_t lr = u_r8 + (l >> 3);
-                size_t slot = (size_t)((u_r8 >> 3) * tiles_x + (u_x8 >> 3)) * 64 + l;
+                uint32_t lx = u_x + (l & tw_mask);
+                uint32_t lr = u_r + (l >> twl);
+                size_t slot = (size_t)u_tile * 64 + l;
                 uint32_t k = u_k0 + (j >> 6);
                 if (TIER == 3 && listed) {  // a listed sample: its bit index in the chunk
                     const uint32_t id = p.redo_ids[u_k0 + j];
@@ -446,8 +447,8 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
                     slot = id - (k - p.k0) * per_k;
                     l = (uint32_t)slot & 63u;
                     const uint32_t tile = (uint32_t)(slot >> 6);
-                    lx = (tile % tiles_x) * 8u + (l & 7u);
-                    lr = (tile / tiles_x) * 8u + (l >> 3);
+                    lx = ((tile % tiles_x) << twl) + (l & tw_mask);
+                    lr = (tile / tiles_x) * th + (l >> twl);
                 }
                 // else: outside a ragged tile (or, redo pass, not flagged), claim again
                 if (lx < p.width && lr < p.rows &&
@@ -521,12 +522,13 @@ __global__ __launch_bounds__(256) void spill_redo_list(Params p) {
 // (pixel-major rows of 96 B wrote 1.26x the colour bytes to HBM as partial lines).  Thread i
 // sums pixel i % 64 of tile i / 64: consecutive threads read consecutive colours.
 __global__ __launch_bounds__(256) void reduce_samples(Params p, uint32_t last) {
-    const uint32_t tiles_x = (p.width + 7u) / 8u;
-    const size_t n_tiles = (size_t)tiles_x * ((p.rows + 7u) / 8u);
+    const uint32_t twl = p.tile_w_log2;
+    const uint32_t tiles_x = tiles_x_of(p.width, twl);
+    const size_t n_tiles = (size_t)tiles_x * tiles_y_of(p.rows, twl);
     const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= n_tiles * 64) return;
     const uint32_t t = (uint32_t)(i >> 6), l = (uint32_t)(i & 63u);
-    const uint32_t lx = (t % tiles_x) * 8u + (l & 7u), lr = (t / tiles_x) * 8u + (l >> 3);
+    const uint32_t lx = ((t % tiles_x) << twl) + (l & ((1u << twl) - 1u)), lr = (t / tiles_x) * (64u >> twl) + (l >> twl);
     if (lx >= p.width || lr >= p.rows) return;  // outside a ragged tile
     float* o = p.out + ((size_t)lr * p.width + lx) * 3;
     float sx = 0.0f, sy = 0.0f, sz = 0.0f;
@@ -594,7 +596,7 @@ hipError_t launch_items(Params p, bool use_lds, hipStream_t stream) {
     hipError_t e = resident_grid((const void*)kern, block, shmem, &per_cu, &cus);
     if (e != hipSuccess) return e;
     const uint32_t spp = p.cam.samples_per_pixel, chunk = p.kn, sub = p.sub;
-    const uint64_t tiles = (uint64_t)((p.width + 7) / 8) * ((p.rows + 7) / 8);
+    const uint64_t tiles = (uint64_t)tiles_x_of(p.width, p.tile_w_log2) * tiles_y_of(p.rows, p.tile_w_log2);
     const uint64_t slots = tiles * 64;  // pixels of the tile-major scratch (ragged tiles padded)
     for (uint32_t k0 = 0; k0 < spp; k0 += chunk) {
         p.k0 = k0;
@@ -641,7 +643,7 @@ hipError_t launch_tiered(Params pn, Params pf, hipStream_t stream) {
     if (e == hipSuccess) e = resident_grid((const void*)kr, block, sf, &per_r, &cus);
     if (e != hipSuccess) return e;
     const uint32_t spp = pn.cam.samples_per_pixel, chunk = pn.kn, sub = pn.sub;
-    const uint64_t tiles = (uint64_t)((pn.width + 7) / 8) * ((pn.rows + 7) / 8);
+    const uint64_t tiles = (uint64_t)tiles_x_of(pn.width, pn.tile_w_log2) * tiles_y_of(pn.rows, pn.tile_w_log2);
     const uint64_t slots = tiles * 64;
     Params pr = pf;  // the redo pass: the far layout over the chunk's units, flagged samples only
     pr.tier = 0;

@@ -483,3 +483,15 @@ def test_tier_deferred_paths_c2_crop(torch_cuda, spheres, dev_spheres):
     _, st, _ = check_scene(torch_cuda, dev_spheres, spheres.desc, cam, 5, reg)
     assert st.walk_layout & rtx.RTX_LAYOUT_TIERED
     assert 0 < st.deferred_paths < 0.2 * st.samples, (st.deferred_paths, st.samples)
+
+
+@pytest.mark.parametrize("tile_w", ["16", "32"])
+def test_tile_shapes(torch_cuda, spheres, dev_spheres, monkeypatch, tile_w):
+    """Tiles of 64 pixels 16 x 4 (the default from four row-interleaved shards on) and 32 x 2
+    (RTX_TILE_W), on a ragged window, whole and as 4 shards: both kernels bit-identical to the oracle."""
+    monkeypatch.setenv("RTX_TILE_W", tile_w)
+    cam = spheres.camera(width=160, spp=4, depth=50)
+    check_scene(torch_cuda, dev_spheres, spheres.desc, cam, 31, rtx.Region(3, 5, 101, 61, 0, 1))
+    for rank in range(4):
+        check_scene(torch_cuda, dev_spheres, spheres.desc, cam, 31, rtx.Region(3, 5, 101, 61, rank, 4),
+                    kernels=("timed",))
