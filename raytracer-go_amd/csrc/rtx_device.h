@@ -482,10 +482,14 @@ struct Ray {
 };
 
 // The tiles of a region's rows (64 pixels each, tile_w_log2 wide): the work units' pixels and the
-// sample scratch's blocks.  Square 8 x 8 tiles for one or two shards; from four row-interleaved
-// shards on, 16 x 4: a shard's 4 consecutive rows lie 4 N image rows apart, so a tile then spans
-// 16 x 16 (N = 4) or 16 x 32 (N = 8) image pixels instead of 8 x 32 or 8 x 64 (coherent rays).
-__host__ __device__ __forceinline__ uint32_t tile_w_log2_for(uint32_t world) { return world >= 4 ? 4u : 3u; }
+// sample scratch's blocks.  Square 8 x 8 tiles for one or two shards; a shard of N row-interleaved
+// ones has its consecutive rows N image rows apart, so wider tiles keep a tile's rays coherent:
+// 16 x 4 for N = 4 (16 x 16 image pixels instead of 8 x 32), 32 x 2 from N = 8 on (32 x 16 instead of
+// 8 x 64).  Rank 0's rows alone (profiles/r04_tile_ab.jsonl): N = 4 25.66 / 25.66 ms (16 / 32 wide)
+// against 25.94 (8); N = 8 13.45 / 13.39 against 13.74.
+__host__ __device__ __forceinline__ uint32_t tile_w_log2_for(uint32_t world) {
+    return world >= 8 ? 5u : (world >= 4 ? 4u : 3u);
+}
 __host__ __device__ __forceinline__ uint32_t tiles_x_of(uint32_t width, uint32_t twl) { return (width + (1u << twl) - 1u) >> twl; }
 __host__ __device__ __forceinline__ uint32_t tiles_y_of(uint32_t rows, uint32_t twl) {
     const uint32_t th = 64u >> twl;
