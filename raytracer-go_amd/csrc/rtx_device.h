@@ -405,14 +405,23 @@ __device__ __forceinline__ SceneRef scene_ref_fixed(const float4* lds, uint32_t 
                     reinterpret_cast<const rtx_material*>(lds + mo),
                     reinterpret_cast<const rtx_texture*>(lds + mo + 2 * n_mats), nullptr, nullptr, 0u, 0u};
 }
-// The LDS cache of a scene too big for the fixed layout: its first entries (whole top
-// levels, rtx_capi.hip ensure_device) in the fixed layout's places.  Up to HOT_ENTRIES_8W
-// (52 KB) three 8-wave workgroups share a CU; up to HOT_ENTRIES_MAX (64 KB: the fixed layout's
-// two 32 KB halves, reached by the ds_read offset field) two 12-wave ones do — 6 waves per
-// SIMD either way.
-constexpr uint32_t HOT_ENTRIES_8W = 1280;
-constexpr uint32_t HOT_ENTRIES_MAX = 2048;
-__host__ __device__ __forceinline__ uint32_t lds_hot_bytes(uint32_t n_hot) { return LDS_B + n_hot * 16; }
+// The LDS cache of a scene too big for the fixed layout: its first entries (the ones the walk
+// reads most, rtx_capi.hip ensure_device), 'a' halves from LDS byte 0 and 'b' halves from
+// HOT_B (reached by the ds_read offset field, as in the fixed layout).  Up to HOT_ENTRIES_8W
+// three 8-wave workgroups share a CU; up to HOT_ENTRIES_MAX (80 KB: half of the CU's 160 KB)
+// two 12-wave ones do — 6 waves per SIMD either way.  (2560 entries against 2048)
+#ifndef RTX_HOT_B
+#define RTX_HOT_B 40960
+#endif
+#ifndef RTX_HOT_MAX
+#define RTX_HOT_MAX 2560
+#endif
+constexpr uint32_t HOT_B = RTX_HOT_B;
+constexpr uint32_t HOT_ENTRIES_MAX = RTX_HOT_MAX;
+constexpr uint32_t HOT_ENTRIES_8W = (160u * 1024u / 3u - HOT_B) / 16u / 64u * 64u;
+static_assert(HOT_ENTRIES_MAX * 16 <= HOT_B && 2 * (HOT_B + HOT_ENTRIES_MAX * 16) <= 160u * 1024u,
+              "two 12-wave workgroups' caches per CU");
+__host__ __device__ __forceinline__ uint32_t lds_hot_bytes(uint32_t n_hot) { return HOT_B + n_hot * 16; }
 // float4s of a scene's device table: both halves with their sentinels, then the quads.
 __host__ __device__ __forceinline__ uint32_t scene_float4s(uint32_t n_entries, uint32_t n_quads) {
     return 2 * (n_entries + 1) + 4 * n_quads;
@@ -741,7 +750,7 @@ __device__ __forceinline__ void load_entry(const SceneRef E, uint32_t pos, float
                      "s_mov_b64 exec, %[sv]\n\t"
                      "s_waitcnt vmcnt(0) lgkmcnt(0)"
                      : [ea] "=&v"(ea), [eb] "=&v"(eb), [sv] "=&s"(sv), [m] "=&s"(m)
-                     : [pos] "v"(pos), [hot] "s"(E.hot), [ba] "s"(E.a), [bb] "s"(E.b), [lb] "i"(LDS_B)
+                     : [pos] "v"(pos), [hot] "s"(E.hot), [ba] "s"(E.a), [bb] "s"(E.b), [lb] "i"(HOT_B)
                      : "scc");
     } else if constexpr (FIXED) {
         asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %2 offset:%3\n\ts_waitcnt lgkmcnt(0)"

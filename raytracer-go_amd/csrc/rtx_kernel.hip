@@ -230,11 +230,11 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
             const uint32_t m = p.n_entries + 1;
             for (uint32_t t = threadIdx.x; t < p.n_hot; t += WAVE_BLOCK) {
                 lds_entries[t] = p.entries[t];
-                lds_entries[LDS_B / 16 + t] = p.entries[m + t];
+                lds_entries[HOT_B / 16 + t] = p.entries[m + t];
             }
             __syncthreads();
             E.la = lds_entries;
-            E.lb = lds_entries + LDS_B / 16;
+            E.lb = lds_entries + HOT_B / 16;
             E.hot = 16 * p.n_hot;
         }
     }
@@ -678,7 +678,7 @@ hipError_t launch_tiered(Params pn, Params pf, hipStream_t stream) {
     return hipSuccess;
 }
 
-#ifndef RTX_HYB_WAVES  // the same for scenes in HBM with a 64 KB LDS cache of their top levels
+#ifndef RTX_HYB_WAVES  // the same for scenes in HBM with an 80 KB LDS cache of their most-read entries
 #define RTX_HYB_WAVES 12
 #define RTX_HYB_MINW 6
 #endif
@@ -695,7 +695,7 @@ hipError_t launch_items_for(const Params& p, bool use_lds, hipStream_t stream) {
         return p.n_quads ? launch_items<COUNT, true, false, 4>(p, use_lds, stream)
                          : launch_items<COUNT, false, false, 4>(p, use_lds, stream);
     // 6 waves per SIMD: at most 80 VGPRs (the allocation granule is 8)
-    if (!use_lds && p.n_hot > HOT_ENTRIES_8W)  // a 64 KB LDS cache: 12-wave workgroups, two per CU
+    if (!use_lds && p.n_hot > HOT_ENTRIES_8W)  // an LDS cache past a third of the CU: 12-wave workgroups, two per CU
         return p.n_quads ? launch_items<COUNT, true, false, RTX_HYB_WAVES, COUNT ? 0 : RTX_HYB_MINW>(p, use_lds, stream)
                          : launch_items<COUNT, false, false, RTX_HYB_WAVES, COUNT ? 0 : RTX_HYB_MINW>(p, use_lds, stream);
     return p.n_quads ? launch_items<COUNT, true, false, RTX_V3_WAVES, COUNT ? 0 : RTX_V3_MINW>(p, use_lds, stream)
@@ -730,7 +730,7 @@ hipError_t launch_render(const Params& p, uint32_t flags, hipStream_t stream, co
             return count ? launch_tiered<true, RTX_V3_WAVES, 0>(p, *far, stream)
                          : launch_tiered<false, RTX_V3_WAVES, RTX_V3_MINW>(p, *far, stream);
         }
-        if (place == RTX_SCENE_LDS_CACHE)  // both caches of 64 KB (tier_placement): 12-wave workgroups, two per CU
+        if (place == RTX_SCENE_LDS_CACHE)  // both cached in LDS (tier_placement): 12-wave workgroups, two per CU
             return count ? launch_tiered<true, RTX_HYB_WAVES, 0, false, false, true>(p, *far, stream)
                          : launch_tiered<false, RTX_HYB_WAVES, RTX_HYB_MINW, false, false, true>(p, *far, stream);
         return count ? launch_tiered<true, RTX_V3_WAVES, 0, false, false, false>(p, *far, stream)

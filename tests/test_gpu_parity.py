@@ -218,7 +218,7 @@ def test_full_frame_bitwise(torch_cuda, built, scene, width, spp):
     check_scene(torch_cuda, dev, s.desc, cam, 23, reg)
 
 
-@pytest.mark.parametrize("hot", ["0", "64", "1280", "2048"])
+@pytest.mark.parametrize("hot", ["0", "64", "832", "1280", "2048", "2560"])
 def test_stress_100k_lds_cache(torch_cuda, built, monkeypatch, hot):
     """Config 4 with its top BVH levels stored first and cached in LDS (RTX_HOT_ENTRIES, read at
     upload): none, the first levels (the collapsed walk leaves the top nodes' own tests out, so the
@@ -456,7 +456,7 @@ def test_tier_queue_overflow_redo(torch_cuda, spheres, dev_spheres, monkeypatch,
     counters (samples, segments, hits, texel fetches, draws) equal the oracle's: the near pass's work
     on a flagged sample is taken back and the redo pass counts it.  RTX_REDO_CAP shortens the redo list
     so that the samples past it take the bits' path (spill_redo_list, the redo pass scanning the bits)."""
-    cam = spheres.camera(width=160, spp=12, depth=50)
+    cam = spheres.camera(width=160, spp=24, depth=50)
     reg = rtx.Region(0, 0, cam.image_width, cam.image_height, 0, 1)
     want, st0 = gpu_region(torch_cuda, dev_spheres, cam, 21, reg, counters=True)
     it, cnt = ob.render(spheres.desc, cam, 21, reg, ob.ORDER_ITERATIVE)
