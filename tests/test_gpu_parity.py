@@ -79,6 +79,16 @@ def test_edge_shapes(torch_cuda, spheres, dev_spheres, w, h, spp, depth):
         assert not gpu.any()
 
 
+@pytest.mark.parametrize("world,rank", [(4, 1), (8, 0), (8, 7), (16, 3)])
+def test_ragged_shard_tiles(torch_cuda, spheres, dev_spheres, world, rank):
+    """One rank's rows of a window whose width and row count are not multiples of the shard's tile
+    shape (16 x 4 at N = 4, 32 x 2 from N = 8 on): both kernels bit-identical to the oracle."""
+    cam = spheres.camera(width=160, spp=3)
+    reg = rtx.Region(7, 2, 45, 37, rank, world)
+    assert rtx.region_rows(reg) > 0
+    check_scene(torch_cuda, dev_spheres, spheres.desc, cam, 17, reg)
+
+
 def test_empty_shard(torch_cuda, spheres, dev_spheres):
     cam = spheres.camera(width=64, spp=1)
     reg = rtx.Region(0, 0, 64, 2, 5, 8)  # rank 5 of 8 over 2 rows: no rows
