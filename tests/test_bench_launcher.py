@@ -58,17 +58,18 @@ def _bench_line(args):
 
 
 @pytest.mark.gpu
-def test_rank_processes_render_the_same_image_on_one_gpu():
-    """The real multi-rank path on a one-GPU box: `bench.py --gpus 3 --rehearse-one-gpu` starts three
-    rank processes on cuda:0, each renders its row-interleaved shard with the megakernel, and the
-    shards are gathered (gloo, host copies: RCCL needs a GPU per rank) and de-interleaved on rank 0.
-    The framebuffer hash must equal the one-rank render's bit for bit."""
+@pytest.mark.parametrize("n", [3, 4, 8])
+def test_rank_processes_render_the_same_image_on_one_gpu(n):
+    """The real multi-rank path on a one-GPU box: `bench.py --gpus N --rehearse-one-gpu` starts N rank
+    processes on cuda:0, each renders its row-interleaved shard with the megakernel (8 x 8 tiles at N = 3,
+    16 x 4 at N = 4, 32 x 2 at N = 8), and the shards are gathered (gloo, host copies: RCCL needs a GPU per
+    rank) and de-interleaved on rank 0.  The framebuffer hash must equal the one-rank render's bit for bit."""
     common = ["--width", "192", "--spp", "8", "--steps", "1", "--warmup", "0", "--no-cpu"]
     one = _bench_line(["--gpus", "1"] + common)
-    three = _bench_line(["--gpus", "3", "--rehearse-one-gpu"] + common)
-    assert three["n_gpus"] == 3 and three["config"]["world_size"] == 3 and three["config"]["backend"] == "gloo"
-    assert three["metric"].startswith("rehearsal")
-    assert one["framebuffer_sha256_16"] == three["framebuffer_sha256_16"]
+    many = _bench_line(["--gpus", str(n), "--rehearse-one-gpu"] + common)
+    assert many["n_gpus"] == n and many["config"]["world_size"] == n and many["config"]["backend"] == "gloo"
+    assert many["metric"].startswith("rehearsal")
+    assert one["framebuffer_sha256_16"] == many["framebuffer_sha256_16"]
 
 
 def _bench_line_env(args, extra):
@@ -83,7 +84,8 @@ def _bench_line_env(args, extra):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("env,kind", [({"RTX_SIM_BANDS": "3"}, "device copies"), ({"RTX_FORCE_RCCL": "1"}, "rccl")])
+@pytest.mark.parametrize("env,kind", [({"RTX_SIM_BANDS": "3"}, "device copies"), ({"RTX_SIM_BANDS": "8"}, "device copies"),
+                                      ({"RTX_FORCE_RCCL": "1"}, "rccl")])
 def test_in_process_leg_on_one_gpu(env, kind):
     """`bench.py --in-process`: one process timing rtx_render(n_gpus) — the C-ABI's own N-device path
     (bands, gather to device 0, de-interleave, copy to the host) that rank 0 of an N-GPU run also times
