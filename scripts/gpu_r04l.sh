@@ -11,6 +11,8 @@ for i in 1 2; do
     RTX_ITEM_GRID=$1 RTX_ITEM_SUB=$2 timeout -k 10 120 python bench.py --width 400 --spp 100 --steps 20 --warmup 3 --no-cpu > "$OUT/c1_g$1_s$2_$i.json" 2> "$OUT/c1_g$1_s$2_$i.err" || exit 1
     line "$OUT/c1_g$1_s$2_$i.json" "c1 grid$1 sub$2 $i"
   done
+  RTX_TIER=0 timeout -k 10 120 python bench.py --width 400 --spp 100 --steps 20 --warmup 3 --no-cpu > "$OUT/c1_notier_$i.json" 2> "$OUT/c1_notier_$i.err" || exit 1
+  line "$OUT/c1_notier_$i.json" "c1 notier $i"
   for g in 100 90; do
     RTX_ITEM_GRID=$g timeout -k 10 200 python bench.py --steps 5 --warmup 1 --no-cpu > "$OUT/c2_g${g}_$i.json" 2> "$OUT/c2_g${g}_$i.err" || exit 1
     line "$OUT/c2_g${g}_$i.json" "c2 grid$g $i"
