@@ -39,10 +39,12 @@ def main():
     ap.add_argument("configs", nargs="+", choices=list(CONFIGS))
     ap.add_argument("--out", required=True)
     ap.add_argument("--stride", action="append", default=[], help="NAME=S: every S-th row (default 1)")
+    ap.add_argument("--offset", action="append", default=[], help="NAME=O: the first row compared (default 7 %% S)")
     ap.add_argument("--band", type=int, default=64, help="rows per oracle call (a progress line each)")
     ap.add_argument("--threads", type=int, default=16)
     args = ap.parse_args()
     strides = {k: int(v) for k, v in (s.split("=") for s in args.stride)}
+    offsets = {k: int(v) for k, v in (s.split("=") for s in args.offset)}
 
     import torch
 
@@ -59,7 +61,7 @@ def main():
         t0 = time.time()
         gpu, st = gpu_region(torch, dev, cam, 2024, rtx.Region(0, 0, W, H, 0, 1), counters=False)
         gpu_s = time.time() - t0
-        off = 7 % stride
+        off = offsets.get(name, 7) % stride
         rows = np.arange(off, H, stride)
         want = gpu[rows]
         it = np.empty_like(want)
@@ -88,7 +90,7 @@ def main():
                                   tier=tw, rank=rank)
                 walked_equal += int(np.array_equal(px[0, 0], want[i, x]))
         line = {
-            "config": name, "scene": scene, "width": W, "height": H, "spp": spp, "row_stride": stride,
+            "config": name, "scene": scene, "width": W, "height": H, "spp": spp, "row_stride": stride, "first_row": off,
             "pixels_compared": int(want.shape[0] * W), "pixels_total": int(W * H),
             "iterative_order_mismatches": int(len(bad)),
             "mismatches_equal_to_walked_tree_oracle": walked_equal,
