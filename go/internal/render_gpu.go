@@ -35,7 +35,6 @@ import (
 	"os"
 	"runtime"
 	"strconv"
-	"strings"
 	"sync"
 	"sync/atomic"
 	"unsafe"
@@ -471,35 +470,26 @@ func (c *Camera) renderOnDevices(world Hittable, writer io.Writer, seed uint64, 
 		defocus_disk_u: vec(c.defocusDiskU), defocus_disk_v: vec(c.defocusDiskV),
 		background: vec(c.background.GetColor()),
 	}
-	if gpus <= 1 { // render + the P3 text (header included) on the device: rtx_render_ppm
-		text := make([]byte, int(C.rtx_ppm_max_bytes(C.uint32_t(w), C.uint32_t(h))))
-		var n C.uint64_t
-		if rc := C.rtx_render_ppm(scene, &cam, C.uint64_t(seed), (*C.char)(unsafe.Pointer(&text[0])),
-			C.uint64_t(len(text)), &n, nil); rc != 0 {
-			if gpuMissing(rc) {
-				return errFallback
-			}
-			return rtxErr(rc)
-		}
-		_, err := writer.Write(text[:int(n)])
-		return err
+	// Render + the P3 text (header included) on the device: rtx_render_ppm on the current device for one
+	// GPU; for several, rtx_render_ppm_ex (ABI 9) gathers the row-interleaved bands to device 0 over RCCL
+	// and encodes them there, so no per-pixel formatting runs on the host at any device count
+	// (camera.go:183-188, 212-215 and vec3.go:141-166 on the GPU, byte-identical).
+	text := make([]byte, int(C.rtx_ppm_max_bytes(C.uint32_t(w), C.uint32_t(h))))
+	var n C.uint64_t
+	var rc C.int
+	if gpus <= 1 {
+		rc = C.rtx_render_ppm(scene, &cam, C.uint64_t(seed), (*C.char)(unsafe.Pointer(&text[0])),
+			C.uint64_t(len(text)), &n, nil)
+	} else {
+		rc = C.rtx_render_ppm_ex(scene, &cam, C.uint64_t(seed), C.int(gpus), (*C.char)(unsafe.Pointer(&text[0])),
+			C.uint64_t(len(text)), &n, nil)
 	}
-	rgb := make([]float32, w*h*3) // several GPUs: float32 image gathered to device 0, text here
-	if rc := C.rtx_render(scene, &cam, C.uint64_t(seed), C.int(gpus), (*C.float)(unsafe.Pointer(&rgb[0])), nil); rc != 0 {
+	if rc != 0 {
 		if gpuMissing(rc) {
 			return errFallback
 		}
 		return rtxErr(rc)
 	}
-	var sb strings.Builder
-	sb.WriteString("P3\n" + strconv.Itoa(w) + " " + strconv.Itoa(h) + "\n255\n") // camera.go:183-188
-	for p := 0; p < w*h; p++ {                                                   // camera.go:212-215
-		col := NewVec3(rgb[3*p], rgb[3*p+1], rgb[3*p+2])
-		col.ToGamma2()
-		col.ToRGB()
-		sb.WriteString(col.String())
-		sb.WriteByte('\n')
-	}
-	_, err = io.WriteString(writer, sb.String())
+	_, err = writer.Write(text[:int(n)])
 	return err
 }

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define RTX_ABI_VERSION 8
+#define RTX_ABI_VERSION 9
 
 /* ---- status codes ------------------------------------------------------------ */
 enum {
@@ -458,6 +458,16 @@ int rtx_encode_ppm_device(const float* d_rgb, uint32_t width, uint32_t height, c
  * buffer: the bytes (*Camera).Render(world, writer) writes (camera.go:180).  Blocking. */
 int rtx_render_ppm(rtx_scene* scene, const rtx_camera* cam, uint64_t seed, char* out_text, uint64_t capacity,
                    uint64_t* out_len, rtx_stats* stats);
+
+/* ABI 9.  rtx_render_ppm for n_gpus devices: the bands rendered and gathered to device 0 exactly
+ * as rtx_render(n_gpus) does (one RCCL ncclGather over xGMI and the de-interleave kernel, or the
+ * per-band copies without RCCL), then the PPM encoded ON device 0 (rtx_encode_ppm_device) and only
+ * the text copied to the caller: the multi-GPU (*Camera).Render(world, writer) of camera.go:180-231
+ * with no per-pixel formatting on the host.  Devices 0..n_gpus-1 (n_gpus <= 1: device 0, one band;
+ * RTX_SIM_BANDS=k simulates k bands on device 0 as rtx_render does).  The bytes equal
+ * rtx_render_ppm's for any n_gpus.  stats as rtx_render's.  Blocking. */
+int rtx_render_ppm_ex(rtx_scene* scene, const rtx_camera* cam, uint64_t seed, int n_gpus, char* out_text,
+                      uint64_t capacity, uint64_t* out_len, rtx_stats* stats);
 
 #ifdef __cplusplus
 }

@@ -85,6 +85,7 @@ struct Scratch {
     size_t defer_bytes = 0;
     uint32_t* redo = nullptr;  // the tiered walk's redo bits: one per sample of a chunk
     size_t redo_bytes = 0;
+    size_t redo_zero = 0;      // bytes at the start of `redo` known to be zero (clear_redo_bits keeps them so)
     hipEvent_t last = nullptr;
     int scenes = 0;
 };
@@ -932,6 +933,9 @@ int enqueue_on(rtx_scene* s, DeviceCopy* c, const rtx_camera* cam, uint64_t seed
         const uint64_t budget = (uint64_t)env_knob("RTX_SCRATCH_MB", 16384, 1, 1 << 20) << 20;
         uint64_t chunk = budget / per_sample;
         if (chunk > cam->samples_per_pixel) chunk = cam->samples_per_pixel;
+        // the tiered walk names a chunk's samples by 32-bit ids ((k - k0) * tiles * 64 + slot: the redo
+        // list, the redo bits' index): at most 2^32 scratch slots per chunk
+        if (tier) chunk = std::min<uint64_t>(chunk, 0xFFFFFFFFull / (per_sample / 12));
         if (chunk < 1) return fail(RTX_ERR_OOM, "RTX_SCRATCH_MB too small for one sample of the region");
         const size_t need = (size_t)(chunk * per_sample);
         if (scr->bytes < need) {
@@ -946,6 +950,9 @@ int enqueue_on(rtx_scene* s, DeviceCopy* c, const rtx_camera* cam, uint64_t seed
         p.kn = (uint32_t)chunk;
         *chunks = (uint32_t)((cam->samples_per_pixel + chunk - 1) / chunk);
         p.sub = env_knob("RTX_ITEM_SUB", 0, 0, 4096);  // 0: chosen per chunk by launch_items
+        // the redo pass skips a unit by one vote over its samples' bit words, one sample per lane
+        if (tier && p.sub > 64) p.sub = 64;
+        p.debug_partial = env_knob("RTX_DEBUG_PARTIAL_SITE", 0, 0, 3);  // (read by librtx_dbgclaim.so only)
         p.item_waves = env_knob("RTX_ITEM_WAVES", 8, 4, 8) >= 8 ? 8u : 4u;
         p.grid_pct = env_knob("RTX_ITEM_GRID", 100, 1, 100);
         p.debug_launch = env_knob("RTX_DEBUG_LAUNCH", 0, 0, 1);
@@ -980,9 +987,14 @@ int enqueue_on(rtx_scene* s, DeviceCopy* c, const rtx_camera* cam, uint64_t seed
                 if (scr->redo) HIP_TRY(hipFree(scr->redo));
                 scr->redo = nullptr;
                 scr->redo_bytes = 0;
+                scr->redo_zero = 0;
                 HIP_TRY(hipMalloc(&scr->redo, 2 * bits));
                 scr->redo_bytes = 2 * bits;
             }
+            // The bits [0, bits) must be zero at the first chunk's start; clear_redo_bits keeps them so after
+            // every chunk.  Past them this render's redo list may leave ids, so only [0, bits) stays known zero.
+            if (scr->redo_zero < bits) HIP_TRY(hipMemsetAsync(scr->redo, 0, bits, stream));
+            scr->redo_zero = bits;
             rtxd::Params lay = pn;  // the near pass: every setting of p, the near walk's layout
             pn = p;
             pn.entries = lay.entries;
@@ -1015,7 +1027,10 @@ int enqueue_on(rtx_scene* s, DeviceCopy* c, const rtx_camera* cam, uint64_t seed
     // every stats slot, the unit queue head and the watchdog flag start at 0 for every render
     HIP_TRY(hipMemsetAsync(c->counters, 0, rtxd::COUNTER_SLOTS * sizeof(unsigned long long), stream));
     if (timed) HIP_TRY(hipEventRecord(c->ev0, stream));
-    HIP_TRY(*tiered ? rtxd::launch_render(pn, flags, stream, &p) : rtxd::launch_render(p, flags, stream));
+    if (const hipError_t e = *tiered ? rtxd::launch_render(pn, flags, stream, &p) : rtxd::launch_render(p, flags, stream)) {
+        scr->redo_zero = 0;  // a chunk may have stopped between setting redo bits and clearing them
+        return fail(e == hipErrorOutOfMemory ? RTX_ERR_OOM : RTX_ERR_HIP, "render launch failed: %s", hipGetErrorString(e));
+    }
     if (timed) HIP_TRY(hipEventRecord(c->ev1, stream));
     HIP_TRY(hipEventRecord(scr->last, stream));
     return RTX_OK;
@@ -1028,7 +1043,11 @@ int collect_on(DeviceCopy* c, bool count, uint64_t samples, uint32_t chunks, rtx
     HIP_TRY(hipEventElapsedTime(&ms, c->ev0, c->ev1));
     unsigned long long h[rtxd::COUNTER_SLOTS] = {0};
     HIP_TRY(hipMemcpy(h, c->counters, rtxd::COUNTER_SLOTS * sizeof(unsigned long long), hipMemcpyDeviceToHost));
-    if ((h[7] >> 32) != 0) return fail(RTX_ERR_HIP, "render kernel watchdog fired (RTX_WATCHDOG_S): output incomplete");
+    const uint64_t kerr = h[7] >> 32;  // rtxd::KERR_* bits
+    if (kerr & rtxd::KERR_PARTIAL_WAVE)
+        return fail(RTX_ERR_HIP, "render kernel: a wave-level claim was reached without the whole wave (partial EXEC): "
+                                 "output invalid");
+    if (kerr != 0) return fail(RTX_ERR_HIP, "render kernel watchdog fired (RTX_WATCHDOG_S): output incomplete");
     std::memset(st, 0, sizeof(*st));
     st->samples = count ? h[0] : samples;
     st->segments = h[1];
@@ -1166,9 +1185,9 @@ int rtx_version(void) { return RTX_ABI_VERSION; }
 // (No build date: the library's bytes depend on its sources only, so the PMC profiles bench.py ties to the
 // library's hash stay valid across rebuilds of the same sources.)
 const char* rtx_build_info(void) {
-    return "librtx gfx950 megakernel (ABI 8: persistent (pixel, sample) item waves, LDS scene, threaded pre-order BVH "
+    return "librtx gfx950 megakernel (ABI 9: persistent (pixel, sample) item waves, LDS scene, threaded pre-order BVH "
            "(binned-SAH walk trees per camera octant: tiered near / guarded, or the caller's), collapsed walk, "
-           "RGBA16 image texels, RCCL band gather)";
+           "RGBA16 image texels, RCCL band gather, PPM on device 0 for any band count)";
 }
 
 const char* rtx_last_error(void) { return g_last_error.c_str(); }
@@ -1436,6 +1455,11 @@ int rtx_render(rtx_scene* s, const rtx_camera* cam, uint64_t seed, int n_gpus, f
     return rtx_render_ex(s, cam, seed, n_gpus, 0u, out_rgb, stats);
 }
 
+namespace {
+int render_bands_locked(rtx_scene* s, const rtx_camera* cam, uint64_t seed, int n_gpus, uint32_t flags, float* out_rgb,
+                        float** dev_img, hipStream_t* dev_stream, rtx_stats* stats);
+}  // namespace
+
 int rtx_render_ex(rtx_scene* s, const rtx_camera* cam, uint64_t seed, int n_gpus, uint32_t flags, float* out_rgb,
                   rtx_stats* stats) {
     g_last_error.clear();
@@ -1445,6 +1469,18 @@ int rtx_render_ex(rtx_scene* s, const rtx_camera* cam, uint64_t seed, int n_gpus
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(RTX_ERR_NO_DEVICE, "no HIP device");
     if (n_gpus <= 0) n_gpus = 1;
     if (n_gpus > ndev) return fail(RTX_ERR_INVALID_ARG, "n_gpus=%d but %d devices visible", n_gpus, ndev);
+    std::lock_guard<std::mutex> lk(s->mu);
+    std::lock_guard<std::mutex> bl(g_render_mu);  // the cached band / gather / image buffers
+    return render_bands_locked(s, cam, seed, n_gpus, flags, out_rgb, nullptr, nullptr, stats);
+}
+
+namespace {
+// rtx_render_ex's bands (rows y % n == d on device d) and their assembly, with s->mu and g_render_mu
+// held by the caller.  out_rgb: the caller's host buffer.  Or out_rgb == nullptr: the assembled image
+// stays on device 0 in *dev_img (a cached render buffer, valid until the next render under
+// g_render_mu), written by *dev_stream (rtx_render_ppm_ex encodes it there).
+int render_bands_locked(rtx_scene* s, const rtx_camera* cam, uint64_t seed, int n_gpus, uint32_t flags, float* out_rgb,
+                        float** dev_img, hipStream_t* dev_stream, rtx_stats* stats) {
     // RTX_SIM_BANDS=k (tests, one device): k bands, all on device 0, gathered by device copies
     const uint32_t sim = n_gpus == 1 ? env_knob("RTX_SIM_BANDS", 1, 1, 64) : 1u;
     int n = sim > 1 ? (int)sim : n_gpus;
@@ -1455,8 +1491,6 @@ int rtx_render_ex(rtx_scene* s, const rtx_camera* cam, uint64_t seed, int n_gpus
     const bool want_rccl = sim == 1 && (n > 1 || env_knob("RTX_FORCE_RCCL", 0, 0, 1) == 1);
     const bool no_rccl = env_knob("RTX_NO_RCCL", 0, 0, 1) == 1;
     const uint32_t kflags = flags & RTX_FLAG_COUNTERS;
-    std::lock_guard<std::mutex> lk(s->mu);
-    std::lock_guard<std::mutex> bl(g_render_mu);  // the cached band / gather / image buffers
     int cur = 0;
     HIP_TRY(hipGetDevice(&cur));
     const uint32_t W = cam->image_width, H = cam->image_height;
@@ -1563,17 +1597,21 @@ int rtx_render_ex(rtx_scene* s, const rtx_camera* cam, uint64_t seed, int n_gpus
                            gathered, img, (uint32_t)n, R, H, W * 3);
         hipError_t e = hipGetLastError();
         if (e == hipSuccess) e = hipEventRecord(g1, streams[0]);
-        if (e == hipSuccess) e = copy_to_host(out_rgb, img, total_floats * sizeof(float), streams[0]);
+        if (e == hipSuccess && out_rgb) e = copy_to_host(out_rgb, img, total_floats * sizeof(float), streams[0]);
         for (int d = 1; d < n && e == hipSuccess; ++d)
             if ((e = hipSetDevice(dev_of(d))) == hipSuccess) e = hipStreamSynchronize(streams[d]);
         if (e != hipSuccess) rc = fail(RTX_ERR_HIP, "band assembly: %s", hipGetErrorString(e));
+        if (rc == RTX_OK && !out_rgb) *dev_img = img;
     } else if (rc == RTX_OK && kind == RTX_GATHER_HOST) {
-        // band d holds image rows y = d + r n: one strided copy per band into the caller's rows
+        // band d holds image rows y = d + r n: one strided copy per band into the caller's rows (for a
+        // device image, rows of a host image that then goes to device 0 in one copy: RCCL's fallback only)
+        std::vector<float> host_img(out_rgb ? 0 : (size_t)H * W * 3);
+        float* dst = out_rgb ? out_rgb : host_img.data();
         for (int d = 0; d < n && rc == RTX_OK; ++d) {
             const uint32_t rows = region_rows(&regs[d]);
             if (!rows) continue;
             if (hipSetDevice(dev_of(d)) != hipSuccess ||
-                hipMemcpy2DAsync(out_rgb + (size_t)d * W * 3, (size_t)n * W * 3 * sizeof(float), bufs[d],
+                hipMemcpy2DAsync(dst + (size_t)d * W * 3, (size_t)n * W * 3 * sizeof(float), bufs[d],
                                  (size_t)W * 3 * sizeof(float), (size_t)W * 3 * sizeof(float), rows,
                                  hipMemcpyDeviceToHost, streams[d]) != hipSuccess)
                 rc = fail(RTX_ERR_HIP, "band %d copy to the host", d);
@@ -1581,14 +1619,26 @@ int rtx_render_ex(rtx_scene* s, const rtx_camera* cam, uint64_t seed, int n_gpus
         for (int d = 0; d < n; ++d)
             if (hipSetDevice(dev_of(d)) == hipSuccess && hipStreamSynchronize(streams[d]) != hipSuccess && rc == RTX_OK)
                 rc = fail(RTX_ERR_HIP, "band %d copy to the host", d);
+        if (rc == RTX_OK && !out_rgb) {
+            (void)hipSetDevice(0);
+            if (!(img = static_cast<float*>(render_buffer(0, -2, img_bytes)))) rc = fail(RTX_ERR_OOM, "device-0 image");
+            else if (hipMemcpyAsync(img, dst, img_bytes, hipMemcpyHostToDevice, streams[0]) != hipSuccess)
+                rc = fail(RTX_ERR_HIP, "image copy to device 0");
+            else *dev_img = img;
+        }
         if (rc == RTX_OK && (hipSetDevice(0) != hipSuccess || hipEventRecord(g1, streams[0]) != hipSuccess ||
                              hipEventSynchronize(g1) != hipSuccess))
             rc = fail(RTX_ERR_HIP, "gather event");
     } else if (rc == RTX_OK) {  // one device, no gather: the band is the image
         (void)hipSetDevice(0);
-        hipError_t e = copy_to_host(out_rgb, bufs[0], img_bytes, streams[0]);
-        if (e != hipSuccess) rc = fail(RTX_ERR_HIP, "copy image: %s", hipGetErrorString(e));
+        if (out_rgb) {
+            hipError_t e = copy_to_host(out_rgb, bufs[0], img_bytes, streams[0]);
+            if (e != hipSuccess) rc = fail(RTX_ERR_HIP, "copy image: %s", hipGetErrorString(e));
+        } else {
+            *dev_img = bufs[0];
+        }
     }
+    if (rc == RTX_OK && dev_stream) *dev_stream = streams[0];
     if (rc == RTX_OK && kind != RTX_GATHER_NONE) {
         float ms = 0.0f;
         if (hipSetDevice(0) == hipSuccess && hipEventElapsedTime(&ms, g0, g1) == hipSuccess) total.gather_ms = ms;
@@ -1601,6 +1651,7 @@ int rtx_render_ex(rtx_scene* s, const rtx_camera* cam, uint64_t seed, int n_gpus
     if (rc == RTX_OK && stats) *stats = total;
     return rc;
 }
+}  // namespace
 
 int rtx_release_device_memory(int device) {
     g_last_error.clear();
@@ -1714,6 +1765,41 @@ int rtx_render_ppm(rtx_scene* s, const rtx_camera* cam, uint64_t seed, char* out
     if (rc == RTX_OK && copy_to_host(out_text, text, len, st) != hipSuccess)
         rc = fail(RTX_ERR_HIP, "copying the PPM text to the host");
     (void)hipStreamSynchronize(st);
+    if (rc == RTX_OK) *out_len = len;
+    return rc;
+}
+
+int rtx_render_ppm_ex(rtx_scene* s, const rtx_camera* cam, uint64_t seed, int n_gpus, char* out_text, uint64_t capacity,
+                      uint64_t* out_len, rtx_stats* stats) {
+    g_last_error.clear();
+    if (!s || !out_text || !out_len) return fail(RTX_ERR_INVALID_ARG, "NULL argument");
+    if (int rc = check_camera(cam)) return rc;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(RTX_ERR_NO_DEVICE, "no HIP device");
+    if (n_gpus <= 0) n_gpus = 1;
+    if (n_gpus > ndev) return fail(RTX_ERR_INVALID_ARG, "n_gpus=%d but %d devices visible", n_gpus, ndev);
+    const uint32_t W = cam->image_width, H = cam->image_height;
+    const uint64_t need = rtxd::ppm_max_bytes(W, H);
+    int cur = 0;
+    HIP_TRY(hipGetDevice(&cur));
+    std::lock_guard<std::mutex> lk(s->mu);  // (lock order: the scene, then the render buffers)
+    std::lock_guard<std::mutex> bl(g_render_mu);
+    float* img = nullptr;
+    hipStream_t st = nullptr;
+    rtx_stats local;
+    // the bands rendered and assembled on device 0 as rtx_render_ex does, the image left there
+    int rc = render_bands_locked(s, cam, seed, n_gpus, 0u, nullptr, &img, &st, stats ? stats : &local);
+    if (rc == RTX_OK && hipSetDevice(0) != hipSuccess) rc = fail(RTX_ERR_HIP, "hipSetDevice(0)");
+    char* text = rc == RTX_OK ? static_cast<char*>(render_buffer(0, -4, need)) : nullptr;
+    if (rc == RTX_OK && !text) rc = fail(RTX_ERR_OOM, "device-0 buffer for a %ux%u PPM", W, H);
+    uint64_t len = 0;
+    if (rc == RTX_OK) rc = rtx_encode_ppm_device(img, W, H, text, need, &len, st);
+    if (rc == RTX_OK && len > capacity) rc = fail(RTX_ERR_INVALID_ARG, "capacity %llu < PPM length %llu",
+                                                  (unsigned long long)capacity, (unsigned long long)len);
+    if (rc == RTX_OK && copy_to_host(out_text, text, len, st) != hipSuccess)
+        rc = fail(RTX_ERR_HIP, "copying the PPM text to the host");
+    if (st) (void)hipStreamSynchronize(st);
+    (void)hipSetDevice(cur);
     if (rc == RTX_OK) *out_len = len;
     return rc;
 }

@@ -484,7 +484,15 @@ struct Params {
     uint32_t redo_cap;
     uint32_t* redo_count;
     uint32_t* redo_bits;
+    // Tests of the wave-level claim guard (rtx_kernel.hip partial_wave): in the debug library
+    // (librtx_dbgclaim.so, -DRTX_DEBUG_PARTIAL=1) claim site 1 (defer queue), 2 (redo list) or 3 (unit
+    // queue) is entered by the even lanes only (RTX_DEBUG_PARTIAL_SITE); ignored by every other build.
+    uint32_t debug_partial;
 };
+
+// Error bits of *Params::error_flag (rtx_capi.hip collect_on turns them into RTX_ERR_HIP).
+constexpr uint32_t KERR_WATCHDOG = 1u;      // a wave outlived RTX_WATCHDOG_S
+constexpr uint32_t KERR_PARTIAL_WAVE = 2u;  // a wave-level claim was reached without the whole wave
 
 struct Ray {
     V3 o, d;

@@ -37,7 +37,26 @@
 #define RTX_NEAR_FMA 1
 #endif
 
+#ifndef RTX_DEBUG_PARTIAL  // 1: the debug library (librtx_dbgclaim.so) that enters a claim with half the wave
+#define RTX_DEBUG_PARTIAL 0
+#endif
+
 namespace rtxd {
+
+// The wave-level claims (the unit queue, the defer queue, the redo list) take ONE atomic, issued by
+// lane 0, and broadcast its result with readfirstlane.  That is only right with the whole wave
+// active: without lane 0 no atomic is issued and every lane reads the first active lane's stale
+// value (slot 0, unit 0: colliding records and a unit rendered again and again — the hang of the
+// round-4 early-claim refactor), and with lane 0 the absent lanes would claim on
+// their own later.  Each site therefore checks EXEC first, on SALU only (s_cmp + s_cbranch on a copy
+// of exec, no VGPR): a partial wave flags the render (KERR_PARTIAL_WAVE -> RTX_ERR_HIP) and claims
+// nothing, every wave stops at its next check of the flag, and the render fails loudly instead of
+// hanging or returning a corrupt frame.
+__device__ __forceinline__ bool partial_wave() { return __builtin_amdgcn_read_exec() != ~0ull; }
+// The debug library only: the odd lanes stay out of claim site `site` (tests/test_claim_guard.py).
+__device__ __forceinline__ bool dbg_skip(const Params& p, uint32_t site, uint32_t lane) {
+    return RTX_DEBUG_PARTIAL && p.debug_partial == site && (lane & 1u);
+}
 
 __device__ __forceinline__ void flush_counters(const Params& p, uint64_t samples, const Counters& cnt) {
     atomicAdd(&p.counters[0], (unsigned long long)samples);
@@ -291,6 +310,12 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
     auto defer = [&](const bool far) {
         const uint64_t fm = ballot(far);
         if (fm == 0) return;
+        if (dbg_skip(p, 1u, lane)) return;  // (debug library: the even lanes reach the claim alone)
+        if (partial_wave()) {  // no claim without the whole wave: the render fails (KERR_PARTIAL_WAVE)
+            atomicOr(p.error_flag, KERR_PARTIAL_WAVE);
+            if (far) mode = M_CLAIM;
+            return;
+        }
         uint32_t b = 0;
         if (lane == 0) b = atomicAdd(p.defer_count, (uint32_t)__popcll(fm));
         b = __builtin_amdgcn_readfirstlane(b);
@@ -313,6 +338,11 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
         // redo list (one reservation per wave, coalesced stores); past the list's end, to the redo bits.
         const uint64_t om = ballot(full);
         if (om == 0) return;
+        if (dbg_skip(p, 2u, lane)) return;
+        if (partial_wave()) {
+            atomicOr(p.error_flag, KERR_PARTIAL_WAVE);
+            return;
+        }
         uint32_t b2 = 0;
         if (lane == 0) b2 = atomicAdd(p.redo_count, (uint32_t)__popcll(om));
         b2 = __builtin_amdgcn_readfirstlane(b2);
@@ -337,9 +367,13 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
         // Watchdog (RTX_WATCHDOG_S): a wave never outlives p.watchdog_ticks, so a bug cannot
         // keep the GPU busy forever; the render then fails with RTX_ERR_HIP (collect_on).
         // The loop is wave-uniform, so is this test.
-        if ((++iter & 255u) == 0 && __builtin_amdgcn_s_memrealtime() - t_start > p.watchdog_ticks) {
-            if (lane == 0) atomicOr(p.error_flag, 1u);
-            break;
+        // A wave also stops once any wave has flagged the render (KERR_*): the output is invalid.
+        if ((++iter & 255u) == 0) {
+            if (__builtin_amdgcn_s_memrealtime() - t_start > p.watchdog_ticks) {
+                if (lane == 0) atomicOr(p.error_flag, KERR_WATCHDOG);
+                break;
+            }
+            if (__builtin_amdgcn_readfirstlane(*(volatile uint32_t*)p.error_flag) != 0u) break;
         }
         if (TIME) clk = __builtin_amdgcn_s_memtime();
         // primitive batching only for a scene in LDS: a lane that waits re-reads its entry, which
@@ -393,9 +427,12 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
         for (;;) {
             const uint64_t wm = ballot(mode == M_CLAIM);
             if (wm == 0) break;
-            if (cursor >= u_items && !exhausted) {  // claim the next unit (wave-uniform)
-                uint32_t un = 0;
-                if (lane == 0) un = atomicAdd(p.tile_counter, 1u);
+            if (cursor >= u_items && !exhausted && dbg_skip(p, 3u, lane)) {
+                exhausted = true;  // (debug library: the even lanes reach the claim alone)
+            } else if (cursor >= u_items && !exhausted) {  // claim the next unit (wave-uniform)
+                uint32_t un = 0xFFFFFFFFu;  // a partial wave claims nothing: exhausted, the render flagged
+                if (partial_wave()) atomicOr(p.error_flag, KERR_PARTIAL_WAVE);
+                else if (lane == 0) un = atomicAdd(p.tile_counter, 1u);
                 const uint32_t uu = __builtin_amdgcn_readfirstlane(un);  // the whole wave is here: lane 0's
                 exhausted = uu >= n_units;
                 if (!exhausted && (TIER == 2 || listed)) {
@@ -513,6 +550,18 @@ __global__ __launch_bounds__(256) void spill_redo_list(Params p) {
         const uint32_t id = p.redo_ids[i];
         atomicOr(p.redo_bits + (id >> 5), 1u << (id & 31u));
     }
+}
+
+// The redo bits are set only when the list overflowed (redo_count > redo_cap: by the near pass past
+// the list's end, and by spill_redo_list); after the redo pass has read them, this clears the chunk's
+// bits again, so they are zero at every chunk's start without a memset of the whole bitmap per chunk
+// (130 MB at C2, ~180 MB at C5).  A return when the list held every id.
+__global__ __launch_bounds__(256) void clear_redo_bits(Params p) {
+    if (__builtin_amdgcn_readfirstlane(*(volatile uint32_t*)p.redo_count) <= p.redo_cap) return;
+    const uint32_t twl = p.tile_w_log2;
+    const uint64_t words = (uint64_t)p.kn * tiles_x_of(p.width, twl) * tiles_y_of(p.rows, twl) * 2;  // 64 bits a tile
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < words; i += (uint64_t)gridDim.x * 256)
+        p.redo_bits[i] = 0u;
 }
 
 // GetPixelColor's sum over the stored colours of samples [k0, k0 + kn), in k order
@@ -660,17 +709,18 @@ hipError_t launch_tiered(Params pn, Params pf, hipStream_t stream) {
             fprintf(stderr, "rtx tiered: waves/wg %d, wgs/CU %d / %d / %d, grid %llu, sub %u, units %llu, lds %zu / %zu B, "
                     "cap %u\n", WAVES, per_n, per_f, per_r, (unsigned long long)bn, pn.sub, (unsigned long long)units, sn,
                     sf, pn.defer_cap);
-        // the unit queue head, the chunk's record count, its redo list count and bits
+        // the unit queue head, the chunk's record count, its redo list count (the redo bits are zero:
+        // the caller zeroes them once, clear_redo_bits after every chunk that set any)
         if ((e = hipMemsetAsync(pn.tile_counter, 0, sizeof(uint32_t), stream)) != hipSuccess) return e;
         if ((e = hipMemsetAsync(pn.defer_count, 0, sizeof(uint32_t), stream)) != hipSuccess) return e;
         if ((e = hipMemsetAsync(pn.redo_count, 0, sizeof(uint32_t), stream)) != hipSuccess) return e;
-        if ((e = hipMemsetAsync(pn.redo_bits, 0, (size_t)pn.kn * tiles * 8, stream)) != hipSuccess) return e;
         hipLaunchKernelGGL(kn, dim3((uint32_t)bn), dim3(block), sn, stream, pn);
         if ((e = hipMemsetAsync(pf.tile_counter, 0, sizeof(uint32_t), stream)) != hipSuccess) return e;
         hipLaunchKernelGGL(kf, dim3((uint32_t)per_f * cus), dim3(block), sf, stream, pf);
         hipLaunchKernelGGL(spill_redo_list, dim3((uint32_t)cus * 4), dim3(256), 0, stream, pn);
         if ((e = hipMemsetAsync(pr.tile_counter, 0, sizeof(uint32_t), stream)) != hipSuccess) return e;
         hipLaunchKernelGGL(kr, dim3((uint32_t)br), dim3(block), sf, stream, pr);
+        hipLaunchKernelGGL(clear_redo_bits, dim3((uint32_t)cus * 4), dim3(256), 0, stream, pn);
         hipLaunchKernelGGL(reduce_samples, dim3((uint32_t)((slots + 255) / 256)), dim3(256), 0, stream, pn,
                            (uint32_t)(k0 + pn.kn >= spp));
         if ((e = hipGetLastError()) != hipSuccess) return e;

@@ -123,7 +123,7 @@ RTX_SYMBOLS = [
     "rtx_ppm_max_bytes", "rtx_encode_ppm_device", "rtx_render_ppm", "rtx_scene_create_spheres", "rtx_scene_export",
     "rtx_release_device_memory", "rtx_device_scratch_bytes", "rtx_scene_create_ex", "rtx_scene_topology",
     "rtx_camera_octant", "rtx_walk_tree", "rtx_render_ex", "rtx_scene_walk_skip", "rtx_walk_skip",
-    "rtx_scene_near_region", "rtx_scene_near_skip", "rtx_walk_near_region",
+    "rtx_scene_near_region", "rtx_scene_near_skip", "rtx_walk_near_region", "rtx_render_ppm_ex",
 ]
 RTXHOST_SYMBOLS = [
     "rtxhost_build_scene", "rtxhost_scene_free", "rtxhost_scene_desc", "rtxhost_scene_camera",
@@ -202,6 +202,9 @@ def load() -> ctypes.CDLL:
     L.rtx_render_ppm.argtypes = [c_void_p, POINTER(Camera), c_uint64, c_void_p, c_uint64, POINTER(c_uint64),
                                  POINTER(Stats)]
     L.rtx_render_ppm.restype = c_int
+    L.rtx_render_ppm_ex.argtypes = [c_void_p, POINTER(Camera), c_uint64, c_int, c_void_p, c_uint64, POINTER(c_uint64),
+                                    POINTER(Stats)]
+    L.rtx_render_ppm_ex.restype = c_int
     L.rtx_scene_create_spheres.argtypes = [POINTER(Sphere), c_uint32, POINTER(Material), c_uint32, POINTER(Texture),
                                            c_uint32, POINTER(c_uint32), c_uint64, c_uint64, c_uint64,
                                            POINTER(c_void_p), POINTER(c_double)]
@@ -444,6 +447,20 @@ class DeviceScene:
         check(L.rtx_render_ppm(self._h, ctypes.byref(cam), seed, buf.ctypes.data_as(c_void_p), cap, ctypes.byref(n),
                                None), "rtx_render_ppm")
         return buf[: n.value].tobytes()
+
+    def render_ppm_ex(self, cam: Camera, seed: int, n_gpus: int = 1, stats: bool = False):
+        """rtx_render_ppm_ex (ABI 9): the bands of rtx_render(n_gpus) gathered to device 0, the PPM encoded
+        there; returns the bytes (and the Stats when stats=True)."""
+        import numpy as np
+        L = load()
+        cap = int(L.rtx_ppm_max_bytes(cam.image_width, cam.image_height))
+        buf = np.empty(cap, dtype=np.uint8)
+        n = c_uint64()
+        st = Stats()
+        check(L.rtx_render_ppm_ex(self._h, ctypes.byref(cam), seed, n_gpus, buf.ctypes.data_as(c_void_p), cap,
+                                  ctypes.byref(n), ctypes.byref(st)), "rtx_render_ppm_ex")
+        out = buf[: n.value].tobytes()
+        return (out, st) if stats else out
 
     def close(self) -> None:
         if self._h:

@@ -28,19 +28,35 @@ def test_broken_source_fails_make(built, tmp_path, src):
     assert not stale.exists()
 
 
+def bench_profile_paths():
+    """The PMC summaries bench.py reads by default (its --valu and --traffic defaults)."""
+    import re
+
+    with open(os.path.join(ROOT, "bench.py")) as f:
+        src = f.read()
+    paths = {}
+    for opt in ("valu", "traffic"):
+        m = re.search(rf'"--{opt}", default=os.path.join\(ROOT, "profiles", "([^"]+)"\)', src)
+        assert m, f"bench.py --{opt} default not found"
+        paths[opt] = os.path.join(ROOT, "profiles", m.group(1))
+    return paths
+
+
 def test_committed_profiles_name_one_build():
     """bench.py derives roofline.frac / roofline.hbm only from PMC summaries measured on the
-    library it loads (by hash): the committed VALU and traffic summaries must name the same one."""
+    library it loads (by hash): the VALU and traffic summaries it reads by default must exist, hold the
+    headline workload (BASELINE configs[1]), and name one library for every workload they hold."""
     import json
 
-    hashes = set()
-    for name in ("valu_r03.json", "traffic_r03.json"):
-        with open(os.path.join(ROOT, "profiles", name)) as f:
-            d = json.load(f)
-        assert d.get("librtx_sha256_16"), name
-        assert d["workload"] == "random_spheres:1920x1080x500"
-        hashes.add(d["librtx_sha256_16"])
-    assert len(hashes) == 1, hashes
+    hashes = {}
+    for opt, path in bench_profile_paths().items():
+        with open(path) as f:
+            rows = [json.loads(line) for line in f if line.strip()] if path.endswith(".jsonl") else [json.load(f)]
+        assert any(r.get("workload") == "random_spheres:1920x1080x500" for r in rows), (path, "no headline entry")
+        for r in rows:
+            assert r.get("librtx_sha256_16"), (path, r.get("workload"))
+            hashes.setdefault(r["librtx_sha256_16"], []).append((opt, r["workload"]))
+    assert len(hashes) == 1, {h: v[:3] for h, v in hashes.items()}
 
 
 def test_library_carries_no_build_date():
@@ -51,5 +67,5 @@ def test_library_carries_no_build_date():
     import rtx
 
     info = rtx.load().rtx_build_info().decode()
-    assert "ABI 8" in info
+    assert "ABI 9" in info
     assert not re.search(r"(Jan|Feb|Mar|Apr|May|Jun|Jul|Aug|Sep|Oct|Nov|Dec) +\d+ +\d{4}|\d\d:\d\d:\d\d", info), info

@@ -1,0 +1,69 @@
+"""The wave-level claim guard (raytracer-go_amd/csrc/rtx_kernel.hip partial_wave).
+
+The megakernel's three claims — a unit of (tile, samples) from the unit queue, slots in the defer queue,
+slots in the redo list — each take ONE atomic issued by lane 0 and broadcast its result with
+readfirstlane.  That is only right when the whole wave reaches the claim.  Each site checks EXEC on
+SALU first; a partial wave flags the render and claims nothing, every wave stops at its next check of
+the flag, and rtx_render fails with RTX_ERR_HIP instead of hanging or returning a corrupt frame (the
+round-4 early-claim refactor hung, then gave run-to-run different frames, on exactly this).
+
+librtx_dbgclaim.so is the megakernel built with RTX_DEBUG_PARTIAL=1: claim site RTX_DEBUG_PARTIAL_SITE
+(1 = defer queue, 2 = redo list, 3 = unit queue) is entered by the even lanes only.  Each case runs in a
+child process with its own time limit, so a guard that failed to fire shows as a timeout, not a hung
+runner.  The work every pixel needs done exactly once is camera.go:198-222's.
+"""
+import os
+import subprocess
+import sys
+
+import pytest
+
+import rtx
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+DBG = os.path.join(ROOT, "raytracer-go_amd", "librtx_dbgclaim.so")
+
+CHILD = """
+import sys, hashlib, numpy as np, torch
+sys.path[:0] = ['raytracer-go_amd', 'tests']
+import rtx
+torch.cuda.set_device(0)
+s = rtx.HostScene('random_spheres', 1)
+d = rtx.DeviceScene(s.desc)
+cam = s.camera(width=96, spp=4)
+try:
+    img, st = d.render_host(cam, 7, n_gpus=1, stats=True)
+    print('OK', hashlib.sha256(img.tobytes()).hexdigest()[:16], st.walk_layout.split(':')[0], st.deferred_paths)
+except rtx.RtxError as e:
+    print('ERR', e.code, e)
+"""
+
+
+def run_child(env: dict) -> str:
+    res = subprocess.run([sys.executable, "-c", CHILD], cwd=ROOT, env=dict(os.environ, **env), capture_output=True,
+                         text=True, timeout=120)
+    assert res.returncode == 0, res.stdout + res.stderr
+    return res.stdout.strip().splitlines()[-1]
+
+
+def test_debug_library_renders_like_the_product(built):
+    """With no site selected the debug library takes the product's path: the same frame as librtx.so,
+    tiered, with deferred paths (so the defer-queue claim ran)."""
+    assert os.path.exists(DBG), "librtx_dbgclaim.so not built (make -C raytracer-go_amd)"
+    want = run_child({})
+    got = run_child({"RTX_LIB": DBG, "RTX_DEBUG_PARTIAL_SITE": "0"})
+    assert want.startswith("OK") and got == want, (want, got)
+    assert want.split()[2] == "tiered" and int(want.split()[3]) > 0, want
+
+
+@pytest.mark.parametrize("site,extra", [(1, {}), (2, {"RTX_DEFER_CAP": "0"}), (3, {})],
+                         ids=["defer_queue", "redo_list", "unit_queue"])
+def test_partial_wave_claim_fails_loudly(built, site, extra):
+    """Half a wave at a claim: rtx_render returns RTX_ERR_HIP naming the partial EXEC, promptly (the
+    watchdog, set to 60 s, is not what stops it)."""
+    env = {"RTX_LIB": DBG, "RTX_DEBUG_PARTIAL_SITE": str(site), "RTX_WATCHDOG_S": "60", **extra}
+    out = run_child(env)
+    assert out.startswith(f"ERR {rtx.RTX_ERR_HIP}"), out
+    assert "without the whole wave" in out, out

@@ -78,8 +78,10 @@ def test_every_c_identifier_is_declared():
     names = set(re.findall(r"\bC\.(\w+)", GO))
     missing = [n for n in sorted(names) if n not in C_SCALARS and not re.search(rf"\b{n}\b", HDR)]
     assert not missing, missing
-    assert {"rtx_scene_create", "rtx_scene_create_spheres", "rtx_render_ppm", "rtx_render", "rtx_scene_destroy",
+    assert {"rtx_scene_create", "rtx_scene_create_spheres", "rtx_render_ppm", "rtx_render_ppm_ex", "rtx_scene_destroy",
             "rtx_last_error", "rtx_ppm_max_bytes"} <= names
+    # several GPUs: the text is encoded on device 0 (rtx_render_ppm_ex), never formatted in Go
+    assert "C.rtx_render(" not in GO and "ToGamma2()" not in GO
 
 
 def test_c_calls_match_the_prototypes():
@@ -235,3 +237,31 @@ def test_go_sequence_gpu_bvh(gpu, scene):
     reg = rtx.Region(0, 0, cam.image_width, cam.image_height, 0, 1)
     want, _ = ob.render(tree, cam, 2024, reg, ob.ORDER_ITERATIVE)
     assert text == oracle_ppm(want)
+
+
+@pytest.mark.gpu
+def test_go_sequence_several_gpus(gpu):
+    """renderOnDevices(gpus > 1): rtx_scene_create(&desc) -> rtx_render_ppm_ex(scene, &cam, seed, gpus, text,
+    cap, &n, NULL) -> rtx_scene_destroy, with no host formatting.  On a one-GPU box the same entry renders 8
+    simulated bands on device 0 (RTX_SIM_BANDS=8: the rows of an 8-GPU node, assembled by the de-interleave
+    kernel) and encodes them there; the P3 bytes are the oracle's Render output."""
+    import os
+
+    L = rtx.load()
+    host = rtx.HostScene("random_spheres", 1)
+    cam = host.camera(width=96, spp=4)
+    h = ctypes.c_void_p()
+    rtx.check(L.rtx_scene_create(host.desc, ctypes.byref(h)), "rtx_scene_create")
+    cap = int(L.rtx_ppm_max_bytes(cam.image_width, cam.image_height))
+    buf = np.empty(cap, dtype=np.uint8)
+    n = ctypes.c_uint64()
+    os.environ["RTX_SIM_BANDS"] = "8"
+    try:
+        rtx.check(L.rtx_render_ppm_ex(h, ctypes.byref(cam), 2024, 1, buf.ctypes.data_as(ctypes.c_void_p), cap,
+                                      ctypes.byref(n), None), "rtx_render_ppm_ex")
+    finally:
+        os.environ.pop("RTX_SIM_BANDS", None)
+        L.rtx_scene_destroy(h)
+    reg = rtx.Region(0, 0, cam.image_width, cam.image_height, 0, 1)
+    want, _ = ob.render(host.desc, cam, 2024, reg, ob.ORDER_ITERATIVE)
+    assert buf[: n.value].tobytes() == oracle_ppm(want)

@@ -78,3 +78,39 @@ def test_render_ppm_matches_render_plus_host_encode(torch_cuda, built):
     rgb, _ = dev.render_host(cam, 9)
     header = f"P3\n{cam.image_width} {cam.image_height}\n255\n".encode()
     assert text == header + rtx.ppm_encode(rgb)
+
+
+@pytest.mark.gpu
+def test_render_ppm_ex_bands_equal_one_device(built):
+    """rtx_render_ppm_ex (ABI 9), the multi-GPU Render's output with no host formatting: the bands of
+    rtx_render(n_gpus) gathered to device 0 and encoded there.  Its bytes equal rtx_render_ppm's one-device
+    bytes for one band, for 8 simulated bands assembled by the de-interleave kernel (RTX_SIM_BANDS=8, the
+    rows an 8-GPU node renders; H = 90 leaves ragged bands), for the same bands without RCCL (the per-band
+    copies, then one upload), and for the RCCL path as a 1-rank ncclGather (RTX_FORCE_RCCL=1).  Run in a
+    child process (its own time limit: an RCCL problem cannot hang the runner)."""
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = (
+        "import os, sys, torch; sys.path[:0] = ['raytracer-go_amd', 'tests']; import rtx\n"
+        "torch.cuda.set_device(0)\n"
+        "s = rtx.HostScene('random_spheres', 1); d = rtx.DeviceScene(s.desc)\n"
+        "cam = s.camera(width=160, spp=4)\n"
+        "assert cam.image_height == 90\n"
+        "want = d.render_ppm(cam, 9)\n"
+        "cases = [({}, rtx.RTX_GATHER_NONE), ({'RTX_SIM_BANDS': '8'}, rtx.RTX_GATHER_DEVICE),\n"
+        "         ({'RTX_SIM_BANDS': '8', 'RTX_NO_RCCL': '1'}, rtx.RTX_GATHER_HOST),\n"
+        "         ({'RTX_FORCE_RCCL': '1'}, rtx.RTX_GATHER_RCCL)]\n"
+        "for env, kind in cases:\n"
+        "    for k in ('RTX_SIM_BANDS', 'RTX_NO_RCCL', 'RTX_FORCE_RCCL'): os.environ.pop(k, None)\n"
+        "    os.environ.update(env)\n"
+        "    got, st = d.render_ppm_ex(cam, 9, n_gpus=1, stats=True)\n"
+        "    assert got == want, (env, len(got), len(want))\n"
+        "    assert st.gather_kind == kind, (env, st.gather_kind)\n"
+        "    print('ok', env, st.gather_kind, round(st.gather_ms, 3))\n"
+        "rtx.release_device_memory(-1)\n")
+    res = subprocess.run([sys.executable, "-c", code], cwd=root, capture_output=True, text=True, timeout=150)
+    assert res.returncode == 0, res.stdout + res.stderr
+    assert res.stdout.count("ok ") == 4, res.stdout
