@@ -35,7 +35,7 @@ d = rtx.DeviceScene(s.desc)
 cam = s.camera(width=96, spp=4)
 try:
     img, st = d.render_host(cam, 7, n_gpus=1, stats=True)
-    print('OK', hashlib.sha256(img.tobytes()).hexdigest()[:16], st.walk_layout.split(':')[0], st.deferred_paths)
+    print('OK', hashlib.sha256(img.tobytes()).hexdigest()[:16], 'tiered' if st.walk_layout & rtx.RTX_LAYOUT_TIERED else 'one', st.deferred_paths)
 except rtx.RtxError as e:
     print('ERR', e.code, e)
 """
