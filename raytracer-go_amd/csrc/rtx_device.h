@@ -488,7 +488,15 @@ struct Params {
     // (librtx_dbgclaim.so, -DRTX_DEBUG_PARTIAL=1) claim site 1 (defer queue), 2 (redo list) or 3 (unit
     // queue) is entered by the even lanes only (RTX_DEBUG_PARTIAL_SITE); ignored by every other build.
     uint32_t debug_partial;
+    uint32_t cam_pool;  // 1: the near pass takes camera rays from the wave's LDS pool when it fits (RTX_CAM_POOL=0: off)
 };
+
+// The camera-ray pool of render_items<POOL>: after the fixed layout's scene copy (16-B aligned), 64 rays
+// of 2 float4 per wave (2 KB).
+constexpr uint32_t POOL_BYTES_PER_WAVE = 64 * 32;
+__host__ __device__ __forceinline__ uint32_t pool_f4_offset(const Params& p) {
+    return (lds_fixed_bytes(p.n_entries, p.n_quads, p.n_materials, p.n_textures) + 15u) / 16u;
+}
 
 // Error bits of *Params::error_flag (rtx_capi.hip collect_on turns them into RTX_ERR_HIP).
 constexpr uint32_t KERR_WATCHDOG = 1u;      // a wave outlived RTX_WATCHDOG_S

@@ -211,10 +211,19 @@ __device__ __forceinline__ void split_clk(uint64_t& acc, uint64_t& clk) {
 // rendered again from their camera rays on the far tree — it returns at once when none did.
 // Every sample's Philox blocks are keyed by (pixel, sample, event), so a path resumed in another
 // launch draws exactly what it would have drawn.
+//
+// POOL (the timed kernel's near pass, scene in the LDS copy): new items take their camera
+// rays from a per-wave pool in LDS after the scene copy, which holds the rays of one 64-item block of
+// the unit — one sample of the tile's 64 pixels, sample-major as the items are handed out — drawn by
+// the whole wave at once when the first item of the block is claimed.  The rays (GetRay, camera.go:
+// 265-299: Philox block (0, 0) of (pixel, sample), the defocus disk's rejection loop) are the same
+// bits; only who evaluates them changes: 64 lanes per evaluation instead of the few lanes a shading
+// phase claims for (about a third of the wave).
 template <bool COUNT, bool USE_LDS, bool QUADS, bool NOISE, int WAVES = 8, int MINW = 0, bool HYB = false,
-          bool CLK = false, int TIER = 0>
+          bool CLK = false, int TIER = 0, bool POOL = false>
 __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
     constexpr bool TIME = COUNT || CLK;
+    static_assert(!POOL || (USE_LDS && !COUNT && (TIER == 0 || TIER == 1)), "the camera-ray pool: timed, LDS scenes");
     if constexpr (TIER == 3) {
         if (__builtin_amdgcn_readfirstlane(*(volatile uint32_t*)p.redo_count) == 0u) return;
         if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&p.counters[24], 1ull);  // chunks with a redo
@@ -282,6 +291,9 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
     // tile (index, origin u_x, u_r), first sample, items, next item
     uint32_t u_tile = 0, u_x = 0, u_r = 0, u_k0 = 0, u_items = 0, cursor = 0;
     bool exhausted = false;
+    // POOL: the wave's 64 camera rays (2 float4 each) after the scene copy, and the unit's block they hold
+    float4* const pool = POOL ? lds_entries + pool_f4_offset(p) + (threadIdx.x >> 6) * 128 : nullptr;
+    uint32_t pool_blk = 0xFFFFFFFFu;
 
     uint32_t mode = M_CLAIM, seg = 0, items_done = 0;
     size_t pix = 0;  // the lane's item in the tile-major scratch: 64 * tile + pixel within the tile
@@ -447,6 +459,7 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
                     const uint32_t cnt_k = min(p.sub, p.k0 + p.kn - u_k0);
                     u_items = 64u * cnt_k;
                     cursor = 0;
+                    pool_blk = 0xFFFFFFFFu;
                     if (TIER == 3 && !listed) {  // a unit without a flagged sample: the next unit
                         const bool any = lane < cnt_k && redo64[(size_t)(u_k0 + lane - p.k0) * n_tiles + u_tile] != 0;
                         if (ballot(any) == 0) cursor = u_items;
@@ -457,9 +470,27 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
                 if (mode == M_CLAIM) mode = M_DONE;
                 break;
             }
+            uint32_t avail = u_items - cursor;  // items this round can hand out
+            if constexpr (POOL) {
+                const uint32_t blk = cursor >> 6;
+                if (blk != pool_blk) {  // the block's 64 camera rays, one per lane (sample u_k0 + blk, pixel lane)
+                    pool_blk = blk;
+                    const uint32_t lx = u_x + (lane & tw_mask), lr = u_r + (lane >> twl);
+                    if (lx < p.width && lr < p.rows) {
+                        const uint32_t x = p.x0 + lx, y = p.y0 + p.rank + lr * p.world;
+                        const PathRng cr{rng.k0, rng.k1, y * c.image_width + x, u_k0 + blk};
+                        uint32_t dr = 0;
+                        const Ray cray = camera_ray<true>(c, pixel_base(c, x, y), cr, cr.block(0u, 0u), dr);
+                        pool[2 * lane] = make_float4(cray.o.x, cray.o.y, cray.o.z, 0.0f);
+                        pool[2 * lane + 1] = make_float4(cray.d.x, cray.d.y, cray.d.z, 0.0f);
+                    }
+                    __builtin_amdgcn_wave_barrier();  // (LDS is in order within the wave)
+                }
+                avail = min(u_items, 64u * blk + 64u) - cursor;
+            }
             const uint32_t rank = (uint32_t)__popcll(wm & ((1ull << lane) - 1ull));
             bool got = false;
-            if (TIER == 2 && mode == M_CLAIM && rank < u_items - cursor) {  // resume a record
+            if (TIER == 2 && mode == M_CLAIM && rank < avail) {  // resume a record
                 const float4* q = p.defer + 4 * (size_t)(u_k0 + cursor + rank);
                 const float4 q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3];
                 r = Ray{v3(q0.x, q0.y, q0.z), v3(q1.x, q1.y, q1.z)};
@@ -471,7 +502,7 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
                 pix = __float_as_uint(q3.w);
                 mode = M_START;
                 ready = true;
-            } else if (TIER != 2 && mode == M_CLAIM && rank < u_items - cursor) {
+            } else if (TIER != 2 && mode == M_CLAIM && rank < avail) {
                 uint32_t j = cursor + rank, l = j & 63u;  // sample-major within the unit
                 uint32_t lx = u_x + (l & tw_mask);
                 uint32_t lr = u_r + (l >> twl);
@@ -491,7 +522,12 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
                 if (lx < p.width && lr < p.rows &&
                     (TIER != 3 || listed || ((redo64[((size_t)(k - p.k0) * n_tiles * 64 + slot) >> 6] >> l) & 1ull))) {
                     const uint32_t x = p.x0 + lx, y = p.y0 + p.rank + lr * p.world;
-                    base = pixel_base(c, x, y);
+                    if constexpr (POOL) {  // the ray the wave drew for this item (l: the pixel of the block)
+                        const float4 po = pool[2 * l], pd = pool[2 * l + 1];
+                        r = Ray{v3(po.x, po.y, po.z), v3(pd.x, pd.y, pd.z)};
+                    } else {
+                        base = pixel_base(c, x, y);
+                    }
                     rng.pixel = y * c.image_width + x;
                     rng.sample = k;
                     pix = slot;
@@ -499,10 +535,10 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
                 }
             }
             const uint32_t taken = (uint32_t)__popcll(wm);
-            cursor = cursor + taken > u_items ? u_items : cursor + taken;
+            cursor += taken < avail ? taken : avail;
             if (got) {
                 if (COUNT && TIER == 1) path0 = cnt;
-                r = camera_ray<!COUNT>(c, base, rng, rng.block(0u, 0u), cnt.draws);  // GetRay, camera.go:257
+                if constexpr (!POOL) r = camera_ray<!COUNT>(c, base, rng, rng.block(0u, 0u), cnt.draws);  // GetRay, camera.go:257
                 thr = v3(1.0f, 1.0f, 1.0f);
                 acc = v3(0.0f, 0.0f, 0.0f);
                 seg = 0;
@@ -679,15 +715,20 @@ inline size_t items_shmem(const Params& p, bool use_lds, bool hyb) {
 // both in the LDS copy (USE_LDS), both in HBM with an LDS cache of their hot entries (HYB), or both
 // in HBM: per chunk the near pass (pn), the far pass over its queue (pf), the redo pass over the
 // samples whose records did not fit (its waves return at once when none), the reduction.
-template <bool COUNT, int WAVES, int MINW, bool CLK = false, bool USE_LDS = true, bool HYB = false>
+// POOL: the near pass takes its camera rays from the waves' LDS pools (render_items<POOL>), in
+// workgroups of WN waves (12: two per CU, each with its scene copy and 12 pools); the far and redo
+// passes keep WAVES.
+template <bool COUNT, int WAVES, int MINW, bool CLK = false, bool USE_LDS = true, bool HYB = false, bool POOL = false,
+          int WN = POOL ? 12 : WAVES>
 hipError_t launch_tiered(Params pn, Params pf, hipStream_t stream) {
-    const auto kn = render_items<COUNT, USE_LDS, false, false, WAVES, MINW, HYB, CLK, 1>;
+    const auto kn = render_items<COUNT, USE_LDS, false, false, WN, MINW, HYB, CLK, 1, POOL>;
     const auto kf = render_items<COUNT, USE_LDS, false, false, WAVES, MINW, HYB, CLK, 2>;
     const auto kr = render_items<COUNT, USE_LDS, false, false, WAVES, MINW, HYB, false, 3>;
-    const size_t sn = items_shmem(pn, USE_LDS, HYB), sf = items_shmem(pf, USE_LDS, HYB);
-    constexpr int block = 64 * WAVES;
+    const size_t sn = POOL ? (size_t)pool_f4_offset(pn) * 16 + WN * POOL_BYTES_PER_WAVE : items_shmem(pn, USE_LDS, HYB),
+                 sf = items_shmem(pf, USE_LDS, HYB);
+    constexpr int block = 64 * WAVES, block_n = 64 * WN;
     int cus = 0, per_n = 0, per_f = 0, per_r = 0;
-    hipError_t e = resident_grid((const void*)kn, block, sn, &per_n, &cus);
+    hipError_t e = resident_grid((const void*)kn, block_n, sn, &per_n, &cus);
     if (e == hipSuccess) e = resident_grid((const void*)kf, block, sf, &per_f, &cus);
     if (e == hipSuccess) e = resident_grid((const void*)kr, block, sf, &per_r, &cus);
     if (e != hipSuccess) return e;
@@ -699,22 +740,22 @@ hipError_t launch_tiered(Params pn, Params pf, hipStream_t stream) {
     for (uint32_t k0 = 0; k0 < spp; k0 += chunk) {
         pn.k0 = pf.k0 = pr.k0 = k0;
         pn.kn = pf.kn = pr.kn = spp - k0 < chunk ? spp - k0 : chunk;
-        pn.sub = sub ? sub : unit_samples(tiles, pn.kn, WAVES, per_n, cus);
+        pn.sub = sub ? sub : unit_samples(tiles, pn.kn, WN, per_n, cus);
         pf.sub = pr.sub = pn.sub;
         const uint64_t units = tiles * ((pn.kn + pn.sub - 1) / pn.sub);
         uint64_t bn = (uint64_t)per_n * cus, br = (uint64_t)per_r * cus;
-        if (bn > (units + WAVES - 1) / WAVES) bn = (units + WAVES - 1) / WAVES;
+        if (bn > (units + WN - 1) / WN) bn = (units + WN - 1) / WN;
         if (br > (units + WAVES - 1) / WAVES) br = (units + WAVES - 1) / WAVES;
         if (pn.debug_launch)
-            fprintf(stderr, "rtx tiered: waves/wg %d, wgs/CU %d / %d / %d, grid %llu, sub %u, units %llu, lds %zu / %zu B, "
-                    "cap %u\n", WAVES, per_n, per_f, per_r, (unsigned long long)bn, pn.sub, (unsigned long long)units, sn,
-                    sf, pn.defer_cap);
+            fprintf(stderr, "rtx tiered: waves/wg %d / %d, wgs/CU %d / %d / %d, grid %llu, sub %u, units %llu, lds %zu / %zu B, "
+                    "cap %u, camera-ray pool %d\n", WN, WAVES, per_n, per_f, per_r, (unsigned long long)bn, pn.sub,
+                    (unsigned long long)units, sn, sf, pn.defer_cap, (int)POOL);
         // the unit queue head, the chunk's record count, its redo list count (the redo bits are zero:
         // the caller zeroes them once, clear_redo_bits after every chunk that set any)
         if ((e = hipMemsetAsync(pn.tile_counter, 0, sizeof(uint32_t), stream)) != hipSuccess) return e;
         if ((e = hipMemsetAsync(pn.defer_count, 0, sizeof(uint32_t), stream)) != hipSuccess) return e;
         if ((e = hipMemsetAsync(pn.redo_count, 0, sizeof(uint32_t), stream)) != hipSuccess) return e;
-        hipLaunchKernelGGL(kn, dim3((uint32_t)bn), dim3(block), sn, stream, pn);
+        hipLaunchKernelGGL(kn, dim3((uint32_t)bn), dim3(block_n), sn, stream, pn);
         if ((e = hipMemsetAsync(pf.tile_counter, 0, sizeof(uint32_t), stream)) != hipSuccess) return e;
         hipLaunchKernelGGL(kf, dim3((uint32_t)per_f * cus), dim3(block), sf, stream, pf);
         hipLaunchKernelGGL(spill_redo_list, dim3((uint32_t)cus * 4), dim3(256), 0, stream, pn);
@@ -726,6 +767,12 @@ hipError_t launch_tiered(Params pn, Params pf, hipStream_t stream) {
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     return hipSuccess;
+}
+
+// Whether the near pass of a tiered LDS render takes the camera-ray pool: wanted (Params::cam_pool) and two
+// 12-wave workgroups' scene copies and pools fit a CU's 160 KB.
+inline bool pool_fits(const Params& p) {
+    return p.cam_pool && (size_t)pool_f4_offset(p) * 16 + 12 * POOL_BYTES_PER_WAVE <= 80u * 1024u;
 }
 
 #ifndef RTX_HYB_WAVES  // the same for scenes in HBM with an 80 KB LDS cache of their most-read entries
@@ -776,9 +823,12 @@ hipError_t launch_render(const Params& p, uint32_t flags, hipStream_t stream, co
             return hipErrorInvalidValue;
         const bool clk = !count && (flags & RTX_FLAG_TIMING);  // diagnostics: the wave-cycle split of the passes
         if (place == RTX_SCENE_IN_LDS) {
-            if (clk) return launch_tiered<false, RTX_V3_WAVES, RTX_V3_MINW, true>(p, *far, stream);
-            return count ? launch_tiered<true, RTX_V3_WAVES, 0>(p, *far, stream)
-                         : launch_tiered<false, RTX_V3_WAVES, RTX_V3_MINW>(p, *far, stream);
+            const bool pool = pool_fits(p);  // (the counting kernel keeps its own camera rays: it counts their draws)
+            if (clk) return pool ? launch_tiered<false, RTX_V3_WAVES, RTX_V3_MINW, true, true, false, true>(p, *far, stream)
+                                 : launch_tiered<false, RTX_V3_WAVES, RTX_V3_MINW, true>(p, *far, stream);
+            if (count) return launch_tiered<true, RTX_V3_WAVES, 0>(p, *far, stream);
+            return pool ? launch_tiered<false, RTX_V3_WAVES, RTX_V3_MINW, false, true, false, true>(p, *far, stream)
+                        : launch_tiered<false, RTX_V3_WAVES, RTX_V3_MINW>(p, *far, stream);
         }
         if (place == RTX_SCENE_LDS_CACHE)  // both cached in LDS (tier_placement): 12-wave workgroups, two per CU
             return count ? launch_tiered<true, RTX_HYB_WAVES, 0, false, false, true>(p, *far, stream)

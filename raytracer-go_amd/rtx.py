@@ -202,9 +202,10 @@ def load() -> ctypes.CDLL:
     L.rtx_render_ppm.argtypes = [c_void_p, POINTER(Camera), c_uint64, c_void_p, c_uint64, POINTER(c_uint64),
                                  POINTER(Stats)]
     L.rtx_render_ppm.restype = c_int
-    L.rtx_render_ppm_ex.argtypes = [c_void_p, POINTER(Camera), c_uint64, c_int, c_void_p, c_uint64, POINTER(c_uint64),
-                                    POINTER(Stats)]
-    L.rtx_render_ppm_ex.restype = c_int
+    if hasattr(L, "rtx_render_ppm_ex"):  # ABI 9 (RTX_LIB may name an older build for A/B)
+        L.rtx_render_ppm_ex.argtypes = [c_void_p, POINTER(Camera), c_uint64, c_int, c_void_p, c_uint64,
+                                        POINTER(c_uint64), POINTER(Stats)]
+        L.rtx_render_ppm_ex.restype = c_int
     L.rtx_scene_create_spheres.argtypes = [POINTER(Sphere), c_uint32, POINTER(Material), c_uint32, POINTER(Texture),
                                            c_uint32, POINTER(c_uint32), c_uint64, c_uint64, c_uint64,
                                            POINTER(c_void_p), POINTER(c_double)]
