@@ -954,6 +954,7 @@ int enqueue_on(rtx_scene* s, DeviceCopy* c, const rtx_camera* cam, uint64_t seed
         if (tier && p.sub > 64) p.sub = 64;
         p.debug_partial = env_knob("RTX_DEBUG_PARTIAL_SITE", 0, 0, 3);  // (read by librtx_dbgclaim.so only)
         p.cam_pool = env_knob("RTX_CAM_POOL", 1, 0, 1);  // the near pass's camera-ray pool (A/B: 0 = off)
+        p.refill_hits = env_knob("RTX_REFILL_HITS", 0, 0, 64);  // its miss phases (A/B)
         p.item_waves = env_knob("RTX_ITEM_WAVES", 8, 4, 8) >= 8 ? 8u : 4u;
         p.grid_pct = env_knob("RTX_ITEM_GRID", 100, 1, 100);
         p.debug_launch = env_knob("RTX_DEBUG_LAUNCH", 0, 0, 1);

@@ -489,6 +489,7 @@ struct Params {
     // queue) is entered by the even lanes only (RTX_DEBUG_PARTIAL_SITE); ignored by every other build.
     uint32_t debug_partial;
     uint32_t cam_pool;  // 1: the near pass takes camera rays from the wave's LDS pool when it fits (RTX_CAM_POOL=0: off)
+    uint32_t refill_hits;  // POOL: a miss phase when fewer waiting lanes than this hit (RTX_REFILL_HITS; 0: never)
 };
 
 // The camera-ray pool of render_items<POOL>: after the fixed layout's scene copy (16-B aligned), 64 rays

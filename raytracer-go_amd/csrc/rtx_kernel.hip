@@ -48,10 +48,12 @@ namespace rtxd {
 // active: without lane 0 no atomic is issued and every lane reads the first active lane's stale
 // value (slot 0, unit 0: colliding records and a unit rendered again and again — the hang of the
 // round-4 early-claim refactor), and with lane 0 the absent lanes would claim on
-// their own later.  Each site therefore checks EXEC first, on SALU only (s_cmp + s_cbranch on a copy
-// of exec, no VGPR): a partial wave flags the render (KERR_PARTIAL_WAVE -> RTX_ERR_HIP) and claims
-// nothing, every wave stops at its next check of the flag, and the render fails loudly instead of
-// hanging or returning a corrupt frame.
+// their own later.  Each site therefore checks EXEC first, on SALU only (s_cmp + s_cselect on a copy
+// of exec into a uniform flag, no VGPR in the hot loop): a partial wave claims nothing (a unit claim
+// leaves the wave exhausted, a queue claim drops its paths), the wave flags the render when it ends
+// (KERR_PARTIAL_WAVE -> RTX_ERR_HIP), and the render fails loudly instead of hanging or returning a
+// corrupt frame.  (The first version set the flag with an atomic at each site: one more spilled VGPR
+// in the near pass and +2.4 % at C2.)
 __device__ __forceinline__ bool partial_wave() { return __builtin_amdgcn_read_exec() != ~0ull; }
 // The debug library only: the odd lanes stay out of claim site `site` (tests/test_claim_guard.py).
 __device__ __forceinline__ bool dbg_skip(const Params& p, uint32_t site, uint32_t lane) {
@@ -294,6 +296,7 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
     // POOL: the wave's 64 camera rays (2 float4 each) after the scene copy, and the unit's block they hold
     float4* const pool = POOL ? lds_entries + pool_f4_offset(p) + (threadIdx.x >> 6) * 128 : nullptr;
     uint32_t pool_blk = 0xFFFFFFFFu;
+    bool kerr = false;  // a claim site found a partial wave (partial_wave): flagged once the wave ends
 
     uint32_t mode = M_CLAIM, seg = 0, items_done = 0;
     size_t pix = 0;  // the lane's item in the tile-major scratch: 64 * tile + pixel within the tile
@@ -323,8 +326,8 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
         const uint64_t fm = ballot(far);
         if (fm == 0) return;
         if (dbg_skip(p, 1u, lane)) return;  // (debug library: the even lanes reach the claim alone)
-        if (partial_wave()) {  // no claim without the whole wave: the render fails (KERR_PARTIAL_WAVE)
-            atomicOr(p.error_flag, KERR_PARTIAL_WAVE);
+        if (partial_wave()) {  // no claim without the whole wave: the paths are dropped, the render fails
+            kerr = true;
             if (far) mode = M_CLAIM;
             return;
         }
@@ -352,7 +355,7 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
         if (om == 0) return;
         if (dbg_skip(p, 2u, lane)) return;
         if (partial_wave()) {
-            atomicOr(p.error_flag, KERR_PARTIAL_WAVE);
+            kerr = true;
             return;
         }
         uint32_t b2 = 0;
@@ -379,13 +382,11 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
         // Watchdog (RTX_WATCHDOG_S): a wave never outlives p.watchdog_ticks, so a bug cannot
         // keep the GPU busy forever; the render then fails with RTX_ERR_HIP (collect_on).
         // The loop is wave-uniform, so is this test.
-        // A wave also stops once any wave has flagged the render (KERR_*): the output is invalid.
         if ((++iter & 255u) == 0) {
             if (__builtin_amdgcn_s_memrealtime() - t_start > p.watchdog_ticks) {
                 if (lane == 0) atomicOr(p.error_flag, KERR_WATCHDOG);
                 break;
             }
-            if (__builtin_amdgcn_readfirstlane(*(volatile uint32_t*)p.error_flag) != 0u) break;
         }
         if (TIME) clk = __builtin_amdgcn_s_memtime();
         // primitive batching only for a scene in LDS: a lane that waits re-reads its entry, which
@@ -402,6 +403,21 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
         if (ballot(mode != M_DONE) == 0) break;
 
         // ---- shading phase ----------------------------------------------------------
+        // POOL: a MISS PHASE instead when fewer than p.refill_hits of the waiting lanes hit something: only
+        // the paths that ended on the background finish (ray.go:52: their colour stored) and take new items,
+        // whose camera rays the pool already holds; the lanes waiting on a hit stay parked and the walk goes
+        // on.  The full phase then shades more hits at once (its Philox evaluations and scatter are paid per
+        // phase).  The same operations per path, so the same bits.
+        // (The lanes a miss phase leaves parked on a hit wait as M_START, which the walk treats as waiting and
+        // the phase's shading skips; they are M_SHADE again at the next phase.)
+        bool mini = false;
+        if constexpr (POOL) {
+            if (mode == M_START) mode = M_SHADE;
+            const uint64_t wait = ballot(mode == M_SHADE), miss = ballot(mode == M_SHADE && t.hit < 0);
+            mini = miss != 0 && (uint32_t)__popcll(wait & ~miss) < p.refill_hits;
+            if (mini && mode == M_SHADE && t.hit >= 0) mode = M_START;
+        }
+        bool ready = false;
         if constexpr (TIER == 1) {
             // The near walk's closest hit is the guarded walk's when the hit sphere's own box (inside
             // its reference leaf's) passes with the bound just past the hit; else the
@@ -412,11 +428,13 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
             if (COUNT && bad) --cnt.segments;  // the far pass walks the segment again and counts it
             defer(bad);
         }
-        U4 b0{0u, 0u, 0u, 0u};
-        if (mode == M_SHADE && t.hit >= 0) b0 = rng.block(seg + 1, 0u);
-        const Scatter sc = coop_scatter<QUADS>(p, E, rng, seg + 1, mode == M_SHADE ? t.hit : -1, b0);
+        Scatter sc{v3(0.0f, 0.0f, 0.0f), 0u, 0u};
+        if (!mini) {  // (a miss phase draws nothing)
+            U4 b0{0u, 0u, 0u, 0u};
+            if (mode == M_SHADE && t.hit >= 0) b0 = rng.block(seg + 1, 0u);
+            sc = coop_scatter<QUADS>(p, E, rng, seg + 1, mode == M_SHADE ? t.hit : -1, b0);
+        }
         if (TIME) split_clk(split[0], clk);
-        bool ready = false;
         if (mode == M_SHADE) {
             V3 color;
             bool done = shade<COUNT, QUADS, NOISE>(p, E, t, seg, r, thr, acc, rng, cnt, color, &sc);
@@ -442,10 +460,13 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
             if (cursor >= u_items && !exhausted && dbg_skip(p, 3u, lane)) {
                 exhausted = true;  // (debug library: the even lanes reach the claim alone)
             } else if (cursor >= u_items && !exhausted) {  // claim the next unit (wave-uniform)
-                uint32_t un = 0xFFFFFFFFu;  // a partial wave claims nothing: exhausted, the render flagged
-                if (partial_wave()) atomicOr(p.error_flag, KERR_PARTIAL_WAVE);
-                else if (lane == 0) un = atomicAdd(p.tile_counter, 1u);
-                const uint32_t uu = __builtin_amdgcn_readfirstlane(un);  // the whole wave is here: lane 0's
+                uint32_t un = 0;
+                if (lane == 0) un = atomicAdd(p.tile_counter, 1u);
+                uint32_t uu = __builtin_amdgcn_readfirstlane(un);  // the whole wave is here: lane 0's
+                if (partial_wave()) {  // else: the wave stops (exhausted) and the render fails
+                    kerr = true;
+                    uu = 0xFFFFFFFFu;
+                }
                 exhausted = uu >= n_units;
                 if (!exhausted && (TIER == 2 || listed)) {
                     u_k0 = 64u * uu;  // the unit's first record / listed sample
@@ -559,6 +580,7 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
         }
         if (TIME) split_clk(split[3], clk);
     }
+    if (kerr) atomicOr(p.error_flag, KERR_PARTIAL_WAVE);
     if (COUNT) {
         flush_counters(p, items_done, cnt);
         if (lane == 0) {
@@ -666,16 +688,19 @@ hipError_t resident_grid(const void* kern, int block, size_t shmem, int* per_cu,
 
 // v3: chunks of p.kn samples (the scratch holds one chunk), each rendered by a
 // resident-capacity grid of render_items and summed into p.out by reduce_samples.
-template <bool COUNT, bool QUADS, bool NOISE, int WAVES = 8, int MINW = 0, bool CLK = false>
+// POOL (a scene in the LDS copy, the timed kernel): the camera-ray pool after the scene copy (render_items<POOL>).
+template <bool COUNT, bool QUADS, bool NOISE, int WAVES = 8, int MINW = 0, bool CLK = false, bool POOL = false>
 hipError_t launch_items(Params p, bool use_lds, hipStream_t stream) {
     // a scene too big for LDS: its top levels (p.n_hot entries) cached in LDS when the
     // device layout stored them first (RTX_HOT_ENTRIES=0 turns that off)
     const bool hyb = !use_lds && p.n_hot > 0 && !NOISE;
-    const size_t shmem = use_lds ? lds_fixed_bytes(p.n_entries, p.n_quads, p.n_materials, p.n_textures)
-                                 : (hyb ? lds_hot_bytes(p.n_hot) : 0);
-    const auto kern = use_lds ? render_items<COUNT, true, QUADS, NOISE, WAVES, MINW, false, CLK>
-                              : (hyb ? render_items<COUNT, false, QUADS, NOISE, WAVES, MINW, !NOISE, CLK>
-                                     : render_items<COUNT, false, QUADS, NOISE, WAVES, MINW, false, CLK>);
+    const size_t shmem = POOL ? (size_t)pool_f4_offset(p) * 16 + WAVES * POOL_BYTES_PER_WAVE
+                              : use_lds ? lds_fixed_bytes(p.n_entries, p.n_quads, p.n_materials, p.n_textures)
+                                        : (hyb ? lds_hot_bytes(p.n_hot) : 0);
+    const auto kern = POOL      ? render_items<COUNT, true, QUADS, NOISE, WAVES, MINW, false, CLK, 0, POOL>
+                      : use_lds ? render_items<COUNT, true, QUADS, NOISE, WAVES, MINW, false, CLK>
+                                : (hyb ? render_items<COUNT, false, QUADS, NOISE, WAVES, MINW, !NOISE, CLK>
+                                       : render_items<COUNT, false, QUADS, NOISE, WAVES, MINW, false, CLK>);
     constexpr int block = 64 * WAVES;
     int cus = 0, per_cu = 0;
     hipError_t e = resident_grid((const void*)kern, block, shmem, &per_cu, &cus);
@@ -795,6 +820,10 @@ hipError_t launch_items_for(const Params& p, bool use_lds, hipStream_t stream) {
     if (!use_lds && p.n_hot > HOT_ENTRIES_8W)  // an LDS cache past a third of the CU: 12-wave workgroups, two per CU
         return p.n_quads ? launch_items<COUNT, true, false, RTX_HYB_WAVES, COUNT ? 0 : RTX_HYB_MINW>(p, use_lds, stream)
                          : launch_items<COUNT, false, false, RTX_HYB_WAVES, COUNT ? 0 : RTX_HYB_MINW>(p, use_lds, stream);
+    if constexpr (!COUNT)  // the camera-ray pool (12-wave workgroups, two per CU) when the scene copy leaves room
+        if (use_lds && pool_fits(p))
+            return p.n_quads ? launch_items<false, true, false, 12, RTX_V3_MINW, false, true>(p, use_lds, stream)
+                             : launch_items<false, false, false, 12, RTX_V3_MINW, false, true>(p, use_lds, stream);
     return p.n_quads ? launch_items<COUNT, true, false, RTX_V3_WAVES, COUNT ? 0 : RTX_V3_MINW>(p, use_lds, stream)
                      : launch_items<COUNT, false, false, RTX_V3_WAVES, COUNT ? 0 : RTX_V3_MINW>(p, use_lds, stream);
 }
