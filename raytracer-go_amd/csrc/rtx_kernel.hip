@@ -54,7 +54,10 @@ namespace rtxd {
 // (KERR_PARTIAL_WAVE -> RTX_ERR_HIP), and the render fails loudly instead of hanging or returning a
 // corrupt frame.  (The first version set the flag with an atomic at each site: one more spilled VGPR
 // in the near pass and +2.4 % at C2.)
-__device__ __forceinline__ bool partial_wave() { return __builtin_amdgcn_read_exec() != ~0ull; }
+#ifndef RTX_CLAIM_GUARD  // 0: the guard compiled out (A/B of its cost only)
+#define RTX_CLAIM_GUARD 1
+#endif
+__device__ __forceinline__ bool partial_wave() { return RTX_CLAIM_GUARD && __builtin_amdgcn_read_exec() != ~0ull; }
 // The debug library only: the odd lanes stay out of claim site `site` (tests/test_claim_guard.py).
 __device__ __forceinline__ bool dbg_skip(const Params& p, uint32_t site, uint32_t lane) {
     return RTX_DEBUG_PARTIAL && p.debug_partial == site && (lane & 1u);
