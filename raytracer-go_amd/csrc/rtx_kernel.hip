@@ -57,6 +57,9 @@ namespace rtxd {
 #ifndef RTX_CLAIM_GUARD  // 0: the guard compiled out (A/B of its cost only)
 #define RTX_CLAIM_GUARD 1
 #endif
+#ifndef RTX_KERR_ITER  // 1: the guard's flag in bit 31 of the loop counter instead of its own SGPR (A/B)
+#define RTX_KERR_ITER 0
+#endif
 __device__ __forceinline__ bool partial_wave() { return RTX_CLAIM_GUARD && __builtin_amdgcn_read_exec() != ~0ull; }
 // The debug library only: the odd lanes stay out of claim site `site` (tests/test_claim_guard.py).
 __device__ __forceinline__ bool dbg_skip(const Params& p, uint32_t site, uint32_t lane) {
@@ -299,7 +302,15 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
     // POOL: the wave's 64 camera rays (2 float4 each) after the scene copy, and the unit's block they hold
     float4* const pool = POOL ? lds_entries + pool_f4_offset(p) + (threadIdx.x >> 6) * 128 : nullptr;
     uint32_t pool_blk = 0xFFFFFFFFu;
+#if RTX_KERR_ITER
+    uint32_t iter = 0;  // main-loop iterations (the watchdog's clock); bit 31: a claim site found a partial wave
+#define RTX_SET_KERR() (iter |= 0x80000000u)
+#define RTX_KERR() ((iter & 0x80000000u) != 0u)
+#else
     bool kerr = false;  // a claim site found a partial wave (partial_wave): flagged once the wave ends
+#define RTX_SET_KERR() (kerr = true)
+#define RTX_KERR() kerr
+#endif
 
     uint32_t mode = M_CLAIM, seg = 0, items_done = 0;
     size_t pix = 0;  // the lane's item in the tile-major scratch: 64 * tile + pixel within the tile
@@ -330,7 +341,7 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
         if (fm == 0) return;
         if (dbg_skip(p, 1u, lane)) return;  // (debug library: the even lanes reach the claim alone)
         if (partial_wave()) {  // no claim without the whole wave: the paths are dropped, the render fails
-            kerr = true;
+            RTX_SET_KERR();
             if (far) mode = M_CLAIM;
             return;
         }
@@ -358,7 +369,7 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
         if (om == 0) return;
         if (dbg_skip(p, 2u, lane)) return;
         if (partial_wave()) {
-            kerr = true;
+            RTX_SET_KERR();
             return;
         }
         uint32_t b2 = 0;
@@ -380,7 +391,9 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
     };
 
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+#if !RTX_KERR_ITER
     uint32_t iter = 0;
+#endif
     for (;;) {
         // Watchdog (RTX_WATCHDOG_S): a wave never outlives p.watchdog_ticks, so a bug cannot
         // keep the GPU busy forever; the render then fails with RTX_ERR_HIP (collect_on).
@@ -467,7 +480,7 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
                 if (lane == 0) un = atomicAdd(p.tile_counter, 1u);
                 uint32_t uu = __builtin_amdgcn_readfirstlane(un);  // the whole wave is here: lane 0's
                 if (partial_wave()) {  // else: the wave stops (exhausted) and the render fails
-                    kerr = true;
+                    RTX_SET_KERR();
                     uu = 0xFFFFFFFFu;
                 }
                 exhausted = uu >= n_units;
@@ -583,7 +596,9 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
         }
         if (TIME) split_clk(split[3], clk);
     }
-    if (kerr) atomicOr(p.error_flag, KERR_PARTIAL_WAVE);
+    if (RTX_KERR()) atomicOr(p.error_flag, KERR_PARTIAL_WAVE);
+#undef RTX_SET_KERR
+#undef RTX_KERR
     if (COUNT) {
         flush_counters(p, items_done, cnt);
         if (lane == 0) {
