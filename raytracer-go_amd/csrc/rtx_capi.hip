@@ -954,7 +954,7 @@ int enqueue_on(rtx_scene* s, DeviceCopy* c, const rtx_camera* cam, uint64_t seed
         if (tier && p.sub > 64) p.sub = 64;
         p.debug_partial = env_knob("RTX_DEBUG_PARTIAL_SITE", 0, 0, 3);  // (read by librtx_dbgclaim.so only)
         p.cam_pool = env_knob("RTX_CAM_POOL", 1, 0, 1);  // the near pass's camera-ray pool (A/B: 0 = off)
-        p.refill_hits = env_knob("RTX_REFILL_HITS", 0, 0, 64);  // its miss phases (A/B)
+        p.refill_hits = env_knob("RTX_REFILL_HITS", 0, 0, 64);  // its miss phases (untiered: off by default)
         p.item_waves = env_knob("RTX_ITEM_WAVES", 8, 4, 8) >= 8 ? 8u : 4u;
         p.grid_pct = env_knob("RTX_ITEM_GRID", 100, 1, 100);
         p.debug_launch = env_knob("RTX_DEBUG_LAUNCH", 0, 0, 1);
@@ -1009,7 +1009,12 @@ int enqueue_on(rtx_scene* s, DeviceCopy* c, const rtx_camera* cam, uint64_t seed
             // the near pass's walk is cheaper: it shades in larger batches and tests primitives in
             // smaller ones (C2 at 100 spp: 56 / 12 lanes 23.15 ms, 48 / 16 23.49 ms; the far pass keeps
             // the defaults), unless RTX_SHADE_THRESH / RTX_SHADE_THRESH(n) / RTX_PRIM_BATCH say otherwise
-            if (!th && !std::getenv("RTX_SHADE_THRESH")) pn.shade_thresh = 56;
+            // With the camera-ray pool and its miss phases the near pass shades at 52 waiting lanes
+            // and takes a miss phase when fewer than 36 of them hit (C2: 90.9 ms against 91.8 at 56 / 36, 92.2 at
+            // 52 / 40; profiles/r05_refill_sweep.jsonl)
+            const bool pooled = rtxd::tier_placement(pn, p, flags) == RTX_SCENE_IN_LDS && rtxd::pool_fits(pn);
+            if (!th && !std::getenv("RTX_SHADE_THRESH")) pn.shade_thresh = pooled ? 52 : 56;
+            if (!std::getenv("RTX_REFILL_HITS")) pn.refill_hits = 36;
             if (!std::getenv("RTX_PRIM_BATCH")) pn.prim_batch = 12;
             pn.defer = p.defer = scr->defer;
             pn.redo_bits = p.redo_bits = scr->redo;

@@ -498,6 +498,11 @@ constexpr uint32_t POOL_BYTES_PER_WAVE = 64 * 32;
 __host__ __device__ __forceinline__ uint32_t pool_f4_offset(const Params& p) {
     return (lds_fixed_bytes(p.n_entries, p.n_quads, p.n_materials, p.n_textures) + 15u) / 16u;
 }
+// Whether a render of a scene in the LDS copy takes the camera-ray pool: wanted (Params::cam_pool) and two
+// 12-wave workgroups' scene copies and pools fit a CU's 160 KB.
+__host__ __device__ __forceinline__ bool pool_fits(const Params& p) {
+    return p.cam_pool && (size_t)pool_f4_offset(p) * 16 + 12 * POOL_BYTES_PER_WAVE <= 80u * 1024u;
+}
 
 // Error bits of *Params::error_flag (rtx_capi.hip collect_on turns them into RTX_ERR_HIP).
 constexpr uint32_t KERR_WATCHDOG = 1u;      // a wave outlived RTX_WATCHDOG_S

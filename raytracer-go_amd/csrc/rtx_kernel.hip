@@ -48,17 +48,14 @@ namespace rtxd {
 // active: without lane 0 no atomic is issued and every lane reads the first active lane's stale
 // value (slot 0, unit 0: colliding records and a unit rendered again and again — the hang of the
 // round-4 early-claim refactor), and with lane 0 the absent lanes would claim on
-// their own later.  Each site therefore checks EXEC first, on SALU only (s_cmp + s_cselect on a copy
-// of exec into a uniform flag, no VGPR in the hot loop): a partial wave claims nothing (a unit claim
-// leaves the wave exhausted, a queue claim drops its paths), the wave flags the render when it ends
-// (KERR_PARTIAL_WAVE -> RTX_ERR_HIP), and the render fails loudly instead of hanging or returning a
-// corrupt frame.  (The first version set the flag with an atomic at each site: one more spilled VGPR
+// their own later.  Each site therefore checks EXEC first, on SALU only (s_cmp on a copy of exec, a
+// bit of the loop counter as the flag, no VGPR in the hot loop): a partial wave claims nothing (a unit
+// claim leaves the wave exhausted, a queue claim drops its paths), the wave flags the render when it
+// ends (KERR_PARTIAL_WAVE -> RTX_ERR_HIP), and the render fails loudly instead of hanging or returning
+// a corrupt frame.  (The first version set the flag with an atomic at each site: one more spilled VGPR
 // in the near pass and +2.4 % at C2.)
 #ifndef RTX_CLAIM_GUARD  // 0: the guard compiled out (A/B of its cost only)
 #define RTX_CLAIM_GUARD 1
-#endif
-#ifndef RTX_KERR_ITER  // 1: the guard's flag in bit 31 of the loop counter instead of its own SGPR (A/B)
-#define RTX_KERR_ITER 0
 #endif
 __device__ __forceinline__ bool partial_wave() { return RTX_CLAIM_GUARD && __builtin_amdgcn_read_exec() != ~0ull; }
 // The debug library only: the odd lanes stay out of claim site `site` (tests/test_claim_guard.py).
@@ -231,7 +228,7 @@ template <bool COUNT, bool USE_LDS, bool QUADS, bool NOISE, int WAVES = 8, int M
           bool CLK = false, int TIER = 0, bool POOL = false>
 __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
     constexpr bool TIME = COUNT || CLK;
-    static_assert(!POOL || (USE_LDS && !COUNT && (TIER == 0 || TIER == 1)), "the camera-ray pool: timed, LDS scenes");
+    static_assert(!POOL || (USE_LDS && (TIER == 0 || TIER == 1)), "the camera-ray pool: LDS scenes, near pass or one walk");
     if constexpr (TIER == 3) {
         if (__builtin_amdgcn_readfirstlane(*(volatile uint32_t*)p.redo_count) == 0u) return;
         if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&p.counters[24], 1ull);  // chunks with a redo
@@ -302,15 +299,12 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
     // POOL: the wave's 64 camera rays (2 float4 each) after the scene copy, and the unit's block they hold
     float4* const pool = POOL ? lds_entries + pool_f4_offset(p) + (threadIdx.x >> 6) * 128 : nullptr;
     uint32_t pool_blk = 0xFFFFFFFFu;
-#if RTX_KERR_ITER
-    uint32_t iter = 0;  // main-loop iterations (the watchdog's clock); bit 31: a claim site found a partial wave
+    // main-loop iterations (the watchdog's clock); bit 31: a claim site found a partial wave (partial_wave),
+    // flagged once the wave ends.  (A bool of its own cost 0.6 % at C2, this bit 0.2 %: one SGPR fewer
+    // live through the walk; profiles/r05_guard_ab.jsonl.)
+    uint32_t iter = 0;
 #define RTX_SET_KERR() (iter |= 0x80000000u)
 #define RTX_KERR() ((iter & 0x80000000u) != 0u)
-#else
-    bool kerr = false;  // a claim site found a partial wave (partial_wave): flagged once the wave ends
-#define RTX_SET_KERR() (kerr = true)
-#define RTX_KERR() kerr
-#endif
 
     uint32_t mode = M_CLAIM, seg = 0, items_done = 0;
     size_t pix = 0;  // the lane's item in the tile-major scratch: 64 * tile + pixel within the tile
@@ -391,9 +385,6 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
     };
 
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
-#if !RTX_KERR_ITER
-    uint32_t iter = 0;
-#endif
     for (;;) {
         // Watchdog (RTX_WATCHDOG_S): a wave never outlives p.watchdog_ticks, so a bug cannot
         // keep the GPU busy forever; the render then fails with RTX_ERR_HIP (collect_on).
@@ -517,8 +508,8 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
                         const uint32_t x = p.x0 + lx, y = p.y0 + p.rank + lr * p.world;
                         const PathRng cr{rng.k0, rng.k1, y * c.image_width + x, u_k0 + blk};
                         uint32_t dr = 0;
-                        const Ray cray = camera_ray<true>(c, pixel_base(c, x, y), cr, cr.block(0u, 0u), dr);
-                        pool[2 * lane] = make_float4(cray.o.x, cray.o.y, cray.o.z, 0.0f);
+                        const Ray cray = camera_ray<!COUNT>(c, pixel_base(c, x, y), cr, cr.block(0u, 0u), dr);
+                        pool[2 * lane] = make_float4(cray.o.x, cray.o.y, cray.o.z, __uint_as_float(dr));  // (COUNT: draws)
                         pool[2 * lane + 1] = make_float4(cray.d.x, cray.d.y, cray.d.z, 0.0f);
                     }
                     __builtin_amdgcn_wave_barrier();  // (LDS is in order within the wave)
@@ -527,6 +518,7 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
             }
             const uint32_t rank = (uint32_t)__popcll(wm & ((1ull << lane) - 1ull));
             bool got = false;
+            uint32_t pool_draws = 0;  // COUNT, POOL: the draws of the ray the lane takes
             if (TIER == 2 && mode == M_CLAIM && rank < avail) {  // resume a record
                 const float4* q = p.defer + 4 * (size_t)(u_k0 + cursor + rank);
                 const float4 q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3];
@@ -562,6 +554,7 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
                     if constexpr (POOL) {  // the ray the wave drew for this item (l: the pixel of the block)
                         const float4 po = pool[2 * l], pd = pool[2 * l + 1];
                         r = Ray{v3(po.x, po.y, po.z), v3(pd.x, pd.y, pd.z)};
+                        if (COUNT) pool_draws = __float_as_uint(po.w);
                     } else {
                         base = pixel_base(c, x, y);
                     }
@@ -576,6 +569,7 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
             if (got) {
                 if (COUNT && TIER == 1) path0 = cnt;
                 if constexpr (!POOL) r = camera_ray<!COUNT>(c, base, rng, rng.block(0u, 0u), cnt.draws);  // GetRay, camera.go:257
+                else if (COUNT) cnt.draws += pool_draws;  // the camera ray's draws, counted by its own lane
                 thr = v3(1.0f, 1.0f, 1.0f);
                 acc = v3(0.0f, 0.0f, 0.0f);
                 seg = 0;
@@ -812,12 +806,6 @@ hipError_t launch_tiered(Params pn, Params pf, hipStream_t stream) {
     return hipSuccess;
 }
 
-// Whether the near pass of a tiered LDS render takes the camera-ray pool: wanted (Params::cam_pool) and two
-// 12-wave workgroups' scene copies and pools fit a CU's 160 KB.
-inline bool pool_fits(const Params& p) {
-    return p.cam_pool && (size_t)pool_f4_offset(p) * 16 + 12 * POOL_BYTES_PER_WAVE <= 80u * 1024u;
-}
-
 #ifndef RTX_HYB_WAVES  // the same for scenes in HBM with an 80 KB LDS cache of their most-read entries
 #define RTX_HYB_WAVES 12
 #define RTX_HYB_MINW 6
@@ -838,10 +826,9 @@ hipError_t launch_items_for(const Params& p, bool use_lds, hipStream_t stream) {
     if (!use_lds && p.n_hot > HOT_ENTRIES_8W)  // an LDS cache past a third of the CU: 12-wave workgroups, two per CU
         return p.n_quads ? launch_items<COUNT, true, false, RTX_HYB_WAVES, COUNT ? 0 : RTX_HYB_MINW>(p, use_lds, stream)
                          : launch_items<COUNT, false, false, RTX_HYB_WAVES, COUNT ? 0 : RTX_HYB_MINW>(p, use_lds, stream);
-    if constexpr (!COUNT)  // the camera-ray pool (12-wave workgroups, two per CU) when the scene copy leaves room
-        if (use_lds && pool_fits(p))
-            return p.n_quads ? launch_items<false, true, false, 12, RTX_V3_MINW, false, true>(p, use_lds, stream)
-                             : launch_items<false, false, false, 12, RTX_V3_MINW, false, true>(p, use_lds, stream);
+    if (use_lds && pool_fits(p))  // the camera-ray pool (12-wave workgroups, two per CU) when the scene copy leaves room
+        return p.n_quads ? launch_items<COUNT, true, false, 12, COUNT ? 0 : RTX_V3_MINW, false, true>(p, use_lds, stream)
+                         : launch_items<COUNT, false, false, 12, COUNT ? 0 : RTX_V3_MINW, false, true>(p, use_lds, stream);
     return p.n_quads ? launch_items<COUNT, true, false, RTX_V3_WAVES, COUNT ? 0 : RTX_V3_MINW>(p, use_lds, stream)
                      : launch_items<COUNT, false, false, RTX_V3_WAVES, COUNT ? 0 : RTX_V3_MINW>(p, use_lds, stream);
 }
@@ -870,10 +857,11 @@ hipError_t launch_render(const Params& p, uint32_t flags, hipStream_t stream, co
             return hipErrorInvalidValue;
         const bool clk = !count && (flags & RTX_FLAG_TIMING);  // diagnostics: the wave-cycle split of the passes
         if (place == RTX_SCENE_IN_LDS) {
-            const bool pool = pool_fits(p);  // (the counting kernel keeps its own camera rays: it counts their draws)
+            const bool pool = pool_fits(p);  // (the counting kernel too: its schedule counters are the timed kernel's)
             if (clk) return pool ? launch_tiered<false, RTX_V3_WAVES, RTX_V3_MINW, true, true, false, true>(p, *far, stream)
                                  : launch_tiered<false, RTX_V3_WAVES, RTX_V3_MINW, true>(p, *far, stream);
-            if (count) return launch_tiered<true, RTX_V3_WAVES, 0>(p, *far, stream);
+            if (count) return pool ? launch_tiered<true, RTX_V3_WAVES, 0, false, true, false, true>(p, *far, stream)
+                                   : launch_tiered<true, RTX_V3_WAVES, 0>(p, *far, stream);
             return pool ? launch_tiered<false, RTX_V3_WAVES, RTX_V3_MINW, false, true, false, true>(p, *far, stream)
                         : launch_tiered<false, RTX_V3_WAVES, RTX_V3_MINW>(p, *far, stream);
         }
