@@ -3,6 +3,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 
 namespace rtxd {
@@ -272,9 +273,21 @@ bool near_region(const std::vector<rtx_entry>& ref, float box[6], double grow) {
 // rho + 11u D + 7u rho of it; the slab test of the grown box passes it with 3u (D + r + m) to spare,
 // and its FMA form (fma(b, 1/d, -(o/d)), the near walk's: §15.5) with 2u (D + r + m) + u omax, omax
 // bounding the origin's coordinates.
+// RTX_MARGIN_K (read once; default 24, the derived constant; at least 24) widens the bound's K u (D^2 + r^2) for
+// A/B and as a safety factor a caller may want on scenes far from the tested ones (tests/test_tier.py measures
+// K <= 8.3 on every adversarial set).
+static double margin_k() {
+    static const double k = [] {
+        const char* e = std::getenv("RTX_MARGIN_K");
+        const double v = e ? std::strtod(e, nullptr) : 24.0;
+        return v >= 24.0 && std::isfinite(v) ? v : 24.0;
+    }();
+    return k;
+}
+
 double sphere_margin(double r, double dmax, double omax) {
-    const double rho = std::sqrt(r * r + 3.0 * std::ldexp(dmax * dmax + r * r, -21));  // 24u = 3 * 2^-21
-    return rho - r + std::ldexp(dmax + rho, -20) + std::ldexp(omax, -23);              // + 16u (D + rho) + 2u omax
+    const double rho = std::sqrt(r * r + std::ldexp(margin_k() * (dmax * dmax + r * r), -24));  // K u, u = 2^-24
+    return rho - r + std::ldexp(dmax + rho, -20) + std::ldexp(omax, -23);                       // + 16u (D + rho) + 2u omax
 }
 
 bool build_topology(const std::vector<rtx_entry>& ref, bool guarded, Topology& out, const float* near_box) {

@@ -217,20 +217,30 @@ def ancestors(arr, root):
     return out
 
 
-def tangent_rays(rng, o, c, r, rel):
+def tangent_rays(rng, o, c, r, rel, dscale=(1e-2, 1e2)):
     """Rays from o aimed at a point of the sphere's silhouette as seen from o, pushed out (rel > 0) or in
-    (rel < 0) by rel * r, with direction lengths from 1e-2 to 1e2 (hittables.go does not normalise)."""
+    (rel < 0) by rel * r, with direction lengths log-uniform in dscale (hittables.go does not normalise)."""
     u = (c - o).astype(np.float64)
     u /= np.linalg.norm(u, axis=1)[:, None]
     w = rng.normal(size=u.shape)
     w -= (w * u).sum(1)[:, None] * u
     w /= np.linalg.norm(w, axis=1)[:, None]
     d = (c.astype(np.float64) + w * (r * (1.0 + rel))[:, None]) - o
-    return (d * np.exp(rng.uniform(np.log(1e-2), np.log(1e2), len(o)))[:, None]).astype(F)
+    return (d * np.exp(rng.uniform(np.log(dscale[0]), np.log(dscale[1]), len(o)))[:, None]).astype(F)
 
 
-@pytest.mark.parametrize("scene,n_spheres", [("random_spheres", 0), ("earth_dielectric", 0), ("stress_100k", 3000)])
-def test_margin_bound_adversarial(built, scene, n_spheres):
+# (scene, spheres sampled (0: all), radius scale of the non-huge spheres, direction lengths): the BASELINE scenes
+# with directions of length 1e-2 .. 1e2; randSpheres with radii x 0.01 (r = 2e-3 .. 1e-2 against D up to ~80: the
+# margin is then ~40 radii) and with directions from 1e-8 to 1e8 (|1/d| up to 1e8 and |d|^2 down to 1e-16, the
+# ends of Trav::safe's [2^-60, 2^60] and of near_fma_ok's |1/d| <= 2^64: the FMA form's products at their largest)
+ADVERSARIAL = [("random_spheres", 0, 1.0, (1e-2, 1e2)), ("earth_dielectric", 0, 1.0, (1e-2, 1e2)),
+               ("stress_100k", 3000, 1.0, (1e-2, 1e2)), ("random_spheres", 0, 0.01, (1e-2, 1e2)),
+               ("random_spheres", 0, 1.0, (1e-8, 1e8))]
+
+
+@pytest.mark.parametrize("scene,n_spheres,rscale,dscale", ADVERSARIAL,
+                         ids=["random_spheres", "earth_dielectric", "stress_100k", "tiny_radii", "extreme_dirs"])
+def test_margin_bound_adversarial(built, scene, n_spheres, rscale, dscale):
     """The forward-error bound behind sphere_margin, adversarially: from the near region's
     8 corners, its 6 face centres and random points in it, near-tangent rays (silhouette offsets of
     1e-7 .. 1e-1 of the radius, inside and out) at every sphere of the scene (a seeded sample of config 4's
@@ -241,9 +251,17 @@ def test_margin_bound_adversarial(built, scene, n_spheres):
     stays below the 24 the margin assumes."""
     s = rtx.HostScene(scene, 1)
     cam = s.camera(width=96, spp=2)
+    if rscale != 1.0:  # shrink every non-huge sphere in place: the caller's node boxes still contain them
+        dd = s.desc.contents
+        for i in range(dd.n_spheres):
+            if abs(dd.spheres[i].radius) < 10:
+                dd.spheres[i].radius = float(F(dd.spheres[i].radius) * F(rscale))
     box, active = rtx.walk_near_region(s.desc, cam)
-    assert active
+    # (tiny radii fail the rebuild's precision gate: the region is then the core box grown by 1 %, the camera
+    # outside it; the near tree and its margins are still built, and the bound is about them)
+    assert box is not None and (active or rscale != 1.0)
     arr, root = near_tree(s.desc, cam)
+    assert arr is not None
     anc = ancestors(arr, root)
     c_all, r_all = spheres_of(s.desc)
     bmin = np.array([list(arr[i].bmin) for i in range(len(arr))], F)
@@ -265,7 +283,7 @@ def test_margin_bound_adversarial(built, scene, n_spheres):
         rel = np.tile(rels, len(sph)) * rng.uniform(0.5, 2.0, len(j))
         o = np.repeat(origins[oi:oi + 1], len(j), axis=0)
         cj, rj = c_all[j], np.abs(r_all[j])
-        d = tangent_rays(rng, o, cj, rj.astype(np.float64), rel)
+        d = tangent_rays(rng, o, cj, rj.astype(np.float64), rel, dscale)
         t = sphere_t(o, d, cj, rj)
         hit = ~np.isnan(t)
         n_hits += int(hit.sum())
