@@ -18,6 +18,7 @@ ab() {
   timeout -k 10 240 env "$@" > "$OUT/$log" 2>&1 || { tail -5 "$OUT/$log"; exit 1; }
   echo "== $log"; grep "median\|sha256\|trav-lane" "$OUT/$log" | head -6
 }
+ab knobs.log python scripts/ab.py --spp 500 --rounds 3 --variants "v3,v3@RTX_ITEM_SUB=8,v3@RTX_ITEM_SUB=32,v3@RTX_PRIM_BATCH=8,v3@RTX_PRIM_BATCH=16,v3@RTX_REFILL_HITS=34,v3@RTX_REFILL_HITS=38"
 for sc in "--spp 500" "--scene stress_100k --spp 100" "--width 400 --spp 100 --rounds 5" "--scene cornell_box --width 600 --spp 200"; do
   ab cur.log python scripts/ab.py $sc --variants v3
   ab r04.log RTX_LIB=$PWD/abl/librtx_r04.so python scripts/ab.py $sc --variants v3
