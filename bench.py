@@ -52,9 +52,9 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0, help="0: the host's CPU share per GPU")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-hash", action="store_true", help="skip the framebuffer hash")
-    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_r04.jsonl"),
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_r05.jsonl"),
                     help="PMC HBM-traffic summaries (scripts/pmc_traffic.py): a .json, or a .jsonl of one per workload")
-    ap.add_argument("--valu", default=os.path.join(ROOT, "profiles", "valu_r04.jsonl"),
+    ap.add_argument("--valu", default=os.path.join(ROOT, "profiles", "valu_r05.jsonl"),
                     help="PMC VALU summaries (scripts/pmc_valu.py): a .json, or a .jsonl of one per workload")
     ap.add_argument("--shard", default="", help="R/N: one process renders only rank R's rows of N (a rank's "
                     "workload of the N-GPU run, for its PMC profile); not a scaling number")
