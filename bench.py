@@ -56,6 +56,8 @@ def parse():
                     help="PMC HBM-traffic summaries (scripts/pmc_traffic.py): a .json, or a .jsonl of one per workload")
     ap.add_argument("--valu", default=os.path.join(ROOT, "profiles", "valu_r05.jsonl"),
                     help="PMC VALU summaries (scripts/pmc_valu.py): a .json, or a .jsonl of one per workload")
+    ap.add_argument("--stripe", type=int, default=0, help="rows per stripe of the shards (0: 8 for N > 1, 1 for N = 1; "
+                    "1 interleaves single rows, the round-4 layout)")
     ap.add_argument("--shard", default="", help="R/N: one process renders only rank R's rows of N (a rank's "
                     "workload of the N-GPU run, for its PMC profile); not a scaling number")
     ap.add_argument("--in-process", action="store_true",
@@ -342,8 +344,9 @@ def main():
     srank, sworld = (int(v) for v in args.shard.split("/")) if args.shard else (rank, world)
     if world > 1 and args.shard:
         raise SystemExit("--shard is a one-process run")
-    reg = rtx.Region(0, 0, W, H, srank, sworld)
-    R = max_shard_rows(H, sworld)
+    stripe = args.stripe if args.stripe > 0 else (8 if sworld > 1 else 1)  # 8-row stripes
+    reg = rtx.Region(0, 0, W, H, srank, sworld, stripe)
+    R = max_shard_rows(H, sworld, stripe)
     shard = torch.zeros((R, W, 3), dtype=torch.float32, device="cuda")
     stream = torch.cuda.current_stream().cuda_stream
 
@@ -366,7 +369,7 @@ def main():
         times.append(s.kernel_ms)
         g0 = time.perf_counter()  # (render_region waited for this rank's kernel)
         out = shard[:rtx.region_rows(reg)] if args.shard else gather_image(shard.cpu() if shared else shard, H, rank,
-                                                                                world)
+                                                                                world, stripe=stripe)
         if world > 1 and out is not None and not shared:
             torch.cuda.synchronize()
         gathers.append((time.perf_counter() - g0) * 1e3)
@@ -410,7 +413,8 @@ def main():
             metric = f"shard {srank}/{sworld} alone (rank {srank}'s rows of an {sworld}-GPU run; not a scaling number); " + metric
         # the PMC profile of this process's own workload: the frame, or its rank's rows of an N-way run
         # (profiled alone with --shard R/N)
-        profile_workload = f"{args.scene}:{W}x{H}x{S}" + (f"/rows{srank}of{sworld}" if sworld > 1 else "")
+        profile_workload = f"{args.scene}:{W}x{H}x{S}" + (f"/rows{srank}of{sworld}" if sworld > 1 else "") + (
+            f"/stripe{stripe}" if stripe > 1 else "")
         out = {
             "metric": metric,
             "value": round(mray, 3),
@@ -532,7 +536,7 @@ def main_in_process(args):
 
 
 def selftest_gloo(args, rank: int, world: int) -> None:
-    """The multi-rank plumbing of main() on the CPU: gloo process group, row-interleaved shards
+    """The multi-rank plumbing of main() on the CPU: gloo process group, striped shards
     of a width x height image (height from the scene's 16:9 aspect), each filled with its global
     pixel index instead of a render, the same gather + de-interleave, and rank 0's JSON line
     with the framebuffer hash (tests/test_bench_launcher.py recomputes it)."""
@@ -547,13 +551,14 @@ def selftest_gloo(args, rank: int, world: int) -> None:
         dist.init_process_group("gloo")
     W = args.width
     H = int(W * 9 // 16)
-    R = max_shard_rows(H, world)
+    S = args.stripe if args.stripe > 0 else (8 if world > 1 else 1)  # main()'s stripes
+    R = max_shard_rows(H, world, S)
     shard = torch.zeros((R, W, 3), dtype=torch.float32)
-    for i in range(shard_rows(H, rank, world)):
-        y = rank + i * world
+    for i in range(shard_rows(H, rank, world, S)):
+        y = ((i // S) * world + rank) * S + i % S  # rtx_region_row
         idx = torch.arange(W, dtype=torch.float32) + float(y * W)
         shard[i] = idx[:, None].expand(W, 3)
-    img = gather_image(shard, H, rank, world)
+    img = gather_image(shard, H, rank, world, stripe=S)
     if rank == 0:
         print(json.dumps({"selftest": True, "n_gpus": world, "world_size": dist.get_world_size() if world > 1 else 1,
                           "backend": "gloo" if world > 1 else None, "height": H,

@@ -197,15 +197,22 @@ typedef struct rtx_camera {
 } rtx_camera;
 
 /* ---- render region / shard ---------------------------------------------------- */
-/* Pixels x in [x0, x0+width), rows y = y0 + r for r in [0, height) with
- * r % world == rank (row-interleaved shard, so sky and ground are balanced across
- * GPUs).  Output rows are stored compacted in shard order: out[(r/world)*width + x].
- * The RNG is keyed by the GLOBAL pixel index y*image_width + x, so every pixel's
- * value is independent of the region and of the shard count.                     */
+/* Pixels x in [x0, x0+width), rows y = y0 + r for r in [0, height) whose STRIPE
+ * (r / stripe, stripes of `stripe` rows; 0 or 1: single rows) is rank modulo world:
+ * stripes dealt round-robin to the shards, so sky and ground are balanced across GPUs.
+ * Output rows are stored compacted in shard order: shard row i is image row
+ * y0 + rtx_region_row(region, i).  The RNG is keyed by the GLOBAL pixel index
+ * y*image_width + x, so every pixel's value is independent of the region, the stripe
+ * and the shard count.  ABI 9 added `stripe` (a power of two, at most 4096): 8-row
+ * stripes keep a shard's 8x8 work tiles compact in the image (rtx_render with
+ * n_gpus > 1 uses them).                                          */
 typedef struct rtx_region {
     uint32_t x0, y0, width, height;
     uint32_t rank, world;
+    uint32_t stripe;
 } rtx_region;
+
+
 
 /* Work counters of one render (filled when RTX_FLAG_COUNTERS is set).  These are
  * the units of SURVEY.md §8(d): segments = world.Hit calls (ray.go:36).          */
@@ -419,8 +426,12 @@ uint64_t rtx_device_scratch_bytes(int device);
 int rtx_render_region_device(rtx_scene* scene, const rtx_camera* cam, uint64_t seed, const rtx_region* region,
                              float* d_out, void* hip_stream, uint32_t flags, rtx_stats* stats);
 
-/* Number of output rows of a region shard: ceil((height - rank) / world). */
+/* Number of output rows of a region shard: the rows of the stripes rank, rank + world, ... that
+ * lie in [0, height) (ceil((height - rank) / world) for single-row stripes). */
 uint32_t rtx_region_rows(const rtx_region* region);
+/* ABI 9.  The row (relative to y0) of shard row i of a region: row i % S of stripe (i / S) * world + rank
+ * (S = max(stripe, 1)). */
+uint32_t rtx_region_row(const rtx_region* region, uint32_t i);
 
 /* ---- BVH build on the GPU ----------------------------------
  * rtx_scene_create for NewBVHFromWorld(world) (bvh.go:138-185) of a World holding only

@@ -1014,9 +1014,15 @@ static vec3 pixel_color(const ctx_t* cx, uint32_t i, uint32_t j) {
 /* ============================================================================
  * Region rendering, threads over rows.
  * ========================================================================== */
+/* Rows of a shard (include/rtx.h rtx_region): stripes of S rows dealt round-robin, the last one maybe partial. */
 uint32_t oracle_region_rows(const rtx_region* r) {
-    if (r->world == 0 || r->rank >= r->world || r->height <= r->rank) return 0;
-    return (r->height - r->rank + r->world - 1) / r->world;
+    if (r->world == 0 || r->rank >= r->world) return 0;
+    const uint32_t S = r->stripe > 1u ? r->stripe : 1u;
+    const uint32_t nst = (r->height + S - 1) / S;
+    if (r->rank >= nst) return 0;
+    uint32_t rows = (nst - r->rank + r->world - 1) / r->world * S;
+    if ((nst - 1) % r->world == r->rank && r->height % S) rows -= S - r->height % S;
+    return rows;
 }
 
 static int scene_supported(const rtx_scene_desc* s) {
@@ -1060,7 +1066,8 @@ static void* worker(void* arg) {
         uint32_t lr = jb->next_row++;
         pthread_mutex_unlock(&jb->mu);
         if (lr >= jb->rows) break;
-        uint32_t y = jb->reg->y0 + jb->reg->rank + lr * jb->reg->world;
+        const uint32_t S = jb->reg->stripe > 1u ? jb->reg->stripe : 1u; /* stripes dealt round-robin (rtx.h) */
+        uint32_t y = jb->reg->y0 + ((lr / S) * jb->reg->world + jb->reg->rank) * S + lr % S;
         for (uint32_t xx = 0; xx < jb->reg->width; ++xx) {
             vec3 c = pixel_color(&cx, jb->reg->x0 + xx, y);
             float* o = jb->out + ((size_t)lr * jb->reg->width + xx) * 3;

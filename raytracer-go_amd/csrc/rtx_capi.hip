@@ -819,6 +819,8 @@ int check_camera(const rtx_camera* cam) {
 int check_region(const rtx_camera* cam, const rtx_region* r) {
     if (!r) return fail(RTX_ERR_INVALID_ARG, "region is NULL");
     if (r->world == 0 || r->rank >= r->world) return fail(RTX_ERR_INVALID_ARG, "bad shard %u/%u", r->rank, r->world);
+    if (r->stripe > 4096 || (r->stripe & (r->stripe - 1)) != 0)
+        return fail(RTX_ERR_INVALID_ARG, "stripe %u: 0 or a power of two up to 4096", r->stripe);
     if ((uint64_t)r->x0 + r->width > cam->image_width || (uint64_t)r->y0 + r->height > cam->image_height)
         return fail(RTX_ERR_INVALID_ARG, "region [%u+%u, %u+%u] outside %ux%u image", r->x0, r->width, r->y0, r->height,
                     cam->image_width, cam->image_height);
@@ -826,8 +828,20 @@ int check_region(const rtx_camera* cam, const rtx_region* r) {
 }
 
 uint32_t region_rows(const rtx_region* r) {
-    if (r->world == 0 || r->rank >= r->world || r->height <= r->rank) return 0;
-    return (r->height - r->rank + r->world - 1) / r->world;
+    if (r->world == 0 || r->rank >= r->world) return 0;
+    const uint32_t S = r->stripe > 1u ? r->stripe : 1u;
+    const uint32_t nst = (r->height + S - 1) / S;  // stripes, the last one maybe partial
+    if (r->rank >= nst) return 0;
+    const uint32_t k = (nst - r->rank + r->world - 1) / r->world;  // this shard's stripes
+    uint32_t rows = k * S;
+    if ((nst - 1) % r->world == r->rank && r->height % S) rows -= S - r->height % S;  // it holds the partial one
+    return rows;
+}
+
+// Stripe rows for the bands of rtx_render(n_gpus > 1) (RTX_STRIPE overrides: 1 = single rows, A/B).
+uint32_t band_stripe(int n) {
+    const uint32_t v = n > 1 ? env_knob("RTX_STRIPE", 8, 1, 4096) : 1u;
+    return 1u << (31 - __builtin_clz(v));  // a power of two
 }
 
 // Integer knob from the environment (read per call), clamped to [lo, hi].
@@ -882,9 +896,10 @@ rtxd::Params make_params(const rtx_scene* s, const DeviceCopy* c, uint32_t oct, 
     p.rows = region_rows(r);
     p.rank = r->rank;
     p.world = r->world;
+    p.stripe_log2 = r->stripe > 1 ? (uint32_t)__builtin_ctz(r->stripe) : 0u;
     // RTX_TILE_W = 8 / 16 / 32 overrides the tile width (A/B)
     const uint32_t tw = env_knob("RTX_TILE_W", 0, 0, 32);
-    p.tile_w_log2 = tw >= 32 ? 5u : (tw >= 16 ? 4u : (tw >= 8 ? 3u : rtxd::tile_w_log2_for(r->world)));
+    p.tile_w_log2 = tw >= 32 ? 5u : (tw >= 16 ? 4u : (tw >= 8 ? 3u : rtxd::tile_w_log2_for(r->world, r->stripe)));
     p.out = d_out;
     p.counters = c->counters;
     p.tile_counter = reinterpret_cast<uint32_t*>(c->counters + 7);  // slot 7 low: unit queue head
@@ -1150,11 +1165,13 @@ int finish_scene(rtx_scene* s, const rtx_scene_desc* d, rtx_scene** out) {
 // rtx_render's band assembly on device 0: the RCCL-gathered bands g[d][r][:] (n bands
 // of R rows, row_floats = 3 W floats each; band d holds image rows y = d + r n) -> img[y][:].
 __global__ __launch_bounds__(256) void deinterleave_bands(const float* __restrict__ g, float* __restrict__ img,
-                                                          uint32_t n, uint32_t R, uint32_t H, uint32_t row_floats) {
+                                                          uint32_t n, uint32_t R, uint32_t H, uint32_t row_floats,
+                                                          uint32_t S) {
     const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= (uint64_t)H * row_floats) return;
     const uint32_t y = (uint32_t)(i / row_floats), x = (uint32_t)(i % row_floats);
-    img[i] = g[((uint64_t)(y % n) * R + y / n) * row_floats + x];
+    const uint32_t st = y / S, d = st % n, lr = (st / n) * S + y % S;  // stripe st of band d: its row lr
+    img[i] = g[((uint64_t)d * R + lr) * row_floats + x];
 }
 
 void add_stats(rtx_stats* acc, const rtx_stats& s) {
@@ -1206,6 +1223,11 @@ int rtx_device_count(void) {
 }
 
 uint32_t rtx_region_rows(const rtx_region* region) { return region ? region_rows(region) : 0; }
+uint32_t rtx_region_row(const rtx_region* region, uint32_t i) {
+    if (!region || region->world == 0) return 0;
+    const uint32_t S = region->stripe > 1u ? region->stripe : 1u;
+    return ((i / S) * region->world + region->rank) * S + i % S;
+}
 
 int rtx_scene_create(const rtx_scene_desc* d, rtx_scene** out) { return rtx_scene_create_ex(d, 0u, out); }
 
@@ -1501,7 +1523,9 @@ int render_bands_locked(rtx_scene* s, const rtx_camera* cam, uint64_t seed, int 
     int cur = 0;
     HIP_TRY(hipGetDevice(&cur));
     const uint32_t W = cam->image_width, H = cam->image_height;
-    const uint32_t R = (H + n - 1) / n;  // rows of band 0, the longest: every band is sent padded to R
+    const uint32_t S = band_stripe(n);  // rows per stripe (8 for several bands: compact 8x8 tiles)
+    rtx_region reg0{0, 0, W, H, 0, (uint32_t)n, S};
+    const uint32_t R = region_rows(&reg0);  // rows of band 0, the longest: every band is sent padded to R
     const size_t band_floats = (size_t)R * W * 3, band_bytes = std::max<size_t>(band_floats, 1) * sizeof(float);
     const size_t img_bytes = (size_t)H * W * 3 * sizeof(float);
     std::vector<float*> bufs(n, nullptr);
@@ -1518,7 +1542,7 @@ int render_bands_locked(rtx_scene* s, const rtx_camera* cam, uint64_t seed, int 
         DeviceCopy* c = nullptr;
         if ((rc = ensure_device(s, dv, &c))) break;
         if (hipSetDevice(dv) != hipSuccess) { rc = fail(RTX_ERR_HIP, "hipSetDevice(%d)", dv); break; }
-        regs[d] = rtx_region{0, 0, W, H, (uint32_t)d, (uint32_t)n};
+        regs[d] = rtx_region{0, 0, W, H, (uint32_t)d, (uint32_t)n, S};
         if (!(streams[d] = render_stream(dv))) { rc = fail(RTX_ERR_HIP, "stream on device %d", dv); break; }
         if (!(bufs[d] = static_cast<float*>(render_buffer(dv, d, band_bytes)))) {
             rc = fail(RTX_ERR_OOM, "hipMalloc band %zu B", band_bytes);
@@ -1601,7 +1625,7 @@ int render_bands_locked(rtx_scene* s, const rtx_camera* cam, uint64_t seed, int 
         (void)hipSetDevice(0);
         const uint64_t total_floats = (uint64_t)H * W * 3;
         hipLaunchKernelGGL(deinterleave_bands, dim3((uint32_t)((total_floats + 255) / 256)), dim3(256), 0, streams[0],
-                           gathered, img, (uint32_t)n, R, H, W * 3);
+                           gathered, img, (uint32_t)n, R, H, W * 3, S);
         hipError_t e = hipGetLastError();
         if (e == hipSuccess) e = hipEventRecord(g1, streams[0]);
         if (e == hipSuccess && out_rgb) e = copy_to_host(out_rgb, img, total_floats * sizeof(float), streams[0]);
@@ -1610,18 +1634,24 @@ int render_bands_locked(rtx_scene* s, const rtx_camera* cam, uint64_t seed, int 
         if (e != hipSuccess) rc = fail(RTX_ERR_HIP, "band assembly: %s", hipGetErrorString(e));
         if (rc == RTX_OK && !out_rgb) *dev_img = img;
     } else if (rc == RTX_OK && kind == RTX_GATHER_HOST) {
-        // band d holds image rows y = d + r n: one strided copy per band into the caller's rows (for a
-        // device image, rows of a host image that then goes to device 0 in one copy: RCCL's fallback only)
+        // band d holds the stripes d, d + n, ... (S rows each): one strided copy per band of its whole stripes
+        // into the caller's rows, the partial last stripe separately (for a device image, rows of a host image that
+        // then goes to device 0 in one copy: RCCL's fallback only)
         std::vector<float> host_img(out_rgb ? 0 : (size_t)H * W * 3);
         float* dst = out_rgb ? out_rgb : host_img.data();
+        const size_t row_b = (size_t)W * 3 * sizeof(float);
         for (int d = 0; d < n && rc == RTX_OK; ++d) {
             const uint32_t rows = region_rows(&regs[d]);
             if (!rows) continue;
-            if (hipSetDevice(dev_of(d)) != hipSuccess ||
-                hipMemcpy2DAsync(dst + (size_t)d * W * 3, (size_t)n * W * 3 * sizeof(float), bufs[d],
-                                 (size_t)W * 3 * sizeof(float), (size_t)W * 3 * sizeof(float), rows,
-                                 hipMemcpyDeviceToHost, streams[d]) != hipSuccess)
-                rc = fail(RTX_ERR_HIP, "band %d copy to the host", d);
+            const uint32_t full = rows / S, part = rows % S;  // whole stripes, rows of a partial last one
+            hipError_t e = hipSetDevice(dev_of(d));
+            if (e == hipSuccess && full)
+                e = hipMemcpy2DAsync(dst + (size_t)d * S * W * 3, (size_t)n * S * row_b, bufs[d], S * row_b, S * row_b,
+                                     full, hipMemcpyDeviceToHost, streams[d]);
+            if (e == hipSuccess && part)
+                e = hipMemcpyAsync(dst + (size_t)((size_t)full * n + d) * S * W * 3, bufs[d] + (size_t)full * S * W * 3,
+                                   part * row_b, hipMemcpyDeviceToHost, streams[d]);
+            if (e != hipSuccess) rc = fail(RTX_ERR_HIP, "band %d copy to the host", d);
         }
         for (int d = 0; d < n; ++d)
             if (hipSetDevice(dev_of(d)) == hipSuccess && hipStreamSynchronize(streams[d]) != hipSuccess && rc == RTX_OK)

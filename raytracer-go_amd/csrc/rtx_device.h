@@ -447,6 +447,7 @@ struct Params {
     rtx_camera cam;
     uint64_t seed;
     uint32_t x0, y0, width, rows, rank, world;
+    uint32_t stripe_log2;  // shard row lr is image row y0 + (((lr >> s) * world + rank) << s) + (lr & (2^s - 1))
     uint32_t tile_w_log2;  // a tile of 64 pixels is (1 << tile_w_log2) wide (8 or 16) and 64 >> tile_w_log2 rows tall
     float* out;
     unsigned long long* counters;  // rtx_stats order when counting (COUNTER_SLOTS x u64)
@@ -518,8 +519,13 @@ struct Ray {
 // 16 x 4 for N = 4 (16 x 16 image pixels instead of 8 x 32), 32 x 2 from N = 8 on (32 x 16 instead of
 // 8 x 64).  Rank 0's rows alone (profiles/r04_tile_ab.jsonl): N = 4 25.66 / 25.66 ms (16 / 32 wide)
 // against 25.94 (8); N = 8 13.45 / 13.39 against 13.74.
-__host__ __device__ __forceinline__ uint32_t tile_w_log2_for(uint32_t world) {
+__host__ __device__ __forceinline__ uint32_t tile_w_log2_for(uint32_t world, uint32_t stripe = 1) {
+    if (stripe >= 8) return 3u;  // 8-row stripes: an 8 x 8 tile is 8 x 8 image pixels again
     return world >= 8 ? 5u : (world >= 4 ? 4u : 3u);
+}
+// The image row (relative to y0) of shard row lr (rtx.h rtx_region_row, stripes of 2^s rows).
+__host__ __device__ __forceinline__ uint32_t region_row(uint32_t lr, uint32_t rank, uint32_t world, uint32_t s) {
+    return (((lr >> s) * world + rank) << s) + (lr & ((1u << s) - 1u));
 }
 __host__ __device__ __forceinline__ uint32_t tiles_x_of(uint32_t width, uint32_t twl) { return (width + (1u << twl) - 1u) >> twl; }
 __host__ __device__ __forceinline__ uint32_t tiles_y_of(uint32_t rows, uint32_t twl) {

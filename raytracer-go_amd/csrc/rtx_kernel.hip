@@ -505,7 +505,7 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
                     pool_blk = blk;
                     const uint32_t lx = u_x + (lane & tw_mask), lr = u_r + (lane >> twl);
                     if (lx < p.width && lr < p.rows) {
-                        const uint32_t x = p.x0 + lx, y = p.y0 + p.rank + lr * p.world;
+                        const uint32_t x = p.x0 + lx, y = p.y0 + region_row(lr, p.rank, p.world, p.stripe_log2);
                         const PathRng cr{rng.k0, rng.k1, y * c.image_width + x, u_k0 + blk};
                         uint32_t dr = 0;
                         const Ray cray = camera_ray<!COUNT>(c, pixel_base(c, x, y), cr, cr.block(0u, 0u), dr);
@@ -550,7 +550,7 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
                 // else: outside a ragged tile (or, redo pass, not flagged), claim again
                 if (lx < p.width && lr < p.rows &&
                     (TIER != 3 || listed || ((redo64[((size_t)(k - p.k0) * n_tiles * 64 + slot) >> 6] >> l) & 1ull))) {
-                    const uint32_t x = p.x0 + lx, y = p.y0 + p.rank + lr * p.world;
+                    const uint32_t x = p.x0 + lx, y = p.y0 + region_row(lr, p.rank, p.world, p.stripe_log2);
                     if constexpr (POOL) {  // the ray the wave drew for this item (l: the pixel of the block)
                         const float4 po = pool[2 * l], pd = pool[2 * l + 1];
                         r = Ray{v3(po.x, po.y, po.z), v3(pd.x, pd.y, pd.z)};

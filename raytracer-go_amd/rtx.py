@@ -97,8 +97,10 @@ class Camera(ctypes.Structure):
 
 
 class Region(ctypes.Structure):
+    """rtx_region: columns [x0, x0 + width), the rows of [y0, y0 + height) in stripes of `stripe` rows (0 / 1:
+    single rows) dealt round-robin: this shard takes stripes rank, rank + world, ... (ABI 9: stripe)."""
     _fields_ = [("x0", c_uint32), ("y0", c_uint32), ("width", c_uint32), ("height", c_uint32),
-                ("rank", c_uint32), ("world", c_uint32)]
+                ("rank", c_uint32), ("world", c_uint32), ("stripe", c_uint32)]
 
 
 class Stats(ctypes.Structure):
@@ -123,7 +125,7 @@ RTX_SYMBOLS = [
     "rtx_ppm_max_bytes", "rtx_encode_ppm_device", "rtx_render_ppm", "rtx_scene_create_spheres", "rtx_scene_export",
     "rtx_release_device_memory", "rtx_device_scratch_bytes", "rtx_scene_create_ex", "rtx_scene_topology",
     "rtx_camera_octant", "rtx_walk_tree", "rtx_render_ex", "rtx_scene_walk_skip", "rtx_walk_skip",
-    "rtx_scene_near_region", "rtx_scene_near_skip", "rtx_walk_near_region", "rtx_render_ppm_ex",
+    "rtx_scene_near_region", "rtx_scene_near_skip", "rtx_walk_near_region", "rtx_render_ppm_ex", "rtx_region_row",
 ]
 RTXHOST_SYMBOLS = [
     "rtxhost_build_scene", "rtxhost_scene_free", "rtxhost_scene_desc", "rtxhost_scene_camera",
