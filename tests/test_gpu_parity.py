@@ -495,6 +495,16 @@ def test_tier_deferred_paths_c2_crop(torch_cuda, spheres, dev_spheres):
     assert 0 < st.deferred_paths < 0.2 * st.samples, (st.deferred_paths, st.samples)
 
 
+@pytest.mark.parametrize("stripe,world", [(8, 4), (4, 3), (16, 2)])
+def test_striped_shards(torch_cuda, spheres, dev_spheres, stripe, world):
+    """Shards of stripes (rtx_region.stripe, ABI 9: stripes of S rows dealt round-robin; 8 is rtx_render's and
+    bench.py's) on a ragged window: every shard of both kernels bit-identical to the oracle's same shard
+    (the oracle restates the row mapping), with the default tile shape for striped shards (8 x 8)."""
+    cam = spheres.camera(width=160, spp=4, depth=50)
+    for rank in range(world):
+        check_scene(torch_cuda, dev_spheres, spheres.desc, cam, 31, rtx.Region(3, 5, 101, 61, rank, world, stripe))
+
+
 @pytest.mark.parametrize("tile_w", ["16", "32"])
 def test_tile_shapes(torch_cuda, spheres, dev_spheres, monkeypatch, tile_w):
     """Tiles of 64 pixels 16 x 4 (the default from four row-interleaved shards on) and 32 x 2

@@ -136,10 +136,10 @@ def test_watchdog_stops_v3(built):
 
 @pytest.mark.parametrize("bands", [2, 3, 5, 7])
 def test_band_assembly_index_math_one_gpu(built, bands):
-    """The n > 1 assembly on one GPU (RTX_SIM_BANDS=k: k row-interleaved bands rendered on device 0,
-    each padded to R = ceil(H / k) rows, placed at band offsets as the RCCL gather places them,
-    de-interleaved by the kernel; with RTX_NO_RCCL=1 each band's rows copied straight into the
-    caller's rows instead).  H = 112 is not a multiple of 3, 5 or 7: ragged last bands."""
+    """The n > 1 assembly on one GPU (RTX_SIM_BANDS=k: k bands of 8-row stripes dealt round-robin, rendered on
+    device 0, each padded to band 0's rows, placed at band offsets as the RCCL gather places them,
+    de-interleaved by the kernel; with RTX_NO_RCCL=1 each band's stripes copied straight into the caller's
+    rows instead).  H = 112 = 14 stripes: 3, 5 and 7 bands get unequal stripe counts."""
     out = child(
         f"k = {bands}\n"
         "import os\n"
