@@ -4,7 +4,7 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-OUT="$PWD/gpurun_out/r05g"; mkdir -p "$OUT"
+OUT="$PWD/gpurun_out/${TRACE_TAG:-r05g}"; mkdir -p "$OUT"
 timeout -s KILL 240 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv -- python bench.py --no-cpu \
     > "$OUT/bench_under_rocprof.json" 2> "$OUT/trace.log" || { tail -5 "$OUT/trace.log"; exit 1; }
 find "$OUT/trace" -name "*kernel_stats.csv" -exec cp {} "$OUT/kernel_stats.csv" \;
