@@ -900,6 +900,7 @@ rtxd::Params make_params(const rtx_scene* s, const DeviceCopy* c, uint32_t oct, 
     // RTX_TILE_W = 8 / 16 / 32 overrides the tile width (A/B)
     const uint32_t tw = env_knob("RTX_TILE_W", 0, 0, 32);
     p.tile_w_log2 = tw >= 32 ? 5u : (tw >= 16 ? 4u : (tw >= 8 ? 3u : rtxd::tile_w_log2_for(r->world, r->stripe)));
+    p.tile_w_log2 = std::max(p.tile_w_log2, rtxd::tile_w_log2_min(p.stripe_log2));  // a tile within one stripe
     p.out = d_out;
     p.counters = c->counters;
     p.tile_counter = reinterpret_cast<uint32_t*>(c->counters + 7);  // slot 7 low: unit queue head

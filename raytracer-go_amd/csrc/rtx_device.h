@@ -521,8 +521,11 @@ struct Ray {
 // against 25.94 (8); N = 8 13.45 / 13.39 against 13.74.
 __host__ __device__ __forceinline__ uint32_t tile_w_log2_for(uint32_t world, uint32_t stripe = 1) {
     if (stripe >= 8) return 3u;  // 8-row stripes: an 8 x 8 tile is 8 x 8 image pixels again
+    if (stripe > 1) return stripe == 4 ? 4u : 5u;  // a tile's rows within one stripe (render_items' u_y)
     return world >= 8 ? 5u : (world >= 4 ? 4u : 3u);
 }
+// The narrowest tile (log2 of its width) whose rows lie within one stripe of 2^s rows (s = 0: single rows, any).
+__host__ __device__ __forceinline__ uint32_t tile_w_log2_min(uint32_t s) { return s == 0 ? 3u : (s >= 3 ? 3u : 6u - s); }
 // The image row (relative to y0) of shard row lr (rtx.h rtx_region_row, stripes of 2^s rows).
 __host__ __device__ __forceinline__ uint32_t region_row(uint32_t lr, uint32_t rank, uint32_t world, uint32_t s) {
     return (((lr >> s) * world + rank) << s) + (lr & ((1u << s) - 1u));

@@ -295,6 +295,10 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
     // the wave's unit (uniform, kept in SGPRs: every value below is derived from readfirstlane):
     // tile (index, origin u_x, u_r), first sample, items, next item
     uint32_t u_tile = 0, u_x = 0, u_r = 0, u_k0 = 0, u_items = 0, cursor = 0;
+    // the image row of the unit's first tile row; a tile's rows lie in one stripe (make_params: its height divides
+    // the stripe), so row i of the tile is image row u_y + i * ystep (ystep = world for single-row stripes)
+    uint32_t u_y = 0;
+    const uint32_t ystep = p.stripe_log2 ? 1u : p.world;
     bool exhausted = false;
     // POOL: the wave's 64 camera rays (2 float4 each) after the scene copy, and the unit's block they hold
     float4* const pool = POOL ? lds_entries + pool_f4_offset(p) + (threadIdx.x >> 6) * 128 : nullptr;
@@ -483,6 +487,7 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
                     u_tile = uu / nsub;
                     u_x = (u_tile % tiles_x) << twl;
                     u_r = (u_tile / tiles_x) * th;
+                    u_y = p.y0 + region_row(u_r, p.rank, p.world, p.stripe_log2);
                     u_k0 = p.k0 + (uu - u_tile * nsub) * p.sub;
                     const uint32_t cnt_k = min(p.sub, p.k0 + p.kn - u_k0);
                     u_items = 64u * cnt_k;
@@ -505,7 +510,7 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
                     pool_blk = blk;
                     const uint32_t lx = u_x + (lane & tw_mask), lr = u_r + (lane >> twl);
                     if (lx < p.width && lr < p.rows) {
-                        const uint32_t x = p.x0 + lx, y = p.y0 + region_row(lr, p.rank, p.world, p.stripe_log2);
+                        const uint32_t x = p.x0 + lx, y = u_y + (lane >> twl) * ystep;
                         const PathRng cr{rng.k0, rng.k1, y * c.image_width + x, u_k0 + blk};
                         uint32_t dr = 0;
                         const Ray cray = camera_ray<!COUNT>(c, pixel_base(c, x, y), cr, cr.block(0u, 0u), dr);
@@ -550,7 +555,9 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
                 // else: outside a ragged tile (or, redo pass, not flagged), claim again
                 if (lx < p.width && lr < p.rows &&
                     (TIER != 3 || listed || ((redo64[((size_t)(k - p.k0) * n_tiles * 64 + slot) >> 6] >> l) & 1ull))) {
-                    const uint32_t x = p.x0 + lx, y = p.y0 + region_row(lr, p.rank, p.world, p.stripe_log2);
+                    const uint32_t x = p.x0 + lx,
+                                   y = TIER == 3 && listed ? p.y0 + region_row(lr, p.rank, p.world, p.stripe_log2)
+                                                           : u_y + (l >> twl) * ystep;
                     if constexpr (POOL) {  // the ray the wave drew for this item (l: the pixel of the block)
                         const float4 po = pool[2 * l], pd = pool[2 * l + 1];
                         r = Ray{v3(po.x, po.y, po.z), v3(pd.x, pd.y, pd.z)};

@@ -1,5 +1,6 @@
 #!/bin/bash
-# gpurun (round 5): the striped library against the one before it (abl/librtx_prestripe.so) on C2 in one call; the
+# gpurun (round 5): the striped library (per-tile row base: affine; per-lane mapping: stripegen) against the one
+# before stripes (prestripe) on C2 in one call; the
 # advisor's mid-size LDS cache A/B on an UNTIERED config-4 render (RTX_TIER=0: the caller's tree alone, where the
 # 8-wave / 12-wave switch applies): RTX_HOT_ENTRIES=1280 in tree (12-wave) against HOT_B = 32 KB (8-wave); then the
 # driver's default bench command.
@@ -8,8 +9,8 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 OUT="$PWD/gpurun_out/r05k"; mkdir -p "$OUT"
 for i in 1 2; do
-  for lib in cur prestripe; do
-    L=""; [ $lib != cur ] && L="RTX_LIB=$PWD/abl/librtx_$lib.so"
+  for lib in affine stripegen prestripe; do
+    L="RTX_LIB=$PWD/abl/librtx_$lib.so"
     timeout -k 10 240 env $L python scripts/ab.py --spp 500 --rounds 3 --variants v3 > "$OUT/c2_${lib}_$i.log" 2>&1 || { tail -5 "$OUT/c2_${lib}_$i.log"; exit 1; }
     echo "$lib $(grep median "$OUT/c2_${lib}_$i.log" | head -1)"
   done
