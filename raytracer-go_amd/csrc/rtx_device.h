@@ -447,7 +447,6 @@ struct Params {
     rtx_camera cam;
     uint64_t seed;
     uint32_t x0, y0, width, rows, rank, world;
-    uint32_t stripe_log2;  // shard row lr is image row y0 + (((lr >> s) * world + rank) << s) + (lr & (2^s - 1))
     uint32_t tile_w_log2;  // a tile of 64 pixels is (1 << tile_w_log2) wide (8 or 16) and 64 >> tile_w_log2 rows tall
     float* out;
     unsigned long long* counters;  // rtx_stats order when counting (COUNTER_SLOTS x u64)
@@ -491,6 +490,9 @@ struct Params {
     uint32_t debug_partial;
     uint32_t cam_pool;  // 1: the near pass takes camera rays from the wave's LDS pool when it fits (RTX_CAM_POOL=0: off)
     uint32_t refill_hits;  // POOL: a miss phase when fewer waiting lanes than this hit (RTX_REFILL_HITS; 0: never)
+    // (last: the fields before it keep their kernel-argument offsets) a striped shard (rtx_region.stripe = 2^s > 1):
+    // shard row lr is image row y0 + (((lr >> s) * world + rank) << s) + (lr & (2^s - 1)); render_items<ST>
+    uint32_t stripe_log2;
 };
 
 // The camera-ray pool of render_items<POOL>: after the fixed layout's scene copy (16-B aligned), 64 rays

@@ -224,8 +224,12 @@ __device__ __forceinline__ void split_clk(uint64_t& acc, uint64_t& clk) {
 // 265-299: Philox block (0, 0) of (pixel, sample), the defocus disk's rejection loop) are the same
 // bits; only who evaluates them changes: 64 lanes per evaluation instead of the few lanes a shading
 // phase claims for (about a third of the wave).
+//
+// ST: the region's shard is in stripes of 2^stripe_log2 > 1 rows; the image row of a tile row comes from
+// a per-unit base.  Single-row shards (every one-GPU render) run the ST = false instantiation, whose row arithmetic is
+// the one before stripes existed (its code unchanged: the headline kernel).
 template <bool COUNT, bool USE_LDS, bool QUADS, bool NOISE, int WAVES = 8, int MINW = 0, bool HYB = false,
-          bool CLK = false, int TIER = 0, bool POOL = false>
+          bool CLK = false, int TIER = 0, bool POOL = false, bool ST = false>
 __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
     constexpr bool TIME = COUNT || CLK;
     static_assert(!POOL || (USE_LDS && (TIER == 0 || TIER == 1)), "the camera-ray pool: LDS scenes, near pass or one walk");
@@ -295,10 +299,9 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
     // the wave's unit (uniform, kept in SGPRs: every value below is derived from readfirstlane):
     // tile (index, origin u_x, u_r), first sample, items, next item
     uint32_t u_tile = 0, u_x = 0, u_r = 0, u_k0 = 0, u_items = 0, cursor = 0;
-    // the image row of the unit's first tile row; a tile's rows lie in one stripe (make_params: its height divides
-    // the stripe), so row i of the tile is image row u_y + i * ystep (ystep = world for single-row stripes)
+    // ST: the image row of the unit's first tile row; a tile's rows lie in one stripe (make_params: its height divides
+    // the stripe), so row i of the tile is image row u_y + i
     uint32_t u_y = 0;
-    const uint32_t ystep = p.stripe_log2 ? 1u : p.world;
     bool exhausted = false;
     // POOL: the wave's 64 camera rays (2 float4 each) after the scene copy, and the unit's block they hold
     float4* const pool = POOL ? lds_entries + pool_f4_offset(p) + (threadIdx.x >> 6) * 128 : nullptr;
@@ -487,7 +490,7 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
                     u_tile = uu / nsub;
                     u_x = (u_tile % tiles_x) << twl;
                     u_r = (u_tile / tiles_x) * th;
-                    u_y = p.y0 + region_row(u_r, p.rank, p.world, p.stripe_log2);
+                    if constexpr (ST) u_y = p.y0 + region_row(u_r, p.rank, p.world, p.stripe_log2);
                     u_k0 = p.k0 + (uu - u_tile * nsub) * p.sub;
                     const uint32_t cnt_k = min(p.sub, p.k0 + p.kn - u_k0);
                     u_items = 64u * cnt_k;
@@ -510,7 +513,7 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
                     pool_blk = blk;
                     const uint32_t lx = u_x + (lane & tw_mask), lr = u_r + (lane >> twl);
                     if (lx < p.width && lr < p.rows) {
-                        const uint32_t x = p.x0 + lx, y = u_y + (lane >> twl) * ystep;
+                        const uint32_t x = p.x0 + lx, y = ST ? u_y + (lane >> twl) : p.y0 + p.rank + lr * p.world;
                         const PathRng cr{rng.k0, rng.k1, y * c.image_width + x, u_k0 + blk};
                         uint32_t dr = 0;
                         const Ray cray = camera_ray<!COUNT>(c, pixel_base(c, x, y), cr, cr.block(0u, 0u), dr);
@@ -556,8 +559,9 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
                 if (lx < p.width && lr < p.rows &&
                     (TIER != 3 || listed || ((redo64[((size_t)(k - p.k0) * n_tiles * 64 + slot) >> 6] >> l) & 1ull))) {
                     const uint32_t x = p.x0 + lx,
-                                   y = TIER == 3 && listed ? p.y0 + region_row(lr, p.rank, p.world, p.stripe_log2)
-                                                           : u_y + (l >> twl) * ystep;
+                                   y = !ST ? p.y0 + p.rank + lr * p.world
+                                           : (TIER == 3 && listed ? p.y0 + region_row(lr, p.rank, p.world, p.stripe_log2)
+                                                                  : u_y + (l >> twl));
                     if constexpr (POOL) {  // the ray the wave drew for this item (l: the pixel of the block)
                         const float4 po = pool[2 * l], pd = pool[2 * l + 1];
                         r = Ray{v3(po.x, po.y, po.z), v3(pd.x, pd.y, pd.z)};
@@ -708,7 +712,8 @@ hipError_t resident_grid(const void* kern, int block, size_t shmem, int* per_cu,
 // v3: chunks of p.kn samples (the scratch holds one chunk), each rendered by a
 // resident-capacity grid of render_items and summed into p.out by reduce_samples.
 // POOL (a scene in the LDS copy, the timed kernel): the camera-ray pool after the scene copy (render_items<POOL>).
-template <bool COUNT, bool QUADS, bool NOISE, int WAVES = 8, int MINW = 0, bool CLK = false, bool POOL = false>
+template <bool COUNT, bool QUADS, bool NOISE, int WAVES = 8, int MINW = 0, bool CLK = false, bool POOL = false,
+          bool ST = false>
 hipError_t launch_items(Params p, bool use_lds, hipStream_t stream) {
     // a scene too big for LDS: its top levels (p.n_hot entries) cached in LDS when the
     // device layout stored them first (RTX_HOT_ENTRIES=0 turns that off)
@@ -716,10 +721,10 @@ hipError_t launch_items(Params p, bool use_lds, hipStream_t stream) {
     const size_t shmem = POOL ? (size_t)pool_f4_offset(p) * 16 + WAVES * POOL_BYTES_PER_WAVE
                               : use_lds ? lds_fixed_bytes(p.n_entries, p.n_quads, p.n_materials, p.n_textures)
                                         : (hyb ? lds_hot_bytes(p.n_hot) : 0);
-    const auto kern = POOL      ? render_items<COUNT, true, QUADS, NOISE, WAVES, MINW, false, CLK, 0, POOL>
-                      : use_lds ? render_items<COUNT, true, QUADS, NOISE, WAVES, MINW, false, CLK>
-                                : (hyb ? render_items<COUNT, false, QUADS, NOISE, WAVES, MINW, !NOISE, CLK>
-                                       : render_items<COUNT, false, QUADS, NOISE, WAVES, MINW, false, CLK>);
+    const auto kern = POOL      ? render_items<COUNT, true, QUADS, NOISE, WAVES, MINW, false, CLK, 0, POOL, ST>
+                      : use_lds ? render_items<COUNT, true, QUADS, NOISE, WAVES, MINW, false, CLK, 0, false, ST>
+                                : (hyb ? render_items<COUNT, false, QUADS, NOISE, WAVES, MINW, !NOISE, CLK, 0, false, ST>
+                                       : render_items<COUNT, false, QUADS, NOISE, WAVES, MINW, false, CLK, 0, false, ST>);
     constexpr int block = 64 * WAVES;
     int cus = 0, per_cu = 0;
     hipError_t e = resident_grid((const void*)kern, block, shmem, &per_cu, &cus);
@@ -763,11 +768,11 @@ inline size_t items_shmem(const Params& p, bool use_lds, bool hyb) {
 // workgroups of WN waves (12: two per CU, each with its scene copy and 12 pools); the far and redo
 // passes keep WAVES.
 template <bool COUNT, int WAVES, int MINW, bool CLK = false, bool USE_LDS = true, bool HYB = false, bool POOL = false,
-          int WN = POOL ? 12 : WAVES>
+          bool ST = false, int WN = POOL ? 12 : WAVES>
 hipError_t launch_tiered(Params pn, Params pf, hipStream_t stream) {
-    const auto kn = render_items<COUNT, USE_LDS, false, false, WN, MINW, HYB, CLK, 1, POOL>;
-    const auto kf = render_items<COUNT, USE_LDS, false, false, WAVES, MINW, HYB, CLK, 2>;
-    const auto kr = render_items<COUNT, USE_LDS, false, false, WAVES, MINW, HYB, false, 3>;
+    const auto kn = render_items<COUNT, USE_LDS, false, false, WN, MINW, HYB, CLK, 1, POOL, ST>;
+    const auto kf = render_items<COUNT, USE_LDS, false, false, WAVES, MINW, HYB, CLK, 2>;  // (rows from the records)
+    const auto kr = render_items<COUNT, USE_LDS, false, false, WAVES, MINW, HYB, false, 3, false, ST>;
     const size_t sn = POOL ? (size_t)pool_f4_offset(pn) * 16 + WN * POOL_BYTES_PER_WAVE : items_shmem(pn, USE_LDS, HYB),
                  sf = items_shmem(pf, USE_LDS, HYB);
     constexpr int block = 64 * WAVES, block_n = 64 * WN;
@@ -822,22 +827,23 @@ hipError_t launch_tiered(Params pn, Params pf, hipStream_t stream) {
 #define RTX_V3_MINW 6
 #endif
 
-template <bool COUNT>
+template <bool COUNT, bool ST>
 hipError_t launch_items_for(const Params& p, bool use_lds, hipStream_t stream) {
-    if (p.has_noise) return p.n_quads ? launch_items<COUNT, true, true>(p, use_lds, stream)
-                                      : launch_items<COUNT, false, true>(p, use_lds, stream);
+    if (p.has_noise) return p.n_quads ? launch_items<COUNT, true, true, 8, 0, false, false, ST>(p, use_lds, stream)
+                                      : launch_items<COUNT, false, true, 8, 0, false, false, ST>(p, use_lds, stream);
     if (p.item_waves == 4)  // A/B: 4 waves per LDS copy of the scene
-        return p.n_quads ? launch_items<COUNT, true, false, 4>(p, use_lds, stream)
-                         : launch_items<COUNT, false, false, 4>(p, use_lds, stream);
+        return p.n_quads ? launch_items<COUNT, true, false, 4, 0, false, false, ST>(p, use_lds, stream)
+                         : launch_items<COUNT, false, false, 4, 0, false, false, ST>(p, use_lds, stream);
     // 6 waves per SIMD: at most 80 VGPRs (the allocation granule is 8)
+    constexpr int MV = COUNT ? 0 : RTX_V3_MINW, MH = COUNT ? 0 : RTX_HYB_MINW;
     if (!use_lds && p.n_hot > HOT_ENTRIES_8W)  // an LDS cache past a third of the CU: 12-wave workgroups, two per CU
-        return p.n_quads ? launch_items<COUNT, true, false, RTX_HYB_WAVES, COUNT ? 0 : RTX_HYB_MINW>(p, use_lds, stream)
-                         : launch_items<COUNT, false, false, RTX_HYB_WAVES, COUNT ? 0 : RTX_HYB_MINW>(p, use_lds, stream);
+        return p.n_quads ? launch_items<COUNT, true, false, RTX_HYB_WAVES, MH, false, false, ST>(p, use_lds, stream)
+                         : launch_items<COUNT, false, false, RTX_HYB_WAVES, MH, false, false, ST>(p, use_lds, stream);
     if (use_lds && pool_fits(p))  // the camera-ray pool (12-wave workgroups, two per CU) when the scene copy leaves room
-        return p.n_quads ? launch_items<COUNT, true, false, 12, COUNT ? 0 : RTX_V3_MINW, false, true>(p, use_lds, stream)
-                         : launch_items<COUNT, false, false, 12, COUNT ? 0 : RTX_V3_MINW, false, true>(p, use_lds, stream);
-    return p.n_quads ? launch_items<COUNT, true, false, RTX_V3_WAVES, COUNT ? 0 : RTX_V3_MINW>(p, use_lds, stream)
-                     : launch_items<COUNT, false, false, RTX_V3_WAVES, COUNT ? 0 : RTX_V3_MINW>(p, use_lds, stream);
+        return p.n_quads ? launch_items<COUNT, true, false, 12, MV, false, true, ST>(p, use_lds, stream)
+                         : launch_items<COUNT, false, false, 12, MV, false, true, ST>(p, use_lds, stream);
+    return p.n_quads ? launch_items<COUNT, true, false, RTX_V3_WAVES, MV, false, false, ST>(p, use_lds, stream)
+                     : launch_items<COUNT, false, false, RTX_V3_WAVES, MV, false, false, ST>(p, use_lds, stream);
 }
 
 uint32_t scene_placement(const Params& p, uint32_t flags) {
@@ -854,35 +860,42 @@ uint32_t tier_placement(const Params& near, const Params& far, uint32_t flags) {
     return a == b ? a : RTX_SCENE_IN_HBM;  // placed unalike: both passes read their layouts from HBM
 }
 
-hipError_t launch_render(const Params& p, uint32_t flags, hipStream_t stream, const Params* far) {
-    if (p.width == 0 || p.rows == 0) return hipSuccess;
-    if (!p.scratch) return hipErrorInvalidValue;  // the caller sizes the sample scratch
+// ST: the render's shard is striped (Params::stripe_log2 > 0): every kernel's ST instantiation (render_items).
+template <bool ST>
+hipError_t launch_render_t(const Params& p, uint32_t flags, hipStream_t stream, const Params* far) {
     const bool count = (flags & RTX_FLAG_COUNTERS) != 0;
     if (far) {  // the caller checked: spheres only, both layouts placed alike (tier_placement), no noise
         const uint32_t place = tier_placement(p, *far, flags);
         if (p.tier != 1 || far->tier != 2 || !p.defer || !far->defer || !p.redo_bits || p.n_quads || p.has_noise)
             return hipErrorInvalidValue;
         const bool clk = !count && (flags & RTX_FLAG_TIMING);  // diagnostics: the wave-cycle split of the passes
+        constexpr int V = RTX_V3_WAVES, MV = RTX_V3_MINW, H = RTX_HYB_WAVES, MH = RTX_HYB_MINW;
         if (place == RTX_SCENE_IN_LDS) {
             const bool pool = pool_fits(p);  // (the counting kernel too: its schedule counters are the timed kernel's)
-            if (clk) return pool ? launch_tiered<false, RTX_V3_WAVES, RTX_V3_MINW, true, true, false, true>(p, *far, stream)
-                                 : launch_tiered<false, RTX_V3_WAVES, RTX_V3_MINW, true>(p, *far, stream);
-            if (count) return pool ? launch_tiered<true, RTX_V3_WAVES, 0, false, true, false, true>(p, *far, stream)
-                                   : launch_tiered<true, RTX_V3_WAVES, 0>(p, *far, stream);
-            return pool ? launch_tiered<false, RTX_V3_WAVES, RTX_V3_MINW, false, true, false, true>(p, *far, stream)
-                        : launch_tiered<false, RTX_V3_WAVES, RTX_V3_MINW>(p, *far, stream);
+            if (clk) return pool ? launch_tiered<false, V, MV, true, true, false, true, ST>(p, *far, stream)
+                                 : launch_tiered<false, V, MV, true, true, false, false, ST>(p, *far, stream);
+            if (count) return pool ? launch_tiered<true, V, 0, false, true, false, true, ST>(p, *far, stream)
+                                   : launch_tiered<true, V, 0, false, true, false, false, ST>(p, *far, stream);
+            return pool ? launch_tiered<false, V, MV, false, true, false, true, ST>(p, *far, stream)
+                        : launch_tiered<false, V, MV, false, true, false, false, ST>(p, *far, stream);
         }
         if (place == RTX_SCENE_LDS_CACHE)  // both cached in LDS (tier_placement): 12-wave workgroups, two per CU
-            return count ? launch_tiered<true, RTX_HYB_WAVES, 0, false, false, true>(p, *far, stream)
-                         : launch_tiered<false, RTX_HYB_WAVES, RTX_HYB_MINW, false, false, true>(p, *far, stream);
-        return count ? launch_tiered<true, RTX_V3_WAVES, 0, false, false, false>(p, *far, stream)
-                     : launch_tiered<false, RTX_V3_WAVES, RTX_V3_MINW, false, false, false>(p, *far, stream);
+            return count ? launch_tiered<true, H, 0, false, false, true, false, ST>(p, *far, stream)
+                         : launch_tiered<false, H, MH, false, false, true, false, ST>(p, *far, stream);
+        return count ? launch_tiered<true, V, 0, false, false, false, false, ST>(p, *far, stream)
+                     : launch_tiered<false, V, MV, false, false, false, false, ST>(p, *far, stream);
     }
     const bool use_lds = scene_placement(p, flags) == RTX_SCENE_IN_LDS;
     if (!count && (flags & RTX_FLAG_TIMING) && !p.has_noise && p.item_waves != 4)  // diagnostics: sphere scenes
-        return p.n_quads ? launch_items<false, true, false, RTX_V3_WAVES, RTX_V3_MINW, true>(p, use_lds, stream)
-                         : launch_items<false, false, false, RTX_V3_WAVES, RTX_V3_MINW, true>(p, use_lds, stream);
-    return count ? launch_items_for<true>(p, use_lds, stream) : launch_items_for<false>(p, use_lds, stream);
+        return p.n_quads ? launch_items<false, true, false, RTX_V3_WAVES, RTX_V3_MINW, true, false, ST>(p, use_lds, stream)
+                         : launch_items<false, false, false, RTX_V3_WAVES, RTX_V3_MINW, true, false, ST>(p, use_lds, stream);
+    return count ? launch_items_for<true, ST>(p, use_lds, stream) : launch_items_for<false, ST>(p, use_lds, stream);
+}
+
+hipError_t launch_render(const Params& p, uint32_t flags, hipStream_t stream, const Params* far) {
+    if (p.width == 0 || p.rows == 0) return hipSuccess;
+    if (!p.scratch) return hipErrorInvalidValue;  // the caller sizes the sample scratch
+    return p.stripe_log2 ? launch_render_t<true>(p, flags, stream, far) : launch_render_t<false>(p, flags, stream, far);
 }
 
 }  // namespace rtxd
