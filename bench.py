@@ -56,8 +56,8 @@ def parse():
                     help="PMC HBM-traffic summaries (scripts/pmc_traffic.py): a .json, or a .jsonl of one per workload")
     ap.add_argument("--valu", default=os.path.join(ROOT, "profiles", "valu_r05.jsonl"),
                     help="PMC VALU summaries (scripts/pmc_valu.py): a .json, or a .jsonl of one per workload")
-    ap.add_argument("--stripe", type=int, default=0, help="rows per stripe of the shards (0: 8 for N > 1, 1 for N = 1; "
-                    "1 interleaves single rows, the round-4 layout)")
+    ap.add_argument("--stripe", type=int, default=1, help="rows per stripe of the shards, a power of two (1: single "
+                    "rows interleaved, the fastest slowest-rank at N = 4 and 8, profiles/r05_stripe_sweep.jsonl)")
     ap.add_argument("--shard", default="", help="R/N: one process renders only rank R's rows of N (a rank's "
                     "workload of the N-GPU run, for its PMC profile); not a scaling number")
     ap.add_argument("--in-process", action="store_true",
@@ -344,7 +344,7 @@ def main():
     srank, sworld = (int(v) for v in args.shard.split("/")) if args.shard else (rank, world)
     if world > 1 and args.shard:
         raise SystemExit("--shard is a one-process run")
-    stripe = args.stripe if args.stripe > 0 else (8 if sworld > 1 else 1)  # 8-row stripes
+    stripe = max(args.stripe, 1)  # rows per stripe
     reg = rtx.Region(0, 0, W, H, srank, sworld, stripe)
     R = max_shard_rows(H, sworld, stripe)
     shard = torch.zeros((R, W, 3), dtype=torch.float32, device="cuda")
@@ -551,7 +551,7 @@ def selftest_gloo(args, rank: int, world: int) -> None:
         dist.init_process_group("gloo")
     W = args.width
     H = int(W * 9 // 16)
-    S = args.stripe if args.stripe > 0 else (8 if world > 1 else 1)  # main()'s stripes
+    S = max(args.stripe, 1)  # main()'s stripes
     R = max_shard_rows(H, world, S)
     shard = torch.zeros((R, W, 3), dtype=torch.float32)
     for i in range(shard_rows(H, rank, world, S)):

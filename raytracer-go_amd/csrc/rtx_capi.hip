@@ -838,9 +838,11 @@ uint32_t region_rows(const rtx_region* r) {
     return rows;
 }
 
-// Stripe rows for the bands of rtx_render(n_gpus > 1) (RTX_STRIPE overrides: 1 = single rows, A/B).
+// Stripe rows for the bands of rtx_render(n_gpus > 1): single rows (RTX_STRIPE = 2^k for A/B).  Every rank of
+// the 4- and 8-GPU headline measured slowest-rank-fastest with single rows (profiles/r05_stripe_sweep.jsonl:
+// N = 8 12.55 ms against 12.78 / 12.83 / 13.05 for 2 / 4 / 8-row stripes).
 uint32_t band_stripe(int n) {
-    const uint32_t v = n > 1 ? env_knob("RTX_STRIPE", 8, 1, 4096) : 1u;
+    const uint32_t v = n > 1 ? env_knob("RTX_STRIPE", 1, 1, 4096) : 1u;
     return 1u << (31 - __builtin_clz(v));  // a power of two
 }
 
@@ -1524,7 +1526,7 @@ int render_bands_locked(rtx_scene* s, const rtx_camera* cam, uint64_t seed, int 
     int cur = 0;
     HIP_TRY(hipGetDevice(&cur));
     const uint32_t W = cam->image_width, H = cam->image_height;
-    const uint32_t S = band_stripe(n);  // rows per stripe (8 for several bands: compact 8x8 tiles)
+    const uint32_t S = band_stripe(n);  // rows per stripe (single rows unless RTX_STRIPE says otherwise)
     rtx_region reg0{0, 0, W, H, 0, (uint32_t)n, S};
     const uint32_t R = region_rows(&reg0);  // rows of band 0, the longest: every band is sent padded to R
     const size_t band_floats = (size_t)R * W * 3, band_bytes = std::max<size_t>(band_floats, 1) * sizeof(float);

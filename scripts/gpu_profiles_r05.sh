@@ -19,9 +19,9 @@ add cornell "cornell_box:600x600x200" "--scene cornell_box --width 600 --spp 200
 add quad "quad_demo:400x225x100" "--scene quad_demo --width 400 --spp 100"
 add perlin "perlin_demo:400x225x100" "--scene perlin_demo --width 400 --spp 100"
 add light "simple_light_demo:400x225x500" "--scene simple_light_demo --width 400 --spp 500"
-add c2_r0of2 "random_spheres:1920x1080x500/rows0of2/stripe8" "--shard 0/2"
-add c2_r0of4 "random_spheres:1920x1080x500/rows0of4/stripe8" "--shard 0/4"
-add c2_r0of8 "random_spheres:1920x1080x500/rows0of8/stripe8" "--shard 0/8"
+add c2_r0of2 "random_spheres:1920x1080x500/rows0of2" "--shard 0/2"
+add c2_r0of4 "random_spheres:1920x1080x500/rows0of4" "--shard 0/4"
+add c2_r0of8 "random_spheres:1920x1080x500/rows0of8" "--shard 0/8"
 [ -n "$ONLY" ] && { for i in "${!NAMES[@]}"; do [[ " $ONLY " == *" ${NAMES[$i]} "* ]] || unset 'NAMES[i]'; done; }
 rc=0
 for i in "${!NAMES[@]}"; do

@@ -106,5 +106,4 @@ def test_shard_run_renders_its_rows():
     the metric says so, and the roofline looks up that shard's own profile."""
     got = _bench_line(["--shard", "1/3", "--width", "192", "--spp", "8", "--steps", "1", "--warmup", "0", "--no-cpu"])
     assert got["metric"].startswith("shard 1/3")
-    # (8-row stripes by default, DESIGN.md §19: the profile of that layout)
-    assert got["roofline"]["workload"].endswith("/rows1of3/stripe8") and "rank 1's kernel" in got["roofline"]["scope"]
+    assert got["roofline"]["workload"].endswith("/rows1of3") and "rank 1's kernel" in got["roofline"]["scope"]

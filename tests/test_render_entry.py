@@ -134,15 +134,16 @@ def test_watchdog_stops_v3(built):
     assert f"ERR {rtx.RTX_ERR_HIP}" in out and "next render ok" in out, out
 
 
-@pytest.mark.parametrize("bands", [2, 3, 5, 7])
-def test_band_assembly_index_math_one_gpu(built, bands):
-    """The n > 1 assembly on one GPU (RTX_SIM_BANDS=k: k bands of 8-row stripes dealt round-robin, rendered on
-    device 0, each padded to band 0's rows, placed at band offsets as the RCCL gather places them,
-    de-interleaved by the kernel; with RTX_NO_RCCL=1 each band's stripes copied straight into the caller's
-    rows instead).  H = 112 = 14 stripes: 3, 5 and 7 bands get unequal stripe counts."""
+@pytest.mark.parametrize("bands,stripe", [(2, 1), (3, 1), (5, 1), (7, 1), (3, 8), (5, 8), (2, 4)])
+def test_band_assembly_index_math_one_gpu(built, bands, stripe):
+    """The n > 1 assembly on one GPU (RTX_SIM_BANDS=k: k bands rendered on device 0 — single rows interleaved, or
+    stripes of RTX_STRIPE rows dealt round-robin —, each padded to band 0's rows, placed at band offsets as the RCCL
+    gather places them, de-interleaved by the kernel; with RTX_NO_RCCL=1 each band's rows (stripes) copied straight
+    into the caller's rows instead).  H = 112: ragged last bands, and 14 stripes of 8 for 3 and 5 bands."""
     out = child(
         f"k = {bands}\n"
         "import os\n"
+        f"os.environ['RTX_STRIPE'] = '{stripe}'\n"
         "s = rtx.HostScene('random_spheres', 1); d = rtx.DeviceScene(s.desc)\n"
         "cam = s.camera(width=200, spp=3)\n"
         "assert cam.image_height == 112\n"
