@@ -83,6 +83,7 @@ struct Scratch {
     size_t bytes = 0;
     float4* defer = nullptr;  // the tiered walk's queue of deferred paths (64 B per record)
     size_t defer_bytes = 0;
+    uint32_t* drain = nullptr;  // the near pass's drain: a record count and a unit cursor per workgroup (Params::drain_count)
     uint32_t* redo = nullptr;  // the tiered walk's redo bits: one per sample of a chunk
     size_t redo_bytes = 0;
     size_t redo_zero = 0;      // bytes at the start of `redo` known to be zero (clear_redo_bits keeps them so)
@@ -159,6 +160,7 @@ void release_scratch_locked(int device) {
         if (sc.ptr) (void)hipFree(sc.ptr);
         if (sc.defer) (void)hipFree(sc.defer);
         if (sc.redo) (void)hipFree(sc.redo);
+        if (sc.drain) (void)hipFree(sc.drain);
         if (sc.last) (void)hipEventDestroy(sc.last);
     }
     (void)hipSetDevice(cur);
@@ -1043,6 +1045,10 @@ int enqueue_on(rtx_scene* s, DeviceCopy* c, const rtx_camera* cam, uint64_t seed
             pn.redo_count = p.redo_count = reinterpret_cast<uint32_t*>(c->counters + 25);
             pn.defer_cap = p.defer_cap = (uint32_t)cap;
             pn.defer_count = p.defer_count = reinterpret_cast<uint32_t*>(c->counters + 22);  // low: records
+            // the drain's per-workgroup words: 2 x the near grid (launch_tiered drains only when they fit)
+            if (!scr->drain) HIP_TRY(hipMalloc(&scr->drain, rtxd::DRAIN_WORDS * sizeof(uint32_t)));
+            pn.drain_count = p.drain_count = scr->drain;
+            pn.drain = p.drain = env_knob("RTX_DRAIN", 1, 0, 1);
             std::memcpy(pn.near_min, s->near_topo.near_box, 3 * sizeof(float));
             std::memcpy(pn.near_max, s->near_topo.near_box + 3, 3 * sizeof(float));
             *tiered = true;

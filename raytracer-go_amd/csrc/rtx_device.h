@@ -493,7 +493,16 @@ struct Params {
     // (last: the fields before it keep their kernel-argument offsets) a striped shard (rtx_region.stripe = 2^s > 1):
     // shard row lr is image row y0 + (((lr >> s) * world + rank) << s) + (lr & (2^s - 1)); render_items<ST>
     uint32_t stripe_log2;
+    // The near pass's drain (render_drain): each workgroup of the near pass writes its records to a
+    // region of its own, drain_region slots from blockIdx.x * drain_region, counted in drain_count[blockIdx.x], and
+    // once its waves have no near work left it resumes them itself (its far phase), claiming units of 64 records
+    // from drain_count[gridDim.x + blockIdx.x].  The far pass's launch is gone: a workgroup whose near work ends
+    // early walks its far records while the others still render, and the long paths of the far tree start then.
+    uint32_t* drain_count;   // 2 x the near grid, zeroed per chunk
+    uint32_t drain_region;   // records per workgroup (the queue's capacity over the near grid)
+    uint32_t drain;          // 1: the timed tiered render drains (RTX_DRAIN=0: the far pass's own launch, A/B)
 };
+constexpr uint32_t DRAIN_WORDS = 16384;  // Params::drain_count's words: near grids up to 8192 workgroups
 
 // The camera-ray pool of render_items<POOL>: after the fixed layout's scene copy (16-B aligned), 64 rays
 // of 2 float4 per wave (2 KB).

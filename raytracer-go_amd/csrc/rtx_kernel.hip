@@ -228,10 +228,15 @@ __device__ __forceinline__ void split_clk(uint64_t& acc, uint64_t& clk) {
 // ST: the region's shard is in stripes of 2^stripe_log2 > 1 rows; the image row of a tile row comes from
 // a per-unit base.  Single-row shards (every one-GPU render) run the ST = false instantiation, whose row arithmetic is
 // the one before stripes existed (its code unchanged: the headline kernel).
-template <bool COUNT, bool USE_LDS, bool QUADS, bool NOISE, int WAVES = 8, int MINW = 0, bool HYB = false,
-          bool CLK = false, int TIER = 0, bool POOL = false, bool ST = false>
-__global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
+//
+// DRAIN (render_drain): TIER 1 writes the records to the workgroup's own region of the queue
+// (Params::drain_count, drain_region); TIER 2 resumes that region's records only, its units claimed by the
+// workgroup's waves.
+template <bool COUNT, bool USE_LDS, bool QUADS, bool NOISE, int WAVES, bool HYB, bool CLK, int TIER, bool POOL, bool ST,
+          bool DRAIN>
+__device__ __forceinline__ void render_body(const Params& p) {
     constexpr bool TIME = COUNT || CLK;
+    static_assert(!DRAIN || (!COUNT && !CLK && (TIER == 1 || TIER == 2)), "the drain: the timed near and far passes");
     static_assert(!POOL || (USE_LDS && (TIER == 0 || TIER == 1)), "the camera-ray pool: LDS scenes, near pass or one walk");
     if constexpr (TIER == 3) {
         if (__builtin_amdgcn_readfirstlane(*(volatile uint32_t*)p.redo_count) == 0u) return;
@@ -284,14 +289,18 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
     const uint32_t n_tiles = tiles_x * tiles_y_of(p.rows, twl);
     const uint32_t nsub = (p.kn + p.sub - 1u) / p.sub;
     // far pass: units of 64 queue records
-    const uint32_t n_rec = TIER == 2 ? min(__builtin_amdgcn_readfirstlane(*(volatile uint32_t*)p.defer_count), p.defer_cap)
-                                     : 0u;
+    // (DRAIN: this workgroup's records, written by its own waves before the barrier that ended its near phase)
+    const uint32_t n_rec =
+        TIER == 2 ? (DRAIN ? min(__builtin_amdgcn_readfirstlane(*(volatile uint32_t*)(p.drain_count + blockIdx.x)),
+                                 p.drain_region)
+                           : min(__builtin_amdgcn_readfirstlane(*(volatile uint32_t*)p.defer_count), p.defer_cap))
+                  : 0u;
     // redo pass: the compacted list of flagged samples when it held them all (else the bits, unit by unit)
     const uint32_t n_ids = TIER == 3 ? __builtin_amdgcn_readfirstlane(*(volatile uint32_t*)p.redo_count) : 0u;
     const bool listed = TIER == 3 && n_ids <= p.redo_cap;
     const uint64_t n_units = TIER == 2 ? (uint64_t)((n_rec + 63u) / 64u)
                                        : (listed ? (uint64_t)((n_ids + 63u) / 64u) : (uint64_t)n_tiles * nsub);
-    if (TIER == 2 && blockIdx.x == 0 && threadIdx.x == 0 && n_rec)
+    if (TIER == 2 && (DRAIN || blockIdx.x == 0) && threadIdx.x == 0 && n_rec)
         atomicAdd(&p.counters[23], (unsigned long long)n_rec);  // deferred paths, all chunks
     const size_t tile_floats = (size_t)n_tiles * 64 * 3;  // one sample of every tile (tile-major scratch)
     const uint64_t* const redo64 = reinterpret_cast<const uint64_t*>(p.redo_bits);  // redo pass: 64 slots a word
@@ -347,13 +356,13 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
             return;
         }
         uint32_t b = 0;
-        if (lane == 0) b = atomicAdd(p.defer_count, (uint32_t)__popcll(fm));
+        if (lane == 0) b = atomicAdd(DRAIN ? p.drain_count + blockIdx.x : p.defer_count, (uint32_t)__popcll(fm));
         b = __builtin_amdgcn_readfirstlane(b);
         bool full = false;
         if (far) {
             const uint32_t slot = b + (uint32_t)__popcll(fm & ((1ull << lane) - 1ull));
-            if (slot < p.defer_cap) {
-                float4* q = p.defer + 4 * (size_t)slot;
+            if (slot < (DRAIN ? p.drain_region : p.defer_cap)) {
+                float4* q = p.defer + 4 * ((DRAIN ? (size_t)blockIdx.x * p.drain_region : 0) + slot);
                 q[0] = make_float4(r.o.x, r.o.y, r.o.z, __uint_as_float(rng.pixel));
                 q[1] = make_float4(r.d.x, r.d.y, r.d.z, __uint_as_float(rng.sample));
                 q[2] = make_float4(thr.x, thr.y, thr.z, __uint_as_float(seg));
@@ -475,7 +484,7 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
                 exhausted = true;  // (debug library: the even lanes reach the claim alone)
             } else if (cursor >= u_items && !exhausted) {  // claim the next unit (wave-uniform)
                 uint32_t un = 0;
-                if (lane == 0) un = atomicAdd(p.tile_counter, 1u);
+                if (lane == 0) un = atomicAdd(DRAIN && TIER == 2 ? p.drain_count + gridDim.x + blockIdx.x : p.tile_counter, 1u);
                 uint32_t uu = __builtin_amdgcn_readfirstlane(un);  // the whole wave is here: lane 0's
                 if (partial_wave()) {  // else: the wave stops (exhausted) and the render fails
                     RTX_SET_KERR();
@@ -528,7 +537,7 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
             bool got = false;
             uint32_t pool_draws = 0;  // COUNT, POOL: the draws of the ray the lane takes
             if (TIER == 2 && mode == M_CLAIM && rank < avail) {  // resume a record
-                const float4* q = p.defer + 4 * (size_t)(u_k0 + cursor + rank);
+                const float4* q = p.defer + 4 * ((DRAIN ? (size_t)blockIdx.x * p.drain_region : 0) + u_k0 + cursor + rank);
                 const float4 q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3];
                 r = Ray{v3(q0.x, q0.y, q0.z), v3(q1.x, q1.y, q1.z)};
                 rng.pixel = __float_as_uint(q0.w);
@@ -621,6 +630,53 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
         }
         atomicAdd(&p.counters[13], (unsigned long long)shade_cycles);
     }
+}
+
+template <bool COUNT, bool USE_LDS, bool QUADS, bool NOISE, int WAVES = 8, int MINW = 0, bool HYB = false,
+          bool CLK = false, int TIER = 0, bool POOL = false, bool ST = false>
+__global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
+    render_body<COUNT, USE_LDS, QUADS, NOISE, WAVES, HYB, CLK, TIER, POOL, ST, false>(p);
+}
+
+// The timed tiered render's near pass with its drain: the near phase (pn, the near tree, records to the
+// workgroup's region), then — once all the workgroup's waves are out of near work — its far phase over those records
+// (pf, the far tree, copied into the same LDS).  A workgroup whose near work ends early walks its far paths while
+// others still render, so the far tree's long paths no longer wait for the last near wave, nor for a second launch.
+// The far phase's own settings (the rest of its Params are the near pass's): its layout and walk knobs.
+struct FarLayout {
+    const float4* entries;
+    uint32_t n_entries, n_hot, start, prim_end, shade_thresh, refill_hits, prim_batch;
+};
+inline FarLayout far_layout(const Params& pf) {
+    return FarLayout{pf.entries, pf.n_entries, pf.n_hot, pf.start, pf.prim_end, pf.shade_thresh, pf.refill_hits, pf.prim_batch};
+}
+
+struct DrainArgs {
+    Params pn;
+    FarLayout fl;
+};
+
+template <bool USE_LDS, int WAVES, int MINW, bool HYB, bool POOL, bool ST>
+__global__ __launch_bounds__(64 * WAVES, MINW) void render_drain(DrainArgs a) {
+    render_body<false, USE_LDS, false, false, WAVES, HYB, false, 1, POOL, ST, true>(a.pn);
+    __syncthreads();  // every wave's near work and records done: the far phase overwrites the scene copy
+    // The far phase reads its settings from the kernel arguments afresh, through an opaque copy of their address:
+    // values it shares with the near phase are then not kept live through the near phase (which spilled 4 more VGPRs).
+    typedef const __attribute__((address_space(4))) DrainArgs* KArgs;
+    KArgs ka = (KArgs)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(ka));
+    const DrainArgs& k = *(const DrainArgs*)ka;
+    Params pf = k.pn;
+    pf.entries = k.fl.entries;
+    pf.n_entries = k.fl.n_entries;
+    pf.n_hot = k.fl.n_hot;
+    pf.start = k.fl.start;
+    pf.prim_end = k.fl.prim_end;
+    pf.shade_thresh = k.fl.shade_thresh;
+    pf.refill_hits = k.fl.refill_hits;
+    pf.prim_batch = k.fl.prim_batch;
+    pf.tier = 2;
+    render_body<false, USE_LDS, false, false, WAVES, HYB, false, 2, false, false, true>(pf);
 }
 
 // The redo list overflowed (more samples than p.redo_cap): its ids join the ones the near pass set in
@@ -781,6 +837,17 @@ hipError_t launch_tiered(Params pn, Params pf, hipStream_t stream) {
     if (e == hipSuccess) e = resident_grid((const void*)kf, block, sf, &per_f, &cus);
     if (e == hipSuccess) e = resident_grid((const void*)kr, block, sf, &per_r, &cus);
     if (e != hipSuccess) return e;
+    // The drain (render_drain, the timed kernels): the near grid's workgroups resume their own records in the
+    // same LDS (the larger of the two layouts), when that keeps the near pass's occupancy.
+    // (Not for a scene in HBM with LDS caches: the combined kernel spilled 24 VGPRs there, and config 4 took +2.3 %.)
+    constexpr bool CAN_DRAIN = !COUNT && !CLK && !HYB;
+    const void* kd = nullptr;
+    if constexpr (CAN_DRAIN) kd = (const void*)render_drain<USE_LDS, WN, MINW, HYB, POOL, ST>;
+    const size_t sd = sn > sf ? sn : sf;
+    int per_d = 0;
+    bool drain = CAN_DRAIN && pn.drain && pn.drain_count;
+    if (drain && (e = resident_grid(kd, block_n, sd, &per_d, &cus)) != hipSuccess) return e;
+    drain = drain && per_d >= per_n;
     const uint32_t spp = pn.cam.samples_per_pixel, chunk = pn.kn, sub = pn.sub;
     const uint64_t tiles = (uint64_t)tiles_x_of(pn.width, pn.tile_w_log2) * tiles_y_of(pn.rows, pn.tile_w_log2);
     const uint64_t slots = tiles * 64;
@@ -797,16 +864,24 @@ hipError_t launch_tiered(Params pn, Params pf, hipStream_t stream) {
         if (br > (units + WAVES - 1) / WAVES) br = (units + WAVES - 1) / WAVES;
         if (pn.debug_launch)
             fprintf(stderr, "rtx tiered: waves/wg %d / %d, wgs/CU %d / %d / %d, grid %llu, sub %u, units %llu, lds %zu / %zu B, "
-                    "cap %u, camera-ray pool %d\n", WN, WAVES, per_n, per_f, per_r, (unsigned long long)bn, pn.sub,
-                    (unsigned long long)units, sn, sf, pn.defer_cap, (int)POOL);
+                    "cap %u, camera-ray pool %d, drain %d\n", WN, WAVES, per_n, per_f, per_r, (unsigned long long)bn, pn.sub,
+                    (unsigned long long)units, sn, sf, pn.defer_cap, (int)POOL, (int)drain);
         // the unit queue head, the chunk's record count, its redo list count (the redo bits are zero:
         // the caller zeroes them once, clear_redo_bits after every chunk that set any)
         if ((e = hipMemsetAsync(pn.tile_counter, 0, sizeof(uint32_t), stream)) != hipSuccess) return e;
         if ((e = hipMemsetAsync(pn.defer_count, 0, sizeof(uint32_t), stream)) != hipSuccess) return e;
         if ((e = hipMemsetAsync(pn.redo_count, 0, sizeof(uint32_t), stream)) != hipSuccess) return e;
-        hipLaunchKernelGGL(kn, dim3((uint32_t)bn), dim3(block_n), sn, stream, pn);
-        if ((e = hipMemsetAsync(pf.tile_counter, 0, sizeof(uint32_t), stream)) != hipSuccess) return e;
-        hipLaunchKernelGGL(kf, dim3((uint32_t)per_f * cus), dim3(block), sf, stream, pf);
+        if (drain && 2 * bn <= DRAIN_WORDS) {  // each workgroup's region: the queue over the near grid (a region that fills sends the rest to the redo pass)
+            pn.drain_region = pf.drain_region = pn.defer_cap / (uint32_t)bn;
+            if ((e = hipMemsetAsync(pn.drain_count, 0, 2 * bn * sizeof(uint32_t), stream)) != hipSuccess) return e;
+            if constexpr (CAN_DRAIN)
+                hipLaunchKernelGGL((render_drain<USE_LDS, WN, MINW, HYB, POOL, ST>), dim3((uint32_t)bn), dim3(block_n), sd,
+                                   stream, DrainArgs{pn, far_layout(pf)});
+        } else {
+            hipLaunchKernelGGL(kn, dim3((uint32_t)bn), dim3(block_n), sn, stream, pn);
+            if ((e = hipMemsetAsync(pf.tile_counter, 0, sizeof(uint32_t), stream)) != hipSuccess) return e;
+            hipLaunchKernelGGL(kf, dim3((uint32_t)per_f * cus), dim3(block), sf, stream, pf);
+        }
         hipLaunchKernelGGL(spill_redo_list, dim3((uint32_t)cus * 4), dim3(256), 0, stream, pn);
         if ((e = hipMemsetAsync(pr.tile_counter, 0, sizeof(uint32_t), stream)) != hipSuccess) return e;
         hipLaunchKernelGGL(kr, dim3((uint32_t)br), dim3(block), sf, stream, pr);

@@ -515,3 +515,32 @@ def test_tile_shapes(torch_cuda, spheres, dev_spheres, monkeypatch, tile_w):
     for rank in range(4):
         check_scene(torch_cuda, dev_spheres, spheres.desc, cam, 31, rtx.Region(3, 5, 101, 61, rank, 4),
                     kernels=("timed",))
+
+
+@pytest.mark.parametrize("world,rank,cap", [(1, 0, None), (8, 3, None), (1, 0, "3000")])
+def test_drain_matches_far_launch(torch_cuda, spheres, dev_spheres, monkeypatch, capfd, world, rank, cap):
+    """The near pass's drain (render_drain, DESIGN.md §21: each workgroup writes its records to a region of its
+    own and resumes them itself once its near work is done) against the far pass's own launch (RTX_DRAIN=0): the
+    same frame, bit for bit, equal to the oracle's; the same deferred paths when no region fills.  With a small
+    queue (RTX_DEFER_CAP: regions of a few records) the records that do not fit take the redo pass, still exact.
+    The launch line (RTX_DEBUG_LAUNCH) shows that the drain ran."""
+    if cap is not None:
+        monkeypatch.setenv("RTX_DEFER_CAP", cap)
+    cam = spheres.camera(width=320, spp=16, depth=50)
+    reg = rtx.Region(0, 0, cam.image_width, cam.image_height, rank, world)
+    monkeypatch.setenv("RTX_DEBUG_LAUNCH", "1")
+    capfd.readouterr()
+    got, st = gpu_region(torch_cuda, dev_spheres, cam, 9, reg, counters=False)
+    launch = capfd.readouterr().err
+    assert "drain 1" in launch, launch
+    monkeypatch.setenv("RTX_DRAIN", "0")
+    want, st0 = gpu_region(torch_cuda, dev_spheres, cam, 9, reg, counters=False)
+    assert "drain 0" in capfd.readouterr().err
+    assert st.walk_layout & rtx.RTX_LAYOUT_TIERED
+    assert np.array_equal(got, want), int((got != want).any(axis=2).sum())
+    it, _ = ob.render(spheres.desc, cam, 9, reg, ob.ORDER_ITERATIVE)
+    assert np.array_equal(got, it)
+    if cap is None:
+        assert st.redo_chunks == 0 and st.deferred_paths == st0.deferred_paths > 0, (st.deferred_paths, st0.deferred_paths)
+    else:
+        assert st.redo_chunks == 1 and st.deferred_paths < st0.deferred_paths
