@@ -18,7 +18,8 @@ import os
 ap = argparse.ArgumentParser()
 ap.add_argument("pmc_dir")
 ap.add_argument("--workload", required=True)
-ap.add_argument("--kernel", default="render_items<false")
+ap.add_argument("--kernel", default="render_items<false,render_drain<",
+                help="comma-separated kernel-name substrings (the render's passes; render_drain: near + far, DESIGN.md §21)")
 ap.add_argument("--out")
 args = ap.parse_args()
 
@@ -26,14 +27,14 @@ v = {}
 for f in glob.glob(os.path.join(args.pmc_dir, "**", "*counter_collection.csv"), recursive=True):
     with open(f) as fh:
         for r in csv.DictReader(fh):
-            if args.kernel in r["Kernel_Name"]:
+            if any(k in r["Kernel_Name"] for k in args.kernel.split(",")):
                 v.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
 c = {k: sum(x) / len(x) for k, x in v.items()}  # mean over the passes' launches
 kname = None
 for f in glob.glob(os.path.join(args.pmc_dir, "**", "*kernel_trace.csv"), recursive=True):
     with open(f) as fh:
         for r in csv.DictReader(fh):
-            if args.kernel in r["Kernel_Name"]:
+            if any(k in r["Kernel_Name"] for k in args.kernel.split(",")):
                 kname = r["Kernel_Name"]
 clk = c["GRBM_GUI_ACTIVE"] / 8.0
 out = {

@@ -22,7 +22,8 @@ ap = argparse.ArgumentParser()
 ap.add_argument("pmc_dir")
 ap.add_argument("out")
 ap.add_argument("--workload", required=True)
-ap.add_argument("--kernel", default="render_items<false")
+ap.add_argument("--kernel", default="render_items<false,render_drain<",
+                help="comma-separated kernel-name substrings (the render's passes; render_drain: near + far, DESIGN.md §21)")
 ap.add_argument("--lib", default=os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                                               "raytracer-go_amd", "librtx.so"),
                 help="the library the profiled run loaded: its hash ties the profile to the code (bench.py checks it)")
@@ -37,7 +38,7 @@ vals = {"FETCH_SIZE": {}, "WRITE_SIZE": {}}
 for f in glob.glob(os.path.join(args.pmc_dir, "**", "*counter_collection.csv"), recursive=True):
     with open(f) as fh:
         for r in csv.DictReader(fh):
-            if args.kernel in r["Kernel_Name"] and r["Counter_Name"] in vals:
+            if any(k in r["Kernel_Name"] for k in args.kernel.split(",")) and r["Counter_Name"] in vals:
                 vals[r["Counter_Name"]].setdefault(r["Kernel_Name"], []).append(float(r["Counter_Value"]))
 assert vals["FETCH_SIZE"] and vals["WRITE_SIZE"], f"no {args.kernel} rows with FETCH_SIZE/WRITE_SIZE under {args.pmc_dir}"
 agg = (lambda v: sum(v) / args.renders) if args.renders else statistics.median

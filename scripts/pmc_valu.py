@@ -18,7 +18,8 @@ ap = argparse.ArgumentParser()
 ap.add_argument("pmc_dir")
 ap.add_argument("out")
 ap.add_argument("--workload", required=True)
-ap.add_argument("--kernel", default="render_items<false")
+ap.add_argument("--kernel", default="render_items<false,render_drain<",
+                help="comma-separated kernel-name substrings (the render's passes; render_drain: near + far, DESIGN.md §21)")
 ap.add_argument("--simds", type=int, default=1024)
 ap.add_argument("--lib", default=os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                                               "raytracer-go_amd", "librtx.so"),
@@ -36,7 +37,7 @@ need = ["SQ_INSTS_VALU", "GRBM_GUI_ACTIVE", "SQ_THREAD_CYCLES_VALU"]
 vals, disp = {}, {}
 for f in sorted(glob.glob(os.path.join(args.pmc_dir, "**", "*counter_collection.csv"), recursive=True)):
     with open(f) as fh:
-        rows = [r for r in csv.DictReader(fh) if args.kernel in r["Kernel_Name"]]
+        rows = [r for r in csv.DictReader(fh) if any(k in r["Kernel_Name"] for k in args.kernel.split(","))]
     if not all(any(r["Counter_Name"] == k for r in rows) for k in need):
         continue
     for r in rows:
