@@ -815,6 +815,9 @@ int check_camera(const rtx_camera* cam) {
     if (cam->samples_per_pixel == 0) return fail(RTX_ERR_INVALID_ARG, "samples_per_pixel must be > 0");
     if ((uint64_t)cam->image_width * cam->image_height > 0xFFFFFFFFull)
         return fail(RTX_ERR_INVALID_ARG, "image has more than 2^32 pixels (RNG counter is 32-bit)");
+    // the kernel's scratch slot of a pixel (64 per tile, tiles padded: at most 64 columns and 64 rows) is 32-bit
+    if ((uint64_t)(cam->image_width + 64) * (cam->image_height + 64) > 0xFFFFFFFFull)
+        return fail(RTX_ERR_INVALID_ARG, "image too large: its padded tiles exceed 2^32 pixel slots");
     return RTX_OK;
 }
 

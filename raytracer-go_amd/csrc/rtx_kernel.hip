@@ -323,7 +323,7 @@ __device__ __forceinline__ void render_body(const Params& p) {
 #define RTX_KERR() ((iter & 0x80000000u) != 0u)
 
     uint32_t mode = M_CLAIM, seg = 0, items_done = 0;
-    size_t pix = 0;  // the lane's item in the tile-major scratch: 64 * tile + pixel within the tile
+    uint32_t pix = 0;  // the lane's item in the tile-major scratch: 64 * tile + pixel within the tile (< 2^32: rtx_capi)
     V3 base = v3(0.0f, 0.0f, 0.0f);
     V3 thr = v3(1.0f, 1.0f, 1.0f), acc = v3(0.0f, 0.0f, 0.0f);
     Ray r{v3(0, 0, 0), v3(0, 0, 0)};
@@ -337,7 +337,7 @@ __device__ __forceinline__ void render_body(const Params& p) {
     uint64_t split[4] = {0, 0, 0, 0};  // COUNT: shading-phase cycles: scatter, shade, claims + camera rays, trav_begin
 
     auto store = [&](V3 col) {  // the item's colour, GetColor's result for sample k
-        float* o = p.scratch + (size_t)(rng.sample - p.k0) * tile_floats + pix * 3;
+        float* o = p.scratch + (size_t)(rng.sample - p.k0) * tile_floats + (size_t)pix * 3;
         o[0] = col.x;
         o[1] = col.y;
         o[2] = col.z;
@@ -366,7 +366,7 @@ __device__ __forceinline__ void render_body(const Params& p) {
                 q[0] = make_float4(r.o.x, r.o.y, r.o.z, __uint_as_float(rng.pixel));
                 q[1] = make_float4(r.d.x, r.d.y, r.d.z, __uint_as_float(rng.sample));
                 q[2] = make_float4(thr.x, thr.y, thr.z, __uint_as_float(seg));
-                q[3] = make_float4(acc.x, acc.y, acc.z, __uint_as_float((uint32_t)pix));
+                q[3] = make_float4(acc.x, acc.y, acc.z, __uint_as_float(pix));
             } else {
                 full = true;
             }
@@ -387,7 +387,7 @@ __device__ __forceinline__ void render_body(const Params& p) {
         b2 = __builtin_amdgcn_readfirstlane(b2);
         if (full) {
             const uint32_t at = b2 + (uint32_t)__popcll(om & ((1ull << lane) - 1ull));
-            const uint32_t id = (rng.sample - p.k0) * n_tiles * 64u + (uint32_t)pix;
+            const uint32_t id = (rng.sample - p.k0) * n_tiles * 64u + pix;
             if (at < p.redo_cap) p.redo_ids[at] = id;
             else atomicOr(p.redo_bits + (id >> 5), 1u << (id & 31u));
             if (COUNT) cnt = path0;
@@ -580,7 +580,7 @@ __device__ __forceinline__ void render_body(const Params& p) {
                     }
                     rng.pixel = y * c.image_width + x;
                     rng.sample = k;
-                    pix = slot;
+                    pix = (uint32_t)slot;
                     got = true;
                 }
             }
@@ -751,8 +751,11 @@ constexpr uint32_t LDS_MAX_BYTES = 64 * 1024;
 // image's last units would run on a near-empty GPU).  Measured at 100 spp: 1920x1080 8 -1.6 % vs
 // 16; 400x225 2 -42 % vs 16; Cornell 600x600 8 -3 % vs 16.  16 when that still leaves >= 64
 // units per wave (the drain stays short): 1920x1080x500 -0.9 % vs 8 (142.5 vs 143.8 ms).
-inline uint32_t unit_samples(uint64_t tiles, uint32_t kn, int waves, int per_cu, int cus) {
+// TIERED (the tiered walk, whose timed near pass drains: DESIGN.md §21): 4 instead of 2 below 8 units of 8 samples per resident wave
+// (C1 400x225x100: 1.68 ms against 1.77 at 2 and 1.77 at 8; profiles/r05_unit_sweep.jsonl).
+inline uint32_t unit_samples(uint64_t tiles, uint32_t kn, int waves, int per_cu, int cus, bool tiered = false) {
     const uint64_t per_wave = tiles * kn / (8ull * waves * (uint64_t)per_cu * cus);
+    if (tiered && per_wave >= 2 && per_wave < 8) return 4u;
     return per_wave >= 128 ? RTX_SUB_MAX : (per_wave >= 8 ? 8u : (per_wave >= 4 ? 4u : (per_wave >= 2 ? 2u : 1u)));
 }
 
@@ -856,7 +859,7 @@ hipError_t launch_tiered(Params pn, Params pf, hipStream_t stream) {
     for (uint32_t k0 = 0; k0 < spp; k0 += chunk) {
         pn.k0 = pf.k0 = pr.k0 = k0;
         pn.kn = pf.kn = pr.kn = spp - k0 < chunk ? spp - k0 : chunk;
-        pn.sub = sub ? sub : unit_samples(tiles, pn.kn, WN, per_n, cus);
+        pn.sub = sub ? sub : unit_samples(tiles, pn.kn, WN, per_n, cus, true);
         pf.sub = pr.sub = pn.sub;
         const uint64_t units = tiles * ((pn.kn + pn.sub - 1) / pn.sub);
         uint64_t bn = (uint64_t)per_n * cus, br = (uint64_t)per_r * cus;
