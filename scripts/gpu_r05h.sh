@@ -5,7 +5,7 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-OUT="$PWD/gpurun_out/r05h"; mkdir -p "$OUT"
+OUT="$PWD/gpurun_out/${FFP_TAG:-r05h}"; mkdir -p "$OUT"
 for s in 0/8 0/4; do
   t=${s/\//of}
   timeout -s KILL 200 rocprofv3 --kernel-trace --stats -d "$OUT/trace_$t" -o run --output-format csv -- python bench.py --no-cpu --shard $s \
