@@ -544,3 +544,27 @@ def test_drain_matches_far_launch(torch_cuda, spheres, dev_spheres, monkeypatch,
         assert st.redo_chunks == 0 and st.deferred_paths == st0.deferred_paths > 0, (st.deferred_paths, st0.deferred_paths)
     else:
         assert st.redo_chunks == 1 and st.deferred_paths < st0.deferred_paths
+
+
+def test_tier_chunk_at_id_limit(torch_cuda, spheres, dev_spheres, monkeypatch):
+    """A tiered chunk as large as the 32-bit sample ids allow (the advisor's round-4 item): the redo list's ids and the
+    redo bits index (k - k0) x slots + slot in 32 bits, so rtx_render clamps a tiered chunk to 2^32 scratch slots.  A
+    64 x 36 window has 2560 slots: with a 60 GB scratch budget the chunk is 1 677 721 samples (2^32 / 2560), so
+    1 677 758 samples per pixel run in 2 chunks and the first one's last ids are just below 2^32.  With the queue and
+    the redo list starved (RTX_DEFER_CAP 1000, RTX_REDO_CAP 100) the deferred samples of those ids go through the redo
+    bits and are rendered again: the frame equals the one with room, bit for bit.  (4.3e9 samples a render, ~57 GB of
+    device memory, freed at the end.)"""
+    monkeypatch.setenv("RTX_SCRATCH_MB", "60000")
+    cam = spheres.camera(width=1920, spp=1677721 + 37, depth=50)
+    reg = rtx.Region(900, 600, 64, 36, 0, 1)
+    try:
+        want, st0 = gpu_region(torch_cuda, dev_spheres, cam, 5, reg, counters=False)
+        assert st0.sample_chunks == 2 and st0.walk_layout & rtx.RTX_LAYOUT_TIERED, (st0.sample_chunks, st0.walk_layout)
+        assert st0.redo_chunks == 0 and st0.deferred_paths > 1000
+        monkeypatch.setenv("RTX_DEFER_CAP", "1000")
+        monkeypatch.setenv("RTX_REDO_CAP", "100")
+        got, st = gpu_region(torch_cuda, dev_spheres, cam, 5, reg, counters=False)
+        assert st.sample_chunks == 2 and st.redo_chunks >= 1, (st.sample_chunks, st.redo_chunks)
+        assert np.isfinite(got).all() and np.array_equal(got, want), int((got != want).any(axis=2).sum())
+    finally:
+        rtx.release_device_memory(0)
