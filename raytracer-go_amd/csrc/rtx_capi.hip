@@ -86,7 +86,7 @@ struct Scratch {
     uint32_t* drain = nullptr;  // the near pass's drain: a record count and a unit cursor per workgroup (Params::drain_count)
     uint32_t* redo = nullptr;  // the tiered walk's redo bits: one per sample of a chunk
     size_t redo_bytes = 0;
-    size_t redo_zero = 0;      // bytes at the start of `redo` known to be zero (clear_redo_bits keeps them so)
+    size_t redo_zero = 0;      // bytes at the start of `redo` known to be zero (reduce_samples keeps them so)
     hipEvent_t last = nullptr;
     int scenes = 0;
 };
@@ -1016,7 +1016,7 @@ int enqueue_on(rtx_scene* s, DeviceCopy* c, const rtx_camera* cam, uint64_t seed
                 HIP_TRY(hipMalloc(&scr->redo, 2 * bits));
                 scr->redo_bytes = 2 * bits;
             }
-            // The bits [0, bits) must be zero at the first chunk's start; clear_redo_bits keeps them so after
+            // The bits [0, bits) must be zero at the first chunk's start; reduce_samples keeps them so after
             // every chunk.  Past them this render's redo list may leave ids, so only [0, bits) stays known zero.
             if (scr->redo_zero < bits) HIP_TRY(hipMemsetAsync(scr->redo, 0, bits, stream));
             scr->redo_zero = bits;

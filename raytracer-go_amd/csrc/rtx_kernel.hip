@@ -689,16 +689,18 @@ __global__ __launch_bounds__(256) void spill_redo_list(Params p) {
     }
 }
 
-// The redo bits are set only when the list overflowed (redo_count > redo_cap: by the near pass past
-// the list's end, and by spill_redo_list); after the redo pass has read them, this clears the chunk's
-// bits again, so they are zero at every chunk's start without a memset of the whole bitmap per chunk
-// (130 MB at C2, ~180 MB at C5).  A return when the list held every id.
-__global__ __launch_bounds__(256) void clear_redo_bits(Params p) {
-    if (__builtin_amdgcn_readfirstlane(*(volatile uint32_t*)p.redo_count) <= p.redo_cap) return;
-    const uint32_t twl = p.tile_w_log2;
-    const uint64_t words = (uint64_t)p.kn * tiles_x_of(p.width, twl) * tiles_y_of(p.rows, twl) * 2;  // 64 bits a tile
-    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < words; i += (uint64_t)gridDim.x * 256)
-        p.redo_bits[i] = 0u;
+// A tiered chunk's counters, zeroed by one launch before its near pass (four memsets cost C1 ~20 us of launch gaps):
+// the unit queue head, the record count, the redo list count, the drain's per-workgroup words [0, n_drain), and the
+// far and redo passes' own unit queue heads (DRAIN_WORDS - 2, - 1).
+__global__ __launch_bounds__(256) void chunk_start(Params p, uint32_t n_drain) {
+    if (threadIdx.x == 0) {
+        *p.tile_counter = 0u;
+        *p.defer_count = 0u;
+        *p.redo_count = 0u;
+        p.drain_count[DRAIN_WORDS - 2] = 0u;
+        p.drain_count[DRAIN_WORDS - 1] = 0u;
+    }
+    for (uint32_t i = threadIdx.x; i < n_drain; i += 256) p.drain_count[i] = 0u;
 }
 
 // GetPixelColor's sum over the stored colours of samples [k0, k0 + kn), in k order
@@ -707,10 +709,20 @@ __global__ __launch_bounds__(256) void clear_redo_bits(Params p) {
 // is one 768-B block of its 64 pixels' colours, so a wave's colour stores fill whole lines
 // (pixel-major rows of 96 B wrote 1.26x the colour bytes to HBM as partial lines).  Thread i
 // sums pixel i % 64 of tile i / 64: consecutive threads read consecutive colours.
+//
+// Tiered renders: the redo bits are set only when the redo list overflowed (redo_count > redo_cap: by the near pass
+// past the list's end, and by spill_redo_list); the redo pass has read them by now, and this clears the chunk's bits
+// again, so they are zero at every chunk's start without a memset of the whole bitmap per chunk (130 MB at C2,
+// ~180 MB at C5).  Nothing to do when the list held every id.
 __global__ __launch_bounds__(256) void reduce_samples(Params p, uint32_t last) {
     const uint32_t twl = p.tile_w_log2;
     const uint32_t tiles_x = tiles_x_of(p.width, twl);
     const size_t n_tiles = (size_t)tiles_x * tiles_y_of(p.rows, twl);
+    if (p.redo_count && __builtin_amdgcn_readfirstlane(*(volatile uint32_t*)p.redo_count) > p.redo_cap) {
+        const uint64_t words = (uint64_t)p.kn * n_tiles * 2;  // 64 bits a tile
+        for (uint64_t w = (uint64_t)blockIdx.x * 256 + threadIdx.x; w < words; w += (uint64_t)gridDim.x * 256)
+            p.redo_bits[w] = 0u;
+    }
     const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= n_tiles * 64) return;
     const uint32_t t = (uint32_t)(i >> 6), l = (uint32_t)(i & 63u);
@@ -856,6 +868,9 @@ hipError_t launch_tiered(Params pn, Params pf, hipStream_t stream) {
     const uint64_t slots = tiles * 64;
     Params pr = pf;  // the redo pass: the far layout over the chunk's units, flagged samples only
     pr.tier = 0;
+    // the far and redo passes' unit queue heads: words of their own, zeroed with the chunk's others (chunk_start)
+    pf.tile_counter = pn.drain_count + DRAIN_WORDS - 2;
+    pr.tile_counter = pn.drain_count + DRAIN_WORDS - 1;
     for (uint32_t k0 = 0; k0 < spp; k0 += chunk) {
         pn.k0 = pf.k0 = pr.k0 = k0;
         pn.kn = pf.kn = pr.kn = spp - k0 < chunk ? spp - k0 : chunk;
@@ -869,26 +884,22 @@ hipError_t launch_tiered(Params pn, Params pf, hipStream_t stream) {
             fprintf(stderr, "rtx tiered: waves/wg %d / %d, wgs/CU %d / %d / %d, grid %llu, sub %u, units %llu, lds %zu / %zu B, "
                     "cap %u, camera-ray pool %d, drain %d\n", WN, WAVES, per_n, per_f, per_r, (unsigned long long)bn, pn.sub,
                     (unsigned long long)units, sn, sf, pn.defer_cap, (int)POOL, (int)drain);
-        // the unit queue head, the chunk's record count, its redo list count (the redo bits are zero:
-        // the caller zeroes them once, clear_redo_bits after every chunk that set any)
-        if ((e = hipMemsetAsync(pn.tile_counter, 0, sizeof(uint32_t), stream)) != hipSuccess) return e;
-        if ((e = hipMemsetAsync(pn.defer_count, 0, sizeof(uint32_t), stream)) != hipSuccess) return e;
-        if ((e = hipMemsetAsync(pn.redo_count, 0, sizeof(uint32_t), stream)) != hipSuccess) return e;
-        if (drain && 2 * bn <= DRAIN_WORDS) {  // each workgroup's region: the queue over the near grid (a region that fills sends the rest to the redo pass)
+        // the chunk's counters (the redo bits are zero: the caller zeroes them once, reduce_samples after every chunk
+        // that set any); with the drain each workgroup's region is the queue over the near grid (a region that fills
+        // sends the rest to the redo pass)
+        const bool drain_now = drain && 2 * bn + 2 <= DRAIN_WORDS;
+        hipLaunchKernelGGL(chunk_start, dim3(1), dim3(256), 0, stream, pn, drain_now ? (uint32_t)(2 * bn) : 0u);
+        if (drain_now) {
             pn.drain_region = pf.drain_region = pn.defer_cap / (uint32_t)bn;
-            if ((e = hipMemsetAsync(pn.drain_count, 0, 2 * bn * sizeof(uint32_t), stream)) != hipSuccess) return e;
             if constexpr (CAN_DRAIN)
                 hipLaunchKernelGGL((render_drain<USE_LDS, WN, MINW, HYB, POOL, ST>), dim3((uint32_t)bn), dim3(block_n), sd,
                                    stream, DrainArgs{pn, far_layout(pf)});
         } else {
             hipLaunchKernelGGL(kn, dim3((uint32_t)bn), dim3(block_n), sn, stream, pn);
-            if ((e = hipMemsetAsync(pf.tile_counter, 0, sizeof(uint32_t), stream)) != hipSuccess) return e;
             hipLaunchKernelGGL(kf, dim3((uint32_t)per_f * cus), dim3(block), sf, stream, pf);
         }
         hipLaunchKernelGGL(spill_redo_list, dim3((uint32_t)cus * 4), dim3(256), 0, stream, pn);
-        if ((e = hipMemsetAsync(pr.tile_counter, 0, sizeof(uint32_t), stream)) != hipSuccess) return e;
         hipLaunchKernelGGL(kr, dim3((uint32_t)br), dim3(block), sf, stream, pr);
-        hipLaunchKernelGGL(clear_redo_bits, dim3((uint32_t)cus * 4), dim3(256), 0, stream, pn);
         hipLaunchKernelGGL(reduce_samples, dim3((uint32_t)((slots + 255) / 256)), dim3(256), 0, stream, pn,
                            (uint32_t)(k0 + pn.kn >= spp));
         if ((e = hipGetLastError()) != hipSuccess) return e;
