@@ -52,6 +52,9 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0, help="0: the host's CPU share per GPU")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-hash", action="store_true", help="skip the framebuffer hash")
+    ap.add_argument("--no-verify", action="store_true",
+                    help="one rank: skip the untimed render with the library's stats and error check after the timed "
+                         "steps (PMC profiles count every dispatch of the bench kernel: scripts/gpu_profiles_r05.sh)")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_r05.jsonl"),
                     help="PMC HBM-traffic summaries (scripts/pmc_traffic.py): a .json, or a .jsonl of one per workload")
     ap.add_argument("--valu", default=os.path.join(ROOT, "profiles", "valu_r05.jsonl"),
@@ -397,7 +400,10 @@ def main():
     elapsed = time.perf_counter() - t0
     if pipelined:
         kms = [e0.elapsed_time(e1) for e0, e1 in evs]
-        img = step([], gms)  # (untimed: the frame once more, with the library's stats and error check)
+        if args.no_verify:
+            img = shard[:rtx.region_rows(reg)] if args.shard else gather_image(shard, H, rank, world, stripe=stripe)
+        else:
+            img = step([], gms)  # (untimed: the frame once more, with the library's stats and error check)
     t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if shared else "cuda")
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

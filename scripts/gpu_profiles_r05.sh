@@ -26,7 +26,7 @@ add c2_r0of8 "random_spheres:1920x1080x500/rows0of8" "--shard 0/8"
 rc=0
 for i in "${!NAMES[@]}"; do
   n=${NAMES[$i]}; k=${KEYS[$i]}; a=${ARGS[$i]}
-  cmd="python bench.py --steps 1 --warmup 0 --no-cpu --no-hash $a"; mkdir -p "$OUT/$n"
+  cmd="python bench.py --steps 1 --warmup 0 --no-cpu --no-hash --no-verify $a"; mkdir -p "$OUT/$n"
   for pass in valu fetch write; do
     case $pass in valu) P="$PV";; fetch) P="FETCH_SIZE";; write) P="WRITE_SIZE";; esac
     timeout -s KILL 300 rocprofv3 --kernel-trace --pmc $P -d "$OUT/$n/$pass" -o run --output-format csv -- $cmd \
