@@ -1058,8 +1058,9 @@ int enqueue_on(rtx_scene* s, DeviceCopy* c, const rtx_camera* cam, uint64_t seed
         }
     }
     c->placement = *tiered ? rtxd::tier_placement(pn, p, flags) : rtxd::scene_placement(p, flags);
-    // every stats slot, the unit queue head and the watchdog flag start at 0 for every render
-    HIP_TRY(hipMemsetAsync(c->counters, 0, rtxd::COUNTER_SLOTS * sizeof(unsigned long long), stream));
+    // every stats slot, the unit queue head and the watchdog flag start at 0 for every render (a tiered render's
+    // first chunk_start launch zeroes them: one launch fewer)
+    if (!*tiered) HIP_TRY(hipMemsetAsync(c->counters, 0, rtxd::COUNTER_SLOTS * sizeof(unsigned long long), stream));
     if (timed) HIP_TRY(hipEventRecord(c->ev0, stream));
     if (const hipError_t e = *tiered ? rtxd::launch_render(pn, flags, stream, &p) : rtxd::launch_render(p, flags, stream)) {
         scr->redo_zero = 0;  // a chunk may have stopped between setting redo bits and clearing them

@@ -691,8 +691,12 @@ __global__ __launch_bounds__(256) void spill_redo_list(Params p) {
 
 // A tiered chunk's counters, zeroed by one launch before its near pass (four memsets cost C1 ~20 us of launch gaps):
 // the unit queue head, the record count, the redo list count, the drain's per-workgroup words [0, n_drain), and the
-// far and redo passes' own unit queue heads (DRAIN_WORDS - 2, - 1).
-__global__ __launch_bounds__(256) void chunk_start(Params p, uint32_t n_drain) {
+// far and redo passes' own unit queue heads (DRAIN_WORDS - 2, - 1); for the render's first chunk (first != 0) every
+// stats slot too (rtx_capi's enqueue_on leaves them to this launch for a tiered render).
+__global__ __launch_bounds__(256) void chunk_start(Params p, uint32_t n_drain, uint32_t first) {
+    if (first)
+        for (uint32_t i = threadIdx.x; i < COUNTER_SLOTS; i += 256) p.counters[i] = 0ull;
+    __syncthreads();  // (the unit queue head and the record count share the slots)
     if (threadIdx.x == 0) {
         *p.tile_counter = 0u;
         *p.defer_count = 0u;
@@ -735,8 +739,27 @@ __global__ __launch_bounds__(256) void reduce_samples(Params p, uint32_t last) {
         sy = o[1];
         sz = o[2];
     }
+    // 8 samples' colours in flight per thread, then added in k order (one load at a time, each waited for, held
+    // the reduction to 6.1 TB/s)
     const float* src = p.scratch + i * 3;
-    for (uint32_t k = 0; k < p.kn; ++k, src += n_tiles * 64 * 3) {
+    const size_t stride = n_tiles * 64 * 3;
+    uint32_t k = 0;
+    for (; k + 8 <= p.kn; k += 8, src += 8 * stride) {
+        float c[8][3];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            c[j][0] = src[j * stride];
+            c[j][1] = src[j * stride + 1];
+            c[j][2] = src[j * stride + 2];
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            sx = sx + c[j][0];
+            sy = sy + c[j][1];
+            sz = sz + c[j][2];
+        }
+    }
+    for (; k < p.kn; ++k, src += stride) {
         sx = sx + src[0];
         sy = sy + src[1];
         sz = sz + src[2];
@@ -888,7 +911,8 @@ hipError_t launch_tiered(Params pn, Params pf, hipStream_t stream) {
         // that set any); with the drain each workgroup's region is the queue over the near grid (a region that fills
         // sends the rest to the redo pass)
         const bool drain_now = drain && 2 * bn + 2 <= DRAIN_WORDS;
-        hipLaunchKernelGGL(chunk_start, dim3(1), dim3(256), 0, stream, pn, drain_now ? (uint32_t)(2 * bn) : 0u);
+        hipLaunchKernelGGL(chunk_start, dim3(1), dim3(256), 0, stream, pn, drain_now ? (uint32_t)(2 * bn) : 0u,
+                           (uint32_t)(k0 == 0));
         if (drain_now) {
             pn.drain_region = pf.drain_region = pn.defer_cap / (uint32_t)bn;
             if constexpr (CAN_DRAIN)
