@@ -739,18 +739,17 @@ __global__ __launch_bounds__(256) void reduce_samples(Params p, uint32_t last) {
         sy = o[1];
         sz = o[2];
     }
-    // 8 samples' colours in flight per thread, then added in k order (one load at a time, each waited for, held
-    // the reduction to 6.1 TB/s)
+    // 8 samples' colours in flight per thread, then added in k order; the scratch is read once (non-temporal loads)
     const float* src = p.scratch + i * 3;
     const size_t stride = n_tiles * 64 * 3;
     uint32_t k = 0;
     for (; k + 8 <= p.kn; k += 8, src += 8 * stride) {
         float c[8][3];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            c[j][0] = src[j * stride];
-            c[j][1] = src[j * stride + 1];
-            c[j][2] = src[j * stride + 2];
+        for (int j = 0; j < 8; ++j) {  // (read once: non-temporal)
+            c[j][0] = __builtin_nontemporal_load(src + j * stride);
+            c[j][1] = __builtin_nontemporal_load(src + j * stride + 1);
+            c[j][2] = __builtin_nontemporal_load(src + j * stride + 2);
         }
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
