@@ -568,3 +568,26 @@ def test_tier_chunk_at_id_limit(torch_cuda, spheres, dev_spheres, monkeypatch):
         assert np.isfinite(got).all() and np.array_equal(got, want), int((got != want).any(axis=2).sum())
     finally:
         rtx.release_device_memory(0)
+
+
+@pytest.mark.parametrize("cap,redo_cap", [(64, 100), (0, 0)])
+def test_tier_overflow_across_chunks(torch_cuda, spheres, dev_spheres, monkeypatch, cap, redo_cap):
+    """The redo bits across sample chunks: a 1 MB scratch splits the window's 24 samples into chunks, and a starved
+    queue and redo list send samples of every chunk through the bits.  reduce_samples clears the bits after each chunk
+    (chunk_start zeroes the chunk's counters): a bit left over would render a sample of the next chunk twice, which
+    leaves the colour alone but not the counting kernel's work — so both kernels' frames and the counting kernel's
+    path counters (samples, segments, hits, texel fetches, draws) must equal the oracle's."""
+    monkeypatch.setenv("RTX_SCRATCH_MB", "1")
+    cam = spheres.camera(width=160, spp=24, depth=50)
+    reg = rtx.Region(0, 0, cam.image_width, cam.image_height, 0, 1)
+    it, cnt = ob.render(spheres.desc, cam, 23, reg, ob.ORDER_ITERATIVE)
+    monkeypatch.setenv("RTX_DEFER_CAP", str(cap))
+    monkeypatch.setenv("RTX_REDO_CAP", str(redo_cap))
+    for counters in (False, True):
+        got, st = gpu_region(torch_cuda, dev_spheres, cam, 23, reg, counters=counters)
+        assert st.sample_chunks > 2 and st.walk_layout & rtx.RTX_LAYOUT_TIERED, st.sample_chunks
+        assert st.redo_chunks == st.sample_chunks, (st.redo_chunks, st.sample_chunks)
+        assert np.array_equal(got, it), (counters, int((got != it).any(axis=2).sum()))
+        if counters:
+            for k in ("samples", "segments", "hits", "texel_fetches", "rng_draws"):
+                assert getattr(st, k) == cnt[k], (k, getattr(st, k), cnt[k])
