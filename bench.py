@@ -75,6 +75,9 @@ def parse():
                          "render path on a one-GPU box; not a scaling number")
     ap.add_argument("--selftest-gloo", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--selftest-fail-rank", type=int, default=-1, help=argparse.SUPPRESS)
+    # test hook (tests/test_bench_check.py): with RTX_LIB = librtx_dbgclaim.so, timed step i (0-based) alone enters
+    # the unit-queue claim with half the wave; the error check after the timed region must fail the bench
+    ap.add_argument("--debug-partial-step", type=int, default=-1, help=argparse.SUPPRESS)
     return ap.parse_args()
 
 
@@ -132,9 +135,10 @@ def cpu_model() -> str:
     return platform.processor() or "unknown"
 
 
-def cpu_baseline(scene, cam, seed: int, target_s: float, threads: int) -> dict:
+def cpu_baseline(scene, cam, seed: int, target_s: float, threads: int, stride: int = 0) -> dict:
     """The oracle (oracle/liboracle.so, a scalar C restatement) on host threads over a
-    bounded sample of the same workload: full-width rows at a fixed stride, all spp."""
+    bounded sample of the same workload: full-width rows at a fixed stride, all spp.
+    stride > 0: that sample (the full-host leg reuses the headline leg's rows), no calibration."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_binding as ob
     import rtx
@@ -143,21 +147,25 @@ def cpu_baseline(scene, cam, seed: int, target_s: float, threads: int) -> dict:
     if threads <= 0:
         threads = min(CPU_SHARE_PER_GPU, logical)
     H = cam.image_height
-    # Calibrate on 2 rows per thread (every thread busy), then size the sample to
-    # ~target_s of wall time on those threads.
-    cal_rows = min(H, 2 * threads)
-    stride = max(1, H // cal_rows)
-    t0 = time.perf_counter()
-    ob.render(scene.desc, cam, seed, rtx.Region(0, 0, cam.image_width, H, 0, stride), ob.ORDER_REFERENCE, threads)
-    dt = time.perf_counter() - t0
-    rows_per_s = ((H + stride - 1) // stride) / max(dt, 1e-6)
-    rows = max(2, min(H, int(rows_per_s * target_s)))
-    stride = max(1, H // rows)
+    if stride <= 0:
+        # Calibrate on 2 rows per thread (every thread busy), then size the sample to
+        # ~target_s of wall time on those threads.
+        cal_rows = min(H, 2 * threads)
+        stride = max(1, H // cal_rows)
+        t0 = time.perf_counter()
+        ob.render(scene.desc, cam, seed, rtx.Region(0, 0, cam.image_width, H, 0, stride), ob.ORDER_REFERENCE, threads)
+        dt = time.perf_counter() - t0
+        rows_per_s = ((H + stride - 1) // stride) / max(dt, 1e-6)
+        rows = max(2, min(H, int(rows_per_s * target_s)))
+        stride = max(1, H // rows)
     reg = rtx.Region(0, 0, cam.image_width, H, 0, stride)
     t0 = time.perf_counter()
     _, c = ob.render(scene.desc, cam, seed, reg, ob.ORDER_REFERENCE, threads)
     dt = time.perf_counter() - t0
     nrows = (H + stride - 1) // stride
+    who = (f"one GPU's share of the host's {logical} logical CPUs" if threads < logical else
+           f"every logical CPU this process may run on (os.sched_getaffinity), as the reference sizes its pool to "
+           f"runtime.NumCPU() (camera.go:167)")
     return {
         "value": c["segments"] / dt / 1e6,
         "unit": "Mray/s",
@@ -165,11 +173,12 @@ def cpu_baseline(scene, cam, seed: int, target_s: float, threads: int) -> dict:
         "kind": "port",
         "samples_per_s": c["samples"] / dt,
         "seconds": dt,
+        "stride": stride,
         "cpu_model": cpu_model(),
         "host_logical_cpus": logical,
         "sample": f"{nrows} full-width rows (every {stride}th) of the same {cam.image_width}x{H}x{cam.samples_per_pixel} "
-                  f"render, {c['samples']} samples, C oracle on {threads} threads = one GPU's share of the host's "
-                  f"{logical} logical CPUs (Go absent on the host: the C restatement stands in for the Go reference)",
+                  f"render, {c['samples']} samples, C oracle on {threads} threads = {who} (Go absent on the host: the "
+                  "C restatement stands in for the Go reference)",
     }
 
 
@@ -382,28 +391,44 @@ def main():
         step([], [])
     barrier()
     kms, gms = [], []
-    # One rank: the K renders are enqueued back to back on the stream (no stats read between them, so the GPU does
-    # not idle for a host round trip per step), each bracketed by events on that stream: the kernel time per step.
-    # The warmup steps above and the check below read the library's stats (and its error word) synchronously.
-    pipelined = world == 1
+    # The K steps are enqueued back to back on the stream (no stats read between them, so the GPU does not idle for
+    # a host round trip per step): per step the render, then (N > 1) the RCCL gather of the shards and rank 0's
+    # de-interleave, each bracketed by events on that stream — the kernel time and the gather time per step.  (An
+    # RCCL collective on torch's NCCL stream waits for this stream's render and makes this stream wait for it, so
+    # the next render does not overwrite the shard before it is sent.)  Nothing of the library's stats is read in
+    # the timed region: its sticky error word is checked once after it, for all K renders.
+    # (A rehearsal on one GPU gathers through gloo and host copies, which wait on the host: its old step loop.)
+    pipelined = not shared
+    timed_img = None
     t0 = time.perf_counter()
     if pipelined:
-        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-        for e0, e1 in evs:
+        evs = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(3)) for _ in range(args.steps)]
+        for i, (e0, e1, e2) in enumerate(evs):
+            if i == args.debug_partial_step:  # (test hook: the debug library's partial-wave claim in this step only)
+                os.environ["RTX_DEBUG_PARTIAL_SITE"] = "3"
             e0.record()
             dev.render_region(cam, args.seed, reg, shard.data_ptr(), stream, counters=False, timed=False)
             e1.record()
+            os.environ.pop("RTX_DEBUG_PARTIAL_SITE", None)
+            timed_img = shard[:rtx.region_rows(reg)] if args.shard else gather_image(shard, H, rank, world,
+                                                                                     stripe=stripe)
+            e2.record()
     else:
         for _ in range(args.steps):
-            img = step(kms, gms)
+            timed_img = step(kms, gms)
     barrier()
     elapsed = time.perf_counter() - t0
+    # Every timed render's kernel ran without a watchdog stop or a partial-wave claim, or the bench fails here
+    # (rtx_device_check reads the error word no render clears: one check covers all K).
+    rtx.device_check(torch.cuda.current_device())
+    # the frame the last timed step produced (rank 0: the gathered image), hashed before anything renders again
+    timed_hash = framebuffer_hash(timed_img) if rank == 0 and not args.no_hash else None
     if pipelined:
-        kms = [e0.elapsed_time(e1) for e0, e1 in evs]
-        if args.no_verify:
-            img = shard[:rtx.region_rows(reg)] if args.shard else gather_image(shard, H, rank, world, stripe=stripe)
-        else:
-            img = step([], gms)  # (untimed: the frame once more, with the library's stats and error check)
+        kms = [e0.elapsed_time(e1) for e0, e1, _ in evs]
+        gms = [e1.elapsed_time(e2) for _, e1, e2 in evs]
+    img = timed_img
+    if not args.no_verify:
+        img = step([], [])  # (untimed: the frame once more, with the library's stats and error check)
     t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if shared else "cuda")
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -477,8 +502,24 @@ def main():
                                          "all": [round(x, 3) for x in rank_kms]}
         if not args.no_hash:
             out["framebuffer_sha256_16"] = framebuffer_hash(img)  # bitwise-comparable across N
+            # the last timed step's own frame: equal to the checked frame, or the timed region rendered something else
+            out["timed_frames_hash"] = timed_hash
+            out["timed_frames_checked"] = (f"rtx_device_check after the {args.steps} timed renders: no watchdog stop, "
+                                           "no partial-wave claim; the last timed frame's hash "
+                                           + ("equals the verify render's" if not args.no_verify else
+                                              "(no verify render: --no-verify)"))
+            if not args.no_verify and timed_hash != out["framebuffer_sha256_16"]:
+                print(json.dumps(out), flush=True)
+                raise SystemExit(f"the last timed frame ({timed_hash}) differs from the verify render "
+                                 f"({out['framebuffer_sha256_16']})")
         if world == 1 and not args.no_cpu and not args.shard:
             out["cpu_baseline"] = cpu_baseline(scene, cam, args.seed, args.cpu_target_s, args.cpu_threads)
+            # the same rows on every CPU the process may use: the reference's own concurrency (runtime.NumCPU()
+            # workers, camera.go:167); the one-GPU share above stays the headline baseline
+            if len(os.sched_getaffinity(0)) > out["cpu_baseline"]["cores"]:
+                out["cpu_baseline_full_host"] = cpu_baseline(scene, cam, args.seed, args.cpu_target_s,
+                                                             len(os.sched_getaffinity(0)),
+                                                             stride=out["cpu_baseline"]["stride"])
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define RTX_ABI_VERSION 9
+#define RTX_ABI_VERSION 10
 
 /* ---- status codes ------------------------------------------------------------ */
 enum {
@@ -416,6 +416,16 @@ int rtx_release_device_memory(int device);
 
 /* Bytes of the per-device scratch currently held on `device` (for tests and tools). */
 uint64_t rtx_device_scratch_bytes(int device);
+
+/* ABI 10.  Wait for every render enqueued on `device` and report whether any of them failed inside the
+ * kernel since the last report: RTX_OK, or RTX_ERR_HIP when a wave hit the watchdog (RTX_WATCHDOG_S) or
+ * reached a wave-level claim without the whole wave (the output of that render is then invalid).  The
+ * kernel's error word is sticky: no later render clears it, so renders enqueued back to back without
+ * stats (rtx_render_region_device with stats == NULL) are checked by ONE call after the last of them.
+ * A render that returns stats reports (and acknowledges) the same word itself.  The report is
+ * acknowledged: a second call without a failed render in between returns RTX_OK.  Blocking.
+ * The Go side: the error a pipelined Render loop returns once (camera.go:180, 230). */
+int rtx_device_check(int device);
 
 /* Render one region/shard on the CURRENT device into device memory d_out (float32
  * RGB, compacted shard rows, see rtx_region) on the given HIP stream (hipStream_t,

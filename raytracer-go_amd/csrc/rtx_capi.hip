@@ -148,6 +148,56 @@ void release_stage_locked() {
     g_stage = HostStage{};
 }
 
+// The sticky error word of a device: rtxd::KERR_WORDS counters the kernels only add to — waves
+// stopped by the watchdog, lanes of waves that found a partial wave at a claim.  No render zeroes them (the stats
+// slots are zeroed by every render, so a flag there was wiped by the next render enqueued behind a failed one):
+// `seen` is what the host has already reported, and a change since is the error of some render after that report.
+// collect_on (every render that returns stats) and rtx_device_check (any number of renders enqueued without
+// stats, e.g. a pipelined benchmark) read it.  8 bytes per device, kept for the process's life.
+struct KernErr {
+    uint32_t* d = nullptr;
+    uint32_t seen[rtxd::KERR_WORDS] = {0, 0};
+};
+std::mutex g_kerr_mu;
+std::map<int, KernErr> g_kerr;
+
+// The device's word (allocated and zeroed on first use, synchronously), or nullptr.
+uint32_t* kerr_word(int device) {
+    std::lock_guard<std::mutex> lk(g_kerr_mu);
+    KernErr& k = g_kerr[device];
+    if (!k.d) {
+        void* p = nullptr;
+        if (hipMalloc(&p, rtxd::KERR_WORDS * sizeof(uint32_t)) != hipSuccess) return nullptr;
+        if (hipMemset(p, 0, rtxd::KERR_WORDS * sizeof(uint32_t)) != hipSuccess) {
+            (void)hipFree(p);
+            return nullptr;
+        }
+        k.d = static_cast<uint32_t*>(p);
+    }
+    return k.d;
+}
+
+// Read the current device's word (the renders to report must have completed) and report what changed since the
+// last read: RTX_OK, or RTX_ERR_HIP naming the failure.  The change is then acknowledged.
+int kerr_take(int device) {
+    std::lock_guard<std::mutex> lk(g_kerr_mu);
+    auto it = g_kerr.find(device);
+    if (it == g_kerr.end() || !it->second.d) return RTX_OK;  // nothing ever rendered on it
+    KernErr& k = it->second;
+    uint32_t h[rtxd::KERR_WORDS] = {0, 0};
+    HIP_TRY(hipMemcpy(h, k.d, sizeof(h), hipMemcpyDeviceToHost));
+    const uint32_t wd = h[rtxd::KERR_WATCHDOG] - k.seen[rtxd::KERR_WATCHDOG];
+    const uint32_t pw = h[rtxd::KERR_PARTIAL_WAVE] - k.seen[rtxd::KERR_PARTIAL_WAVE];
+    std::memcpy(k.seen, h, sizeof(h));
+    if (pw)
+        return fail(RTX_ERR_HIP, "render kernel: a wave-level claim was reached without the whole wave (partial EXEC; "
+                                 "%u lanes on device %d): output invalid", pw, device);
+    if (wd)
+        return fail(RTX_ERR_HIP, "render kernel watchdog fired (RTX_WATCHDOG_S; %u waves on device %d): output "
+                                 "incomplete", wd, device);
+    return RTX_OK;
+}
+
 // Free a device's scratch buffers (g_scratch_mu held).
 void release_scratch_locked(int device) {
     auto it = g_scratch.find(device);
@@ -816,7 +866,7 @@ int check_camera(const rtx_camera* cam) {
     if ((uint64_t)cam->image_width * cam->image_height > 0xFFFFFFFFull)
         return fail(RTX_ERR_INVALID_ARG, "image has more than 2^32 pixels (RNG counter is 32-bit)");
     // the kernel's scratch slot of a pixel (64 per tile, tiles padded: at most 64 columns and 64 rows) is 32-bit
-    if ((uint64_t)(cam->image_width + 64) * (cam->image_height + 64) > 0xFFFFFFFFull)
+    if (((uint64_t)cam->image_width + 64) * ((uint64_t)cam->image_height + 64) > 0xFFFFFFFFull)
         return fail(RTX_ERR_INVALID_ARG, "image too large: its padded tiles exceed 2^32 pixel slots");
     return RTX_OK;
 }
@@ -911,7 +961,7 @@ rtxd::Params make_params(const rtx_scene* s, const DeviceCopy* c, uint32_t oct, 
     p.out = d_out;
     p.counters = c->counters;
     p.tile_counter = reinterpret_cast<uint32_t*>(c->counters + 7);  // slot 7 low: unit queue head
-    p.error_flag = reinterpret_cast<uint32_t*>(c->counters + 7) + 1;  // slot 7 high: watchdog flag
+    p.error_flag = nullptr;  // the device's sticky error word (KernErr), set by enqueue_on
     p.watchdog_ticks = watchdog_ticks();
     p.shade_thresh = shade_thresh();
     p.has_uv = s->has_image ? 1u : 0u;
@@ -930,6 +980,7 @@ int enqueue_on(rtx_scene* s, DeviceCopy* c, const rtx_camera* cam, uint64_t seed
     const uint32_t oct = layout_slot(s, cam);  // the walk's layout (rtx_topology.h, rtx_collapse.h)
     if (int rc = ensure_layout(s, c, cam)) return rc;
     rtxd::Params p = make_params(s, c, oct, cam, seed, r, d_out);
+    if (!(p.error_flag = kerr_word(c->device))) return fail(RTX_ERR_OOM, "the error word on device %d", c->device);
     // the tiered walk: a camera in the near region of a sphere scene (rtx_scene_near_region's rule)
     bool tier = camera_in_near(s, cam) && p.n_quads == 0 && !p.has_noise;
     rtxd::Params pn;
@@ -1058,8 +1109,8 @@ int enqueue_on(rtx_scene* s, DeviceCopy* c, const rtx_camera* cam, uint64_t seed
         }
     }
     c->placement = *tiered ? rtxd::tier_placement(pn, p, flags) : rtxd::scene_placement(p, flags);
-    // every stats slot, the unit queue head and the watchdog flag start at 0 for every render (a tiered render's
-    // first chunk_start launch zeroes them: one launch fewer)
+    // every stats slot and the unit queue head start at 0 for every render (a tiered render's first chunk_start
+    // launch zeroes them: one launch fewer); the sticky error word is not among them
     if (!*tiered) HIP_TRY(hipMemsetAsync(c->counters, 0, rtxd::COUNTER_SLOTS * sizeof(unsigned long long), stream));
     if (timed) HIP_TRY(hipEventRecord(c->ev0, stream));
     if (const hipError_t e = *tiered ? rtxd::launch_render(pn, flags, stream, &p) : rtxd::launch_render(p, flags, stream)) {
@@ -1078,11 +1129,8 @@ int collect_on(DeviceCopy* c, bool count, uint64_t samples, uint32_t chunks, rtx
     HIP_TRY(hipEventElapsedTime(&ms, c->ev0, c->ev1));
     unsigned long long h[rtxd::COUNTER_SLOTS] = {0};
     HIP_TRY(hipMemcpy(h, c->counters, rtxd::COUNTER_SLOTS * sizeof(unsigned long long), hipMemcpyDeviceToHost));
-    const uint64_t kerr = h[7] >> 32;  // rtxd::KERR_* bits
-    if (kerr & rtxd::KERR_PARTIAL_WAVE)
-        return fail(RTX_ERR_HIP, "render kernel: a wave-level claim was reached without the whole wave (partial EXEC): "
-                                 "output invalid");
-    if (kerr != 0) return fail(RTX_ERR_HIP, "render kernel watchdog fired (RTX_WATCHDOG_S): output incomplete");
+    // any render on the device since the last report (this one, or one enqueued without stats before it)
+    if (int rc = kerr_take(c->device)) return rc;
     std::memset(st, 0, sizeof(*st));
     st->samples = count ? h[0] : samples;
     st->segments = h[1];
@@ -1737,6 +1785,21 @@ int rtx_release_device_memory(int device) {
         release_comms_locked();
     }
     return RTX_OK;
+}
+
+int rtx_device_check(int device) {
+    g_last_error.clear();
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(RTX_ERR_NO_DEVICE, "no HIP device");
+    if (device < 0 || device >= ndev) return fail(RTX_ERR_INVALID_ARG, "device %d of %d", device, ndev);
+    int cur = 0;
+    HIP_TRY(hipGetDevice(&cur));
+    HIP_TRY(hipSetDevice(device));
+    const hipError_t e = hipDeviceSynchronize();  // every render enqueued on the device has ended
+    const int rc = e == hipSuccess ? kerr_take(device)
+                                   : fail(RTX_ERR_HIP, "hipDeviceSynchronize(%d): %s", device, hipGetErrorString(e));
+    (void)hipSetDevice(cur);
+    return rc;
 }
 
 uint64_t rtx_device_scratch_bytes(int device) {

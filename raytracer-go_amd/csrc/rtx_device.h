@@ -452,7 +452,7 @@ struct Params {
     unsigned long long* counters;  // rtx_stats order when counting (COUNTER_SLOTS x u64)
     uint32_t shade_thresh;         // shade once this many lanes of a wave wait (1..64)
     uint32_t* tile_counter;        // global unit queue head (zeroed before each chunk's launch)
-    uint32_t* error_flag;          // set to 1 by a wave that hit the watchdog (zeroed per render)
+    uint32_t* error_flag;          // the device's sticky error word: KERR_* counters, never zeroed by a render
     uint64_t watchdog_ticks;       // per-wave limit in s_memrealtime ticks (100 MHz)
     uint32_t has_uv;               // scene has an image texture (UV needed at hits)
     uint32_t has_noise;            // scene has a Perlin NoiseTexture (v3 NOISE kernels)
@@ -516,9 +516,12 @@ __host__ __device__ __forceinline__ bool pool_fits(const Params& p) {
     return p.cam_pool && (size_t)pool_f4_offset(p) * 16 + 12 * POOL_BYTES_PER_WAVE <= 80u * 1024u;
 }
 
-// Error bits of *Params::error_flag (rtx_capi.hip collect_on turns them into RTX_ERR_HIP).
-constexpr uint32_t KERR_WATCHDOG = 1u;      // a wave outlived RTX_WATCHDOG_S
-constexpr uint32_t KERR_PARTIAL_WAVE = 2u;  // a wave-level claim was reached without the whole wave
+// The words of Params::error_flag, the device's sticky error word (rtx_capi.hip KernErr): counters
+// the kernel only adds to and no render zeroes, so a failed render stays visible behind any renders enqueued after
+// it, until collect_on or rtx_device_check reads them (and turns a change into RTX_ERR_HIP).
+constexpr uint32_t KERR_WATCHDOG = 0u;      // waves that outlived RTX_WATCHDOG_S
+constexpr uint32_t KERR_PARTIAL_WAVE = 1u;  // lanes of waves that reached a wave-level claim without the whole wave
+constexpr uint32_t KERR_WORDS = 2u;
 
 struct Ray {
     V3 o, d;

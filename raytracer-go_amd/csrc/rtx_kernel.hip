@@ -234,7 +234,7 @@ __device__ __forceinline__ void split_clk(uint64_t& acc, uint64_t& clk) {
 // workgroup's waves.
 template <bool COUNT, bool USE_LDS, bool QUADS, bool NOISE, int WAVES, bool HYB, bool CLK, int TIER, bool POOL, bool ST,
           bool DRAIN>
-__device__ __forceinline__ void render_body(const Params& p) {
+__device__ __forceinline__ void render_body(const Params& p, const uint64_t t0 = 0) {
     constexpr bool TIME = COUNT || CLK;
     static_assert(!DRAIN || (!COUNT && !CLK && (TIER == 1 || TIER == 2)), "the drain: the timed near and far passes");
     static_assert(!POOL || (USE_LDS && (TIER == 0 || TIER == 1)), "the camera-ray pool: LDS scenes, near pass or one walk");
@@ -400,14 +400,19 @@ __device__ __forceinline__ void render_body(const Params& p) {
         if (far) ready = false;
     };
 
-    const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+    // the watchdog's start: the launch's (render_drain hands its near phase's start to its far phase, so the
+    // limit holds for the whole launch), or now
+    const uint64_t t_start = t0 ? t0 : __builtin_amdgcn_s_memrealtime();
     for (;;) {
         // Watchdog (RTX_WATCHDOG_S): a wave never outlives p.watchdog_ticks, so a bug cannot
         // keep the GPU busy forever; the render then fails with RTX_ERR_HIP (collect_on).
         // The loop is wave-uniform, so is this test.
         if ((++iter & 255u) == 0) {
+            // the count wrapped into the flag bit (2^31 iterations: only with RTX_WATCHDOG_S raised): flip it
+            // back, which restores the flag as it was whether it was set (0xFFFFFFFF + 1 = 0) or not
+            if ((iter & 0x7FFFFFFFu) == 0u) iter ^= 0x80000000u;
             if (__builtin_amdgcn_s_memrealtime() - t_start > p.watchdog_ticks) {
-                if (lane == 0) atomicOr(p.error_flag, KERR_WATCHDOG);
+                if (lane == 0) atomicAdd(p.error_flag + KERR_WATCHDOG, 1u);
                 break;
             }
         }
@@ -610,7 +615,7 @@ __device__ __forceinline__ void render_body(const Params& p) {
         }
         if (TIME) split_clk(split[3], clk);
     }
-    if (RTX_KERR()) atomicOr(p.error_flag, KERR_PARTIAL_WAVE);
+    if (RTX_KERR()) atomicAdd(p.error_flag + KERR_PARTIAL_WAVE, 1u);
 #undef RTX_SET_KERR
 #undef RTX_KERR
     if (COUNT) {
@@ -658,7 +663,8 @@ struct DrainArgs {
 
 template <bool USE_LDS, int WAVES, int MINW, bool HYB, bool POOL, bool ST>
 __global__ __launch_bounds__(64 * WAVES, MINW) void render_drain(DrainArgs a) {
-    render_body<false, USE_LDS, false, false, WAVES, HYB, false, 1, POOL, ST, true>(a.pn);
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime() | 1ull;  // the watchdog's start for both phases (nonzero)
+    render_body<false, USE_LDS, false, false, WAVES, HYB, false, 1, POOL, ST, true>(a.pn, t0);
     __syncthreads();  // every wave's near work and records done: the far phase overwrites the scene copy
     // The far phase reads its settings from the kernel arguments afresh, through an opaque copy of their address:
     // values it shares with the near phase are then not kept live through the near phase (which spilled 4 more VGPRs).
@@ -676,7 +682,7 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_drain(DrainArgs a) {
     pf.refill_hits = k.fl.refill_hits;
     pf.prim_batch = k.fl.prim_batch;
     pf.tier = 2;
-    render_body<false, USE_LDS, false, false, WAVES, HYB, false, 2, false, false, true>(pf);
+    render_body<false, USE_LDS, false, false, WAVES, HYB, false, 2, false, false, true>(pf, t0);
 }
 
 // The redo list overflowed (more samples than p.redo_cap): its ids join the ones the near pass set in

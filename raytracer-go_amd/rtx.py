@@ -126,6 +126,7 @@ RTX_SYMBOLS = [
     "rtx_release_device_memory", "rtx_device_scratch_bytes", "rtx_scene_create_ex", "rtx_scene_topology",
     "rtx_camera_octant", "rtx_walk_tree", "rtx_render_ex", "rtx_scene_walk_skip", "rtx_walk_skip",
     "rtx_scene_near_region", "rtx_scene_near_skip", "rtx_walk_near_region", "rtx_render_ppm_ex", "rtx_region_row",
+    "rtx_device_check",
 ]
 RTXHOST_SYMBOLS = [
     "rtxhost_build_scene", "rtxhost_scene_free", "rtxhost_scene_desc", "rtxhost_scene_camera",
@@ -218,6 +219,9 @@ def load() -> ctypes.CDLL:
     L.rtx_release_device_memory.restype = c_int
     L.rtx_device_scratch_bytes.argtypes = [c_int]
     L.rtx_device_scratch_bytes.restype = c_uint64
+    if hasattr(L, "rtx_device_check"):  # ABI 10 (RTX_LIB may name an older build for A/B)
+        L.rtx_device_check.argtypes = [c_int]
+        L.rtx_device_check.restype = c_int
     _lib = L
     return L
 
@@ -484,6 +488,12 @@ def release_device_memory(device: int = -1) -> None:
 
 def device_scratch_bytes(device: int = 0) -> int:
     return int(load().rtx_device_scratch_bytes(device))
+
+
+def device_check(device: int = 0) -> None:
+    """rtx_device_check (ABI 10): wait for every render enqueued on `device` and raise RtxError
+    (RTX_ERR_HIP) if any of them failed in the kernel since the last report (watchdog, partial-wave claim)."""
+    check(load().rtx_device_check(device), "rtx_device_check")
 
 
 def synthetic_earth_ycbcr(seed: int, w: int = 2048, h: int = 1024):

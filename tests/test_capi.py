@@ -34,7 +34,7 @@ def test_binding_lists_match_headers(built):
 
 def test_version_and_build_info(built):
     L = rtx.load()
-    assert L.rtx_version() == 9
+    assert L.rtx_version() == 10
     assert b"gfx950" in L.rtx_build_info()
 
 

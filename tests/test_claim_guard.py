@@ -67,3 +67,64 @@ def test_partial_wave_claim_fails_loudly(built, site, extra):
     out = run_child(env)
     assert out.startswith(f"ERR {rtx.RTX_ERR_HIP}"), out
     assert "without the whole wave" in out, out
+
+
+PIPELINED = """
+import os, sys, numpy as np, torch
+sys.path[:0] = ['raytracer-go_amd', 'tests']
+import rtx
+torch.cuda.set_device(0)
+s = rtx.HostScene('random_spheres', 1)
+d = rtx.DeviceScene(s.desc)
+cam = s.camera(width=96, spp=4)
+reg = rtx.Region(0, 0, cam.image_width, cam.image_height, 0, 1)
+o = torch.zeros((cam.image_height, cam.image_width, 3), device='cuda')
+stream = torch.cuda.current_stream().cuda_stream
+bad = int(sys.argv[1])
+for i in range(3):  # enqueued back to back, no stats read between them (bench.py's timed loop)
+    if i == bad:
+        os.environ['RTX_DEBUG_PARTIAL_SITE'] = '3'
+    d.render_region(cam, 7, reg, o.data_ptr(), stream)
+    os.environ.pop('RTX_DEBUG_PARTIAL_SITE', None)
+for k in range(2):
+    try:
+        rtx.device_check(0)
+        print('OK', k)
+    except rtx.RtxError as e:
+        print('ERR', k, e.code, e)
+"""
+
+
+@pytest.mark.parametrize("bad", [-1, 1], ids=["clean", "second_of_three"])
+def test_error_word_is_sticky_across_pipelined_renders(built, bad):
+    """The kernel's error word survives later renders (no render zeroes it): a partial-wave claim
+    in the 2nd of 3 renders enqueued back to back without stats is still reported by ONE rtx_device_check after
+    the 3rd; the report is acknowledged (a second check passes), and a clean run passes both."""
+    res = subprocess.run([sys.executable, "-c", PIPELINED, str(bad)], cwd=ROOT,
+                         env=dict(os.environ, RTX_LIB=DBG, RTX_WATCHDOG_S="60"), capture_output=True, text=True,
+                         timeout=120)
+    assert res.returncode == 0, res.stdout + res.stderr
+    lines = res.stdout.strip().splitlines()[-2:]
+    if bad < 0:
+        assert lines == ["OK 0", "OK 1"], lines
+    else:
+        assert lines[0].startswith(f"ERR 0 {rtx.RTX_ERR_HIP}") and "without the whole wave" in lines[0], lines
+        assert lines[1] == "OK 1", lines
+
+
+def test_bench_fails_on_a_flagged_timed_step(built):
+    """bench.py's timed renders are checked: a partial-wave claim in the 2nd of 3 timed steps (enqueued with no
+    stats read) fails the bench with a non-zero status; without it, the last timed frame's hash is the verify
+    render's (timed_frames_hash == framebuffer_sha256_16)."""
+    cmd = [sys.executable, "bench.py", "--steps", "3", "--warmup", "1", "--width", "96", "--spp", "4", "--no-cpu"]
+    env = dict(os.environ, RTX_LIB=DBG, RTX_WATCHDOG_S="60")
+    ok = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert ok.returncode == 0, ok.stdout + ok.stderr
+    import json
+
+    line = json.loads([ln for ln in ok.stdout.splitlines() if ln.startswith("{")][-1])
+    assert line["timed_frames_hash"] == line["framebuffer_sha256_16"], line
+    bad = subprocess.run(cmd + ["--debug-partial-step", "1"], cwd=ROOT, env=env, capture_output=True, text=True,
+                         timeout=300)
+    assert bad.returncode != 0, bad.stdout + bad.stderr
+    assert "without the whole wave" in bad.stderr, bad.stderr[-2000:]
