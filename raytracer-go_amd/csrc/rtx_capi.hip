@@ -58,6 +58,8 @@ struct DeviceLayout {
     uint32_t hot = 0;       // entries stored first and cached in LDS by v3 (scenes too big for the LDS copy)
     uint32_t start = 0;     // walk position of the first entry of the walk (the root)
     uint32_t prim_end = 0;  // scenes in the LDS copy: primitives stored first, below this position
+    uint32_t n_entries = 0; // device entries before the sentinel (the paired walk's: twice its records)
+    uint32_t w2 = 0;        // 1: the paired walk's records (build_w2)
 };
 
 struct DeviceCopy {
@@ -562,6 +564,131 @@ int scene_layout(rtx_scene* s, const rtx_camera* cam, const std::vector<rtx_entr
     return RTX_OK;
 }
 
+// The paired walk of a layout in HBM: the threaded walk E (host form, escapes as entry indices)
+// as RECORDS of two entries — an entry p and the entry the walk takes after p when p does not descend (a node's
+// escape, a primitive's successor: its fail successor q(p)).  A lane at a record tests p; if p is a node whose box
+// passes it goes to the record of p + 1, else it tests q(p) in the same step and goes to the record of q(p) + 1
+// (q(p) a passing node) or of q(q(p)).  So the lane takes exactly the threaded walk's tests, in its order, with its
+// bounds — every result and every work counter is the walk's — in up to half the dependent reads: a record holds a
+// node's two children (the left child's fail successor is its sibling), so a box that fails costs no read of its
+// own.  The slots are entries in the device format (rtx_layout.h) with their successors as record positions: slot 0
+// a node's next (b.w) only, slot 1 its escape too (a.w) or a primitive's next (b.z); the sentinel as slot 1 where the
+// walk ends.  A record starts at every entry the walk can arrive at (the root, a node's first child, q(q(p)) of a
+// record): at most one per entry.  The records the walk reads most (R: the plan's estimate for the record's first
+// entry) are stored first, for the LDS cache (hot = 2 x their count entries).
+struct W2Layout {
+    std::vector<float> soa;  // 'a' halves, 'b' halves (n_entries + 1 each, the sentinel last), the quad table
+    uint32_t n_entries = 0, hot = 0, start = 0;
+};
+void build_w2(const std::vector<rtx_entry>& E, const std::vector<double>* R, uint32_t cap, const std::vector<uint32_t>& rank,
+              const std::vector<float>& quadtab, W2Layout& out) {
+    const uint32_t n = (uint32_t)E.size();
+    auto tag = [&](uint32_t i) {
+        int32_t t;
+        std::memcpy(&t, &E[i].b[3], 4);
+        return t;
+    };
+    auto q = [&](uint32_t i) -> uint32_t {  // the fail successor (n: the sentinel)
+        if (i >= n) return n;
+        if (tag(i) != RTX_E_NODE) return i + 1;
+        int32_t esc;
+        std::memcpy(&esc, &E[i].a[3], 4);
+        return (uint32_t)esc;
+    };
+    std::vector<int64_t> rec_of(n + 1, -1);
+    std::vector<uint32_t> first;  // record -> its first entry
+    auto need = [&](uint32_t i) {
+        if (i < n && rec_of[i] < 0) {
+            rec_of[i] = (int64_t)first.size();
+            first.push_back(i);
+        }
+    };
+    need(0);
+    for (size_t k = 0; k < first.size(); ++k) {  // (first grows as records are found)
+        const uint32_t p = first[k], u = q(p);
+        if (tag(p) == RTX_E_NODE) need(p + 1);
+        if (u < n) {
+            if (tag(u) == RTX_E_NODE) need(u + 1);
+            need(q(u));
+        }
+    }
+    const uint32_t nr = (uint32_t)first.size();
+    // storage order: the hot records (most reads first when estimated, else walk order), then the rest, each in walk order
+    std::vector<uint32_t> order(nr);
+    for (uint32_t r = 0; r < nr; ++r) order[r] = r;
+    std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return first[a] < first[b]; });
+    const uint32_t take = std::min<uint32_t>(cap / 2, nr);
+    std::vector<uint8_t> in_hot(nr, 0);
+    if (R && R->size() == n) {
+        std::vector<uint32_t> idx(order);
+        std::partial_sort(idx.begin(), idx.begin() + take, idx.end(), [&](uint32_t a, uint32_t b) {
+            const double ra = (*R)[first[a]], rb = (*R)[first[b]];
+            return ra != rb ? ra > rb : first[a] < first[b];
+        });
+        for (uint32_t k = 0; k < take; ++k) in_hot[idx[k]] = 1;
+    } else {
+        for (uint32_t k = 0; k < take; ++k) in_hot[order[k]] = 1;
+    }
+    std::vector<uint32_t> slot(nr);
+    uint32_t k = 0;
+    for (uint32_t r : order)
+        if (in_hot[r]) slot[r] = k++;
+    for (uint32_t r : order)
+        if (!in_hot[r]) slot[r] = k++;
+    out.n_entries = 2 * nr;
+    out.hot = 2 * take;
+    const uint32_t m = out.n_entries + 1;
+    const int32_t end = (int32_t)(16 * out.n_entries);
+    auto P = [&](uint32_t i) -> int32_t { return i >= n ? end : (int32_t)(32 * slot[(size_t)rec_of[i]]); };
+    out.start = (uint32_t)P(0);
+    out.soa.assign((size_t)m * 8 + quadtab.size(), 0.0f);
+    auto put = [&](uint32_t j, const float a[4], const float b[4]) {  // entry j's halves
+        std::memcpy(&out.soa[4 * (size_t)j], a, 16);
+        std::memcpy(&out.soa[4 * ((size_t)m + j)], b, 16);
+    };
+    auto word = [](float* f, int32_t v) { std::memcpy(f, &v, 4); };
+    const float inf = std::numeric_limits<float>::infinity();
+    const float sa[4] = {inf, inf, inf, 0.0f}, sb[4] = {-inf, -inf, -inf, 0.0f};
+    for (uint32_t r = 0; r < nr; ++r) {
+        const uint32_t p = first[r], u = q(p);
+        for (uint32_t s2 = 0; s2 < 2; ++s2) {
+            const uint32_t i = s2 == 0 ? p : u, j = 2 * slot[r] + s2;
+            float a[4], b[4];
+            if (i >= n) {  // the walk's end as slot 1: the sentinel (empty box, escape = next = the end)
+                std::memcpy(a, sa, 16);
+                std::memcpy(b, sb, 16);
+                word(&a[3], end);
+                word(&b[3], end);
+                put(j, a, b);
+                continue;
+            }
+            std::memcpy(a, E[i].a, 16);
+            std::memcpy(b, E[i].b, 16);
+            const int32_t t = tag(i);
+            if (t == RTX_E_NODE) {
+                word(&b[3], P(i + 1));                 // the box passes: the record of the first child
+                word(&a[3], s2 ? P(q(i)) : -1);        // slot 1 fails: the record of its escape (slot 0: slot 1)
+            } else {
+                word(&b[2], s2 ? P(i + 1) : 0);        // slot 1: the record of its successor (slot 0: slot 1)
+                if (t >= 0) {
+                    word(&b[3], RTX_DEV_SPHERE(t));
+                    int32_t si;  // the sphere's rank word (sphere_test RANK_WORD) in place of its index
+                    std::memcpy(&si, &E[i].b[1], 4);
+                    word(&b[1], (int32_t)rank[(uint32_t)si]);
+                }
+            }
+            put(j, a, b);
+        }
+    }
+    float a[4], b[4];  // the sentinel entry after the records
+    std::memcpy(a, sa, 16);
+    std::memcpy(b, sb, 16);
+    word(&a[3], end);
+    word(&b[3], end);
+    put(out.n_entries, a, b);
+    if (!quadtab.empty()) std::memcpy(&out.soa[8 * (size_t)m], quadtab.data(), quadtab.size() * sizeof(float));
+}
+
 // Upload the walk layout for `cam` to copy c (current device = c's; s->mu held).
 int ensure_layout(rtx_scene* s, DeviceCopy* c, const rtx_camera* cam, bool near = false) {
     const uint32_t oct = layout_slot(s, cam, near);
@@ -569,6 +696,24 @@ int ensure_layout(rtx_scene* s, DeviceCopy* c, const rtx_camera* cam, bool near 
     const std::vector<rtx_entry>* E = nullptr;
     if (int rc = scene_layout(s, cam, &E, near)) return rc;
     DeviceLayout& lay = c->lay[oct];
+    // A layout in HBM with an LDS cache (config 4's): the paired walk's records, unless RTX_W2=0.
+    // (Scenes with Perlin noise, or without a cache, walk HBM without the cache kernels, which read entries only.)
+    // RTX_W2=2 (tests): records for any layout — walked only from HBM (RTX_FLAG_NO_LDS), else the launch fails.
+    const uint32_t cap = env_knob("RTX_HOT_ENTRIES", rtxd::HOT_ENTRIES_MAX, 0, rtxd::HOT_ENTRIES_MAX) & ~1u;
+    const uint32_t w2k = env_knob("RTX_W2", 1, 0, 2);
+    if (cap > 0 && !s->has_noise && (w2k == 2 || (w2k == 1 && (E->size() + 1) * 16 > rtxd::LDS_B))) {
+        W2Layout w;
+        build_w2(*E, &s->reads[oct], cap, s->sphere_rank, s->quadtab, w);
+        // (+64 B: a lane's record read at the walk's end may touch the sentinel's neighbour; its result is unused)
+        HIP_TRY(hipMalloc(&lay.entries, w.soa.size() * sizeof(float) + 64));
+        HIP_TRY(hipMemcpy(lay.entries, w.soa.data(), w.soa.size() * sizeof(float), hipMemcpyHostToDevice));
+        lay.n_entries = w.n_entries;
+        lay.hot = w.hot;
+        lay.start = w.start;
+        lay.w2 = 1;
+        return RTX_OK;
+    }
+    lay.n_entries = (uint32_t)E->size();
     HIP_TRY(hipMalloc(&lay.entries, (E->size() + 1) * sizeof(rtx_entry) + s->quadtab.size() * sizeof(float)));
     {  // device layout: all 'a' halves, then all 'b' halves (rtxd::SceneRef), each ending
        // with the sentinel entry (rtx_layout.h).  Every entry names its successor (node: next
@@ -938,7 +1083,7 @@ rtxd::Params make_params(const rtx_scene* s, const DeviceCopy* c, uint32_t oct, 
     std::memset(&p, 0, sizeof(p));
     const DeviceLayout& lay = c->lay[oct];
     p.entries = reinterpret_cast<const float4*>(lay.entries);
-    p.n_entries = (uint32_t)s->layouts[oct].size();
+    p.n_entries = lay.n_entries;
     p.n_quads = (uint32_t)(s->quadtab.size() / 16);
     p.n_materials = (uint32_t)s->materials.size();
     p.materials = c->materials;
@@ -969,6 +1114,7 @@ rtxd::Params make_params(const rtx_scene* s, const DeviceCopy* c, uint32_t oct, 
     p.n_hot = lay.hot;
     p.start = lay.start;
     p.prim_end = lay.prim_end;
+    p.w2 = lay.w2;
     return p;
 }
 
@@ -987,6 +1133,8 @@ int enqueue_on(rtx_scene* s, DeviceCopy* c, const rtx_camera* cam, uint64_t seed
     if (tier) {
         if (int rc = ensure_layout(s, c, cam, true)) return rc;
         pn = make_params(s, c, layout_slot(s, cam, true), cam, seed, r, d_out);
+        // the paired walk's records are read by the LDS-cache kernels only: two layouts placed unalike walk alone
+        if ((p.w2 || pn.w2) && rtxd::tier_placement(pn, p, flags) != RTX_SCENE_LDS_CACHE) tier = false;
     }
     *tiered = false;
     const uint32_t th = (flags >> 8) & 0x7Fu;  // RTX_FLAG_SHADE_THRESH(n) override

@@ -501,6 +501,9 @@ struct Params {
     uint32_t* drain_count;   // 2 x the near grid, zeroed per chunk
     uint32_t drain_region;   // records per workgroup (the queue's capacity over the near grid)
     uint32_t drain;          // 1: the timed tiered render drains (RTX_DRAIN=0: the far pass's own launch, A/B)
+    // The layout is the paired walk's records (rtx_capi.hip build_w2): a layout in HBM with an LDS
+    // cache, walked by trav_step_w2 (only the cache kernels, HYB, ever get one; never a drain launch).
+    uint32_t w2;
 };
 constexpr uint32_t DRAIN_WORDS = 16384;  // Params::drain_count's words: near grids up to 8192 workgroups
 
@@ -931,11 +934,10 @@ __device__ __forceinline__ bool own_box_pass(const Trav& t, const Ray& r, const 
 // check whatever boxes pass (§14-15), so only the work counts change — as the oracle's near walk restates.
 // Rays outside near_fma_ok take the reference's form (per lane in the select form; the MED3 form runs
 // only when every walking lane's ray is safe, which for the near pass includes near_fma_ok).
-template <bool COUNT, bool MED3 = false, bool FMA = false>
-__device__ __forceinline__ void box_step(Trav& t, const Ray& r, const float4 ea, const float4 eb, int32_t tag,
-                                         Counters& cnt, const V3 no = V3{0.0f, 0.0f, 0.0f}) {
+template <bool MED3 = false, bool FMA = false>
+__device__ __forceinline__ bool box_hit(const Trav& t, const Ray& r, const float4 ea, const float4 eb,
+                                        const V3 no = V3{0.0f, 0.0f, 0.0f}) {
     const float tmin = 0.001f;  // ray.go:37
-    if (COUNT && __float_as_int(ea.w) != tag) ++cnt.node_visits;  // (not the sentinel: escape == next)
     if constexpr (MED3) {
         float tax, tbx, tay, tby, taz, tbz;
         if constexpr (FMA) {
@@ -949,9 +951,7 @@ __device__ __forceinline__ void box_step(Trav& t, const Ray& r, const float4 ea,
         }
         const float lo = med3(med3(med3(tmin, tax, tbx), tay, tby), taz, tbz);
         const float hi = med3(med3(med3(t.closest, tax, tbx), tay, tby), taz, tbz);
-        const uint32_t take = 0u - (uint32_t)(lo < hi);
-        t.i = ((uint32_t)tag & take) | ((uint32_t)__float_as_int(ea.w) & ~take);
-        return;
+        return lo < hi;
     }
     // Per axis: t0 = (min - o) * invD, t1 = (max - o) * invD, swapped if invD < 0.
     // (Scalar FP32 throughout: a v_pk_mul_f32 / v_pk_add_f32 issues at a quarter of
@@ -979,9 +979,16 @@ __device__ __forceinline__ void box_step(Trav& t, const Ray& r, const float4 ea,
     // result: the operands are arithmetic results or +inf, never signalling NaNs.
     float hi;
     asm("v_min3_f32 %0, %1, %2, %3\n\tv_min_f32 %0, %0, %4" : "=&v"(hi) : "v"(t.closest), "v"(t1x), "v"(t1y), "v"(t1z));
+    return lo < hi;
+}
+
+template <bool COUNT, bool MED3 = false, bool FMA = false>
+__device__ __forceinline__ void box_step(Trav& t, const Ray& r, const float4 ea, const float4 eb, int32_t tag,
+                                         Counters& cnt, const V3 no = V3{0.0f, 0.0f, 0.0f}) {
+    if (COUNT && __float_as_int(ea.w) != tag) ++cnt.node_visits;  // (not the sentinel: escape == next)
     // the next entry on a box hit, else the escape (both stored as walk positions): a
     // mask select (a ?: here became a branch).
-    const uint32_t take = 0u - (uint32_t)(lo < hi);
+    const uint32_t take = 0u - (uint32_t)box_hit<MED3, FMA>(t, r, ea, eb, no);
     t.i = ((uint32_t)tag & take) | ((uint32_t)__float_as_int(ea.w) & ~take);
 }
 
@@ -1005,6 +1012,74 @@ __device__ __forceinline__ void trav_step(Trav& t, const Ray& r, const SceneRef 
         if (QUADS && tag == RTX_E_QUAD) quad_test<COUNT>(t, r, E, ea, eb, t.i, cnt);
         else sphere_test<COUNT, MED3, FIXED, !FIXED>(t, r, ea, eb, t.i, cnt, E.b);
         t.i = (uint32_t)__float_as_int(eb.z);  // the primitive's successor
+    }
+}
+
+// The record at walk position `pos` of the paired walk (build_w2): entries pos and pos + 16, both halves, in one
+// round trip — from the LDS cache (its 'a' halves at 0, 'b' halves at HOT_B) below E.hot, else from HBM, both kinds
+// issued under their exec masks before one wait (load_entry<HYB>).
+__device__ __forceinline__ void load_record(const SceneRef E, uint32_t pos, float4& a0, float4& b0, float4& a1, float4& b1) {
+    uint64_t sv, m;
+    asm volatile("s_mov_b64 %[sv], exec\n\t"
+                 "v_cmp_gt_u32_e64 %[m], %[hot], %[pos]\n\t" /* the LDS cache's lanes */
+                 "s_andn2_b64 exec, %[sv], %[m]\n\t"
+                 "s_cbranch_execz LG%=\n\t"
+                 "global_load_dwordx4 %[a0], %[pos], %[ba]\n\t"
+                 "global_load_dwordx4 %[a1], %[pos], %[ba] offset:16\n\t"
+                 "global_load_dwordx4 %[b0], %[pos], %[bb]\n\t"
+                 "global_load_dwordx4 %[b1], %[pos], %[bb] offset:16\n"
+                 "LG%=:\n\t"
+                 "s_and_b64 exec, %[sv], %[m]\n\t"
+                 "s_cbranch_execz LL%=\n\t"
+                 "ds_read_b128 %[a0], %[pos]\n\t"
+                 "ds_read_b128 %[a1], %[pos] offset:16\n\t"
+                 "ds_read_b128 %[b0], %[pos] offset:%[lb]\n\t"
+                 "ds_read_b128 %[b1], %[pos] offset:%[lb16]\n"
+                 "LL%=:\n\t"
+                 "s_mov_b64 exec, %[sv]\n\t"
+                 "s_waitcnt vmcnt(0) lgkmcnt(0)"
+                 : [a0] "=&v"(a0), [b0] "=&v"(b0), [a1] "=&v"(a1), [b1] "=&v"(b1), [sv] "=&s"(sv), [m] "=&s"(m)
+                 : [pos] "v"(pos), [hot] "s"(E.hot), [ba] "s"(E.a), [bb] "s"(E.b), [lb] "i"(HOT_B), [lb16] "i"(HOT_B + 16)
+                 : "scc");
+}
+
+// One step of the paired walk (rtx_capi.hip build_w2) for a layout in HBM with its LDS cache: the
+// record at t.i holds the threaded walk's entry p and its fail successor q(p).  Slot 0: a node whose box passes
+// descends (the record of its first child, b.w); otherwise (a failed box, a primitive tested) the lane goes on to
+// slot 1 in the same step: a node to its first child's record (b.w) or its escape's (a.w), a primitive tested and to
+// its successor's record (b.z).  The same tests in the same order with the same bounds as trav_step on the threaded
+// layout — so the same hits, draws and work counters — in fewer dependent reads.  Lanes at the walk's end (the
+// sentinel position) read nothing.
+template <bool COUNT, bool QUADS = false, bool MED3 = false, bool FMA = false>
+__device__ __forceinline__ void trav_step_w2(Trav& t, const Ray& r, const SceneRef E, Counters& cnt, uint32_t end,
+                                             const V3 no = V3{0.0f, 0.0f, 0.0f}) {
+    if (t.i >= end) return;
+    const uint32_t pos = t.i;
+    float4 a0, b0, a1, b1;
+    load_record(E, pos, a0, b0, a1, b1);
+    if (COUNT && pos < E.hot) ++cnt.cache_hits;
+    const int32_t tag0 = __float_as_int(b0.w);
+    bool down = false;
+    if (tag0 > -2) {  // a node (slot 0 is never the sentinel)
+        if (COUNT) ++cnt.node_visits;
+        down = box_hit<MED3, FMA>(t, r, a0, b0, no);
+    } else if (QUADS && tag0 == RTX_E_QUAD) {
+        quad_test<COUNT>(t, r, E, a0, b0, pos, cnt);
+    } else {
+        sphere_test<COUNT, MED3, false, true>(t, r, a0, b0, pos, cnt, E.b);
+    }
+    if (down) {
+        t.i = (uint32_t)tag0;
+        return;
+    }
+    const int32_t tag1 = __float_as_int(b1.w);
+    if (tag1 > -2) {  // a node, or the sentinel (escape == next: not a test)
+        if (COUNT && __float_as_int(a1.w) != tag1) ++cnt.node_visits;
+        t.i = box_hit<MED3, FMA>(t, r, a1, b1, no) ? (uint32_t)tag1 : (uint32_t)__float_as_int(a1.w);
+    } else {
+        if (QUADS && tag1 == RTX_E_QUAD) quad_test<COUNT>(t, r, E, a1, b1, pos + 16, cnt);
+        else sphere_test<COUNT, MED3, false, true>(t, r, a1, b1, pos + 16, cnt, E.b);
+        t.i = (uint32_t)__float_as_int(b1.z);
     }
 }
 

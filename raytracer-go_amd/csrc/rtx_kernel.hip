@@ -57,6 +57,24 @@ namespace rtxd {
 #ifndef RTX_CLAIM_GUARD  // 0: the guard compiled out (A/B of its cost only)
 #define RTX_CLAIM_GUARD 1
 #endif
+#ifndef RTX_KARG_RELOAD  // 1: uniform values of the shading phase re-read from the kernel arguments at their use (A/B)
+#define RTX_KARG_RELOAD 0
+#endif
+#ifndef RTX_NT_COLOR  // 1: the sample colours stored non-temporally (A/B of the scratch's write amplification)
+#define RTX_NT_COLOR 0
+#endif
+// The kernel's Params as its kernel arguments hold them, behind an opaque copy of their address: a field read
+// through it is loaded (s_load) at its use instead of being kept live through the main loop, where the kernel
+// is at the SGPR limit and a live value is spilled to a VGPR lane (a v_readlane per use).  Only
+// for fields whose kernel-argument value is the one in use: render_items' Params, render_drain's near Params
+// (its first member), whose camera and near region its far phase shares.
+__device__ __forceinline__ const Params& karg_params() {
+    typedef const __attribute__((address_space(4))) Params* KP;
+    KP q = (KP)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(q));
+    return *(const Params*)q;
+}
+
 __device__ __forceinline__ bool partial_wave() { return RTX_CLAIM_GUARD && __builtin_amdgcn_read_exec() != ~0ull; }
 // The debug library only: the odd lanes stay out of claim site `site` (tests/test_claim_guard.py).
 __device__ __forceinline__ bool dbg_skip(const Params& p, uint32_t site, uint32_t lane) {
@@ -97,7 +115,7 @@ __device__ __forceinline__ void traverse_loop(uint32_t& mode, Trav& t, const Ray
                                               uint32_t n_entries, uint32_t thresh, Counters& cnt,
                                               uint64_t& wave_iters, uint64_t& lane_steps, uint64_t& shade_phases,
                                               uint64_t& shade_lanes, uint64_t& idle_lanes, uint64_t& parked,
-                                              uint64_t& deferred, uint32_t prim_batch) {
+                                              uint64_t& deferred, uint32_t prim_batch, bool w2) {
     // The lane modes are fixed during the phase except walking -> waiting (mode 0 -> 1) on
     // reaching the sentinel, so the votes are SALU on masks taken once: walking lanes W, waiting
     // lanes P0, lanes without an item D; per iteration only `at_end` is voted.
@@ -120,7 +138,17 @@ __device__ __forceinline__ void traverse_loop(uint32_t& mode, Trav& t, const Ray
         // the wave per step.
         uint32_t done = 0;  // COUNT: lane-steps that tested an entry (a lane on the sentinel idles)
         uint32_t idle = 0;  // COUNT: parked (low 16 bits) and deferred (high 16 bits) lane-steps
-        if constexpr (BATCH) {
+        if (HYB && w2) {  // the paired walk's records
+#pragma unroll
+            for (int s = 0; s < STEPS; ++s) {
+                if (COUNT) {
+                    const uint32_t w = (uint32_t)__popcll(ballot(t.i < 16 * n_entries));
+                    done += w;
+                    idle += 64u - w;
+                }
+                trav_step_w2<COUNT, QUADS, MED3, FMA>(t, r, E, cnt, 16 * n_entries, no);
+            }
+        } else if constexpr (BATCH) {
 #pragma unroll
             for (int s = 0; s < STEPS; ++s)
                 done += trav_step_batched<COUNT, QUADS, FIXED, HYB, MED3, FMA>(t, r, E, cnt, 16 * n_entries,
@@ -167,17 +195,17 @@ __device__ __forceinline__ void traverse_phase(uint32_t& mode, Trav& t, const Ra
                                                uint32_t n_entries, uint32_t thresh, Counters& cnt,
                                                uint64_t& wave_iters, uint64_t& lane_steps, uint64_t& shade_phases,
                                                uint64_t& shade_lanes, uint64_t& idle_lanes, uint64_t& parked,
-                                               uint64_t& deferred, uint32_t prim_batch = 0) {
+                                               uint64_t& deferred, uint32_t prim_batch = 0, bool w2 = false) {
     if (ballot(!t.safe && t.i < 16 * n_entries) == 0)
         traverse_loop<COUNT, STEPS, QUADS, FIXED, HYB, BATCH, true, FMA>(mode, t, r, E, n_entries, thresh, cnt,
                                                                        wave_iters, lane_steps, shade_phases,
                                                                        shade_lanes, idle_lanes, parked, deferred,
-                                                                       prim_batch);
+                                                                       prim_batch, w2);
     else
         traverse_loop<COUNT, STEPS, QUADS, FIXED, HYB, BATCH, false, FMA>(mode, t, r, E, n_entries, thresh, cnt,
                                                                         wave_iters, lane_steps, shade_phases,
                                                                         shade_lanes, idle_lanes, parked, deferred,
-                                                                        prim_batch);
+                                                                        prim_batch, w2);
 }
 
 enum : uint32_t { M_TRAV = 0, M_SHADE = 1, M_START = 2, M_DONE = 3, M_CLAIM = 4 };
@@ -338,9 +366,15 @@ __device__ __forceinline__ void render_body(const Params& p, const uint64_t t0 =
 
     auto store = [&](V3 col) {  // the item's colour, GetColor's result for sample k
         float* o = p.scratch + (size_t)(rng.sample - p.k0) * tile_floats + (size_t)pix * 3;
-        o[0] = col.x;
-        o[1] = col.y;
-        o[2] = col.z;
+        if (RTX_NT_COLOR) {
+            __builtin_nontemporal_store(col.x, o);
+            __builtin_nontemporal_store(col.y, o + 1);
+            __builtin_nontemporal_store(col.z, o + 2);
+        } else {
+            o[0] = col.x;
+            o[1] = col.y;
+            o[2] = col.z;
+        }
         ++items_done;
     };
 
@@ -394,8 +428,9 @@ __device__ __forceinline__ void render_body(const Params& p, const uint64_t t0 =
         }
     };
     auto defer_far = [&](bool& ready) {  // segments that would start outside the near region
-        const bool far = ready && !(r.o.x >= p.near_min[0] && r.o.x <= p.near_max[0] && r.o.y >= p.near_min[1] &&
-                                    r.o.y <= p.near_max[1] && r.o.z >= p.near_min[2] && r.o.z <= p.near_max[2]);
+        const Params& q = RTX_KARG_RELOAD ? karg_params() : p;
+        const bool far = ready && !(r.o.x >= q.near_min[0] && r.o.x <= q.near_max[0] && r.o.y >= q.near_min[1] &&
+                                    r.o.y <= q.near_max[1] && r.o.z >= q.near_min[2] && r.o.z <= q.near_max[2]);
         defer(far);
         if (far) ready = false;
     };
@@ -422,7 +457,7 @@ __device__ __forceinline__ void render_body(const Params& p, const uint64_t t0 =
         traverse_phase<COUNT, STEPS, QUADS, USE_LDS, HYB, USE_LDS || (RTX_HYB_BATCH && HYB), TIER == 1 && RTX_NEAR_FMA>(
             mode, t, r, E, n_entries, thresh, cnt, wave_iters,
                                                               lane_steps, shade_phases, shade_lanes, idle_lanes,
-                                                              parked, deferred, p.prim_batch);
+                                                              parked, deferred, p.prim_batch, HYB && p.w2);
         if (TIME) {
             const uint64_t now = __builtin_amdgcn_s_memtime();
             trav_cycles += now - clk;
@@ -525,6 +560,7 @@ __device__ __forceinline__ void render_body(const Params& p, const uint64_t t0 =
                 const uint32_t blk = cursor >> 6;
                 if (blk != pool_blk) {  // the block's 64 camera rays, one per lane (sample u_k0 + blk, pixel lane)
                     pool_blk = blk;
+                    const rtx_camera& c = RTX_KARG_RELOAD ? karg_params().cam : p.cam;
                     const uint32_t lx = u_x + (lane & tw_mask), lr = u_r + (lane >> twl);
                     if (lx < p.width && lr < p.rows) {
                         const uint32_t x = p.x0 + lx, y = ST ? u_y + (lane >> twl) : p.y0 + p.rank + lr * p.world;
@@ -984,6 +1020,7 @@ hipError_t launch_render_t(const Params& p, uint32_t flags, hipStream_t stream, 
     const bool count = (flags & RTX_FLAG_COUNTERS) != 0;
     if (far) {  // the caller checked: spheres only, both layouts placed alike (tier_placement), no noise
         const uint32_t place = tier_placement(p, *far, flags);
+        if ((p.w2 || far->w2) && place != RTX_SCENE_LDS_CACHE) return hipErrorInvalidValue;  // (records: cache kernels)
         if (p.tier != 1 || far->tier != 2 || !p.defer || !far->defer || !p.redo_bits || p.n_quads || p.has_noise)
             return hipErrorInvalidValue;
         const bool clk = !count && (flags & RTX_FLAG_TIMING);  // diagnostics: the wave-cycle split of the passes
@@ -1004,6 +1041,7 @@ hipError_t launch_render_t(const Params& p, uint32_t flags, hipStream_t stream, 
                      : launch_tiered<false, V, MV, false, false, false, false, ST>(p, *far, stream);
     }
     const bool use_lds = scene_placement(p, flags) == RTX_SCENE_IN_LDS;
+    if (p.w2 && scene_placement(p, flags) != RTX_SCENE_LDS_CACHE) return hipErrorInvalidValue;  // (records: cache kernels)
     if (!count && (flags & RTX_FLAG_TIMING) && !p.has_noise && p.item_waves != 4)  // diagnostics: sphere scenes
         return p.n_quads ? launch_items<false, true, false, RTX_V3_WAVES, RTX_V3_MINW, true, false, ST>(p, use_lds, stream)
                          : launch_items<false, false, false, RTX_V3_WAVES, RTX_V3_MINW, true, false, ST>(p, use_lds, stream);

@@ -58,6 +58,8 @@ out = {
     "valu_lane_frac": round(thread_cycles / (64.0 * insts), 4),
     "kernels": sorted({k for (f, c, k) in disp}),
     "librtx_sha256_16": hashlib.sha256(open(args.lib, "rb").read()).hexdigest()[:16],
+    # every counter of the pass per launch (SQ_INSTS_SALU, SQ_WAIT_ANY, SQ_WAVE_CYCLES, ... when collected)
+    "counters_per_launch": {c: v / (args.renders or renders["SQ_INSTS_VALU"]) for c, v in sorted(vals.items())},
     "method": "rocprofv3 --kernel-trace --pmc SQ_INSTS_VALU SQ_THREAD_CYCLES_VALU GRBM_GUI_ACTIVE ...; "
               "issue frac = 2 cycles x SQ_INSTS_VALU / (GRBM_GUI_ACTIVE / 8 XCDs x 1024 SIMDs)",
 }

@@ -591,3 +591,43 @@ def test_tier_overflow_across_chunks(torch_cuda, spheres, dev_spheres, monkeypat
         if counters:
             for k in ("samples", "segments", "hits", "texel_fetches", "rng_draws"):
                 assert getattr(st, k) == cnt[k], (k, getattr(st, k), cnt[k])
+
+
+@pytest.mark.parametrize("scene,width,spp", [("random_spheres", 160, 4), ("cornell_box", 120, 8),
+                                             ("earth_dielectric", 192, 4), ("nested_worlds", 160, 4)])
+def test_paired_walk_records_small_scenes(torch_cuda, built, monkeypatch, scene, width, spp):
+    """The paired walk forced on small scenes (RTX_W2=2) and walked from HBM through a 64-entry LDS
+    cache (RTX_FLAG_NO_LDS): tiered sphere scenes (near and far trees both as records), quads, the image texture,
+    Worlds nested in the tree.  Bit-identical to the oracle with every work counter equal: a record's step takes
+    the threaded walk's tests in its order with its bounds."""
+    monkeypatch.setenv("RTX_W2", "2")
+    monkeypatch.setenv("RTX_HOT_ENTRIES", "64")
+    s = rtx.HostScene(scene, 1)
+    dev = rtx.DeviceScene(s.desc)
+    cam = s.camera(width=width, spp=spp)
+    reg = rtx.Region(0, 0, cam.image_width, cam.image_height, 0, 1)
+    check_scene(torch_cuda, dev, s.desc, cam, 29, reg, flags=rtx.RTX_FLAG_NO_LDS)
+
+
+def test_paired_walk_equals_entry_walk_c4(torch_cuda, built, monkeypatch):
+    """Config 4's layouts as records (the default for a layout in HBM with an LDS cache) against the same layouts as
+    threaded entries (RTX_W2=0): the same image and the same work counters (box and sphere tests, hits, draws,
+    segments), in fewer walk steps."""
+    scene = rtx.HostScene("stress_100k", 1)
+    cam = scene.camera(width=1920, spp=2, depth=50)
+    reg = rtx.Region(640, 360, 64, 48, 0, 1)
+    out = {}
+    for w2 in ("0", "1"):
+        monkeypatch.setenv("RTX_W2", w2)
+        dev = rtx.DeviceScene(scene.desc)
+        img, st = gpu_region(torch_cuda, dev, cam, 31, reg, counters=True)
+        timed, _ = gpu_region(torch_cuda, dev, cam, 31, reg, counters=False)
+        assert np.array_equal(img, timed), w2
+        out[w2] = (img, st)
+        dev.close()
+    (a, sa), (b, sb) = out["0"], out["1"]
+    assert np.array_equal(a, b)
+    for k in ("samples", "segments", "node_visits", "prim_tests", "hits", "texel_fetches", "rng_draws",
+              "deferred_paths"):
+        assert getattr(sa, k) == getattr(sb, k), (k, getattr(sa, k), getattr(sb, k))
+    assert sb.lane_steps < 0.8 * sa.lane_steps, (sa.lane_steps, sb.lane_steps)
