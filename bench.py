@@ -390,32 +390,26 @@ def main():
     for _ in range(args.warmup):
         step([], [])
     barrier()
-    kms, gms = [], []
     # The K steps are enqueued back to back on the stream (no stats read between them, so the GPU does not idle for
     # a host round trip per step): per step the render, then (N > 1) the RCCL gather of the shards and rank 0's
     # de-interleave, each bracketed by events on that stream — the kernel time and the gather time per step.  (An
     # RCCL collective on torch's NCCL stream waits for this stream's render and makes this stream wait for it, so
     # the next render does not overwrite the shard before it is sent.)  Nothing of the library's stats is read in
     # the timed region: its sticky error word is checked once after it, for all K renders.
-    # (A rehearsal on one GPU gathers through gloo and host copies, which wait on the host: its old step loop.)
-    pipelined = not shared
+    # (A rehearsal on one GPU runs the same loop; its gloo gather takes host copies, which wait on the host.)
     timed_img = None
+    evs = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(3)) for _ in range(args.steps)]
     t0 = time.perf_counter()
-    if pipelined:
-        evs = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(3)) for _ in range(args.steps)]
-        for i, (e0, e1, e2) in enumerate(evs):
-            if i == args.debug_partial_step:  # (test hook: the debug library's partial-wave claim in this step only)
-                os.environ["RTX_DEBUG_PARTIAL_SITE"] = "3"
-            e0.record()
-            dev.render_region(cam, args.seed, reg, shard.data_ptr(), stream, counters=False, timed=False)
-            e1.record()
-            os.environ.pop("RTX_DEBUG_PARTIAL_SITE", None)
-            timed_img = shard[:rtx.region_rows(reg)] if args.shard else gather_image(shard, H, rank, world,
-                                                                                     stripe=stripe)
-            e2.record()
-    else:
-        for _ in range(args.steps):
-            timed_img = step(kms, gms)
+    for i, (e0, e1, e2) in enumerate(evs):
+        if i == args.debug_partial_step:  # (test hook: the debug library's partial-wave claim in this step only)
+            os.environ["RTX_DEBUG_PARTIAL_SITE"] = "3"
+        e0.record()
+        dev.render_region(cam, args.seed, reg, shard.data_ptr(), stream, counters=False, timed=False)
+        e1.record()
+        os.environ.pop("RTX_DEBUG_PARTIAL_SITE", None)
+        timed_img = shard[:rtx.region_rows(reg)] if args.shard else gather_image(shard.cpu() if shared else shard, H,
+                                                                                 rank, world, stripe=stripe)
+        e2.record()
     barrier()
     elapsed = time.perf_counter() - t0
     # Every timed render's kernel ran without a watchdog stop or a partial-wave claim, or the bench fails here
@@ -423,9 +417,8 @@ def main():
     rtx.device_check(torch.cuda.current_device())
     # the frame the last timed step produced (rank 0: the gathered image), hashed before anything renders again
     timed_hash = framebuffer_hash(timed_img) if rank == 0 and not args.no_hash else None
-    if pipelined:
-        kms = [e0.elapsed_time(e1) for e0, e1, _ in evs]
-        gms = [e1.elapsed_time(e2) for _, e1, e2 in evs]
+    kms = [e0.elapsed_time(e1) for e0, e1, _ in evs]
+    gms = [e1.elapsed_time(e2) for _, e1, e2 in evs]
     img = timed_img
     if not args.no_verify:
         img = step([], [])  # (untimed: the frame once more, with the library's stats and error check)

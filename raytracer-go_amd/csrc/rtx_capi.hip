@@ -613,17 +613,28 @@ void build_w2(const std::vector<rtx_entry>& E, const std::vector<double>* R, uin
         }
     }
     const uint32_t nr = (uint32_t)first.size();
-    // storage order: the hot records (most reads first when estimated, else walk order), then the rest, each in walk order
+    // storage order: the hot records (most reads first when estimated, else walk order), then the rest, each in walk
+    // order.  A record's reads are its first entry's (R, the threaded walk's) less the arrivals there that a record
+    // before it takes as its slot 1 — those of a record whose first entry does not descend (a node's fail fraction
+    // 1 - R[p + 1] / R[p]: p + 1, its first child, is read once per pass of p; a primitive always goes on).
     std::vector<uint32_t> order(nr);
     for (uint32_t r = 0; r < nr; ++r) order[r] = r;
     std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return first[a] < first[b]; });
     const uint32_t take = std::min<uint32_t>(cap / 2, nr);
     std::vector<uint8_t> in_hot(nr, 0);
     if (R && R->size() == n) {
+        std::vector<double> absorbed(n + 1, 0.0), reads(nr, 0.0);
+        for (uint32_t r : order) {  // (q(p) > p: every record taking arrivals at p comes before p's)
+            const uint32_t p = first[r], u = q(p);
+            reads[r] = std::max(0.0, (*R)[p] - absorbed[p]);
+            const double f = tag(p) != RTX_E_NODE ? 1.0
+                             : (*R)[p] > 0.0    ? std::max(0.0, 1.0 - (p + 1 < n ? (*R)[p + 1] : 0.0) / (*R)[p])
+                                                : 1.0;
+            absorbed[u] += reads[r] * f;
+        }
         std::vector<uint32_t> idx(order);
         std::partial_sort(idx.begin(), idx.begin() + take, idx.end(), [&](uint32_t a, uint32_t b) {
-            const double ra = (*R)[first[a]], rb = (*R)[first[b]];
-            return ra != rb ? ra > rb : first[a] < first[b];
+            return reads[a] != reads[b] ? reads[a] > reads[b] : first[a] < first[b];
         });
         for (uint32_t k = 0; k < take; ++k) in_hot[idx[k]] = 1;
     } else {
@@ -696,11 +707,11 @@ int ensure_layout(rtx_scene* s, DeviceCopy* c, const rtx_camera* cam, bool near 
     const std::vector<rtx_entry>* E = nullptr;
     if (int rc = scene_layout(s, cam, &E, near)) return rc;
     DeviceLayout& lay = c->lay[oct];
-    // A layout in HBM with an LDS cache (config 4's): the paired walk's records, unless RTX_W2=0.
+    // RTX_W2=1: a layout in HBM with an LDS cache (config 4's) as the paired walk's records.
     // (Scenes with Perlin noise, or without a cache, walk HBM without the cache kernels, which read entries only.)
     // RTX_W2=2 (tests): records for any layout — walked only from HBM (RTX_FLAG_NO_LDS), else the launch fails.
     const uint32_t cap = env_knob("RTX_HOT_ENTRIES", rtxd::HOT_ENTRIES_MAX, 0, rtxd::HOT_ENTRIES_MAX) & ~1u;
-    const uint32_t w2k = env_knob("RTX_W2", 1, 0, 2);
+    const uint32_t w2k = env_knob("RTX_W2", 0, 0, 2);  // (off by default: config 4 +6.5 %)
     if (cap > 0 && !s->has_noise && (w2k == 2 || (w2k == 1 && (E->size() + 1) * 16 > rtxd::LDS_B))) {
         W2Layout w;
         build_w2(*E, &s->reads[oct], cap, s->sphere_rank, s->quadtab, w);

@@ -57,8 +57,11 @@ namespace rtxd {
 #ifndef RTX_CLAIM_GUARD  // 0: the guard compiled out (A/B of its cost only)
 #define RTX_CLAIM_GUARD 1
 #endif
-#ifndef RTX_KARG_RELOAD  // 1: uniform values of the shading phase re-read from the kernel arguments at their use (A/B)
-#define RTX_KARG_RELOAD 0
+#ifndef RTX_KARG_RELOAD  // 1: uniform values of the shading phase re-read from the kernel arguments at their use (0: A/B)
+#define RTX_KARG_RELOAD 1
+#endif
+#ifndef RTX_HYB_DRAIN  // 1: the drain also for scenes in HBM with an LDS cache (A/B; round 5: +2.3 % at config 4)
+#define RTX_HYB_DRAIN 0
 #endif
 #ifndef RTX_NT_COLOR  // 1: the sample colours stored non-temporally (A/B of the scratch's write amplification)
 #define RTX_NT_COLOR 0
@@ -428,7 +431,7 @@ __device__ __forceinline__ void render_body(const Params& p, const uint64_t t0 =
         }
     };
     auto defer_far = [&](bool& ready) {  // segments that would start outside the near region
-        const Params& q = RTX_KARG_RELOAD ? karg_params() : p;
+        const Params& q = RTX_KARG_RELOAD && !HYB ? karg_params() : p;  // (the cache kernels: kept live)
         const bool far = ready && !(r.o.x >= q.near_min[0] && r.o.x <= q.near_max[0] && r.o.y >= q.near_min[1] &&
                                     r.o.y <= q.near_max[1] && r.o.z >= q.near_min[2] && r.o.z <= q.near_max[2]);
         defer(far);
@@ -686,10 +689,11 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_items(Params p) {
 // The far phase's own settings (the rest of its Params are the near pass's): its layout and walk knobs.
 struct FarLayout {
     const float4* entries;
-    uint32_t n_entries, n_hot, start, prim_end, shade_thresh, refill_hits, prim_batch;
+    uint32_t n_entries, n_hot, start, prim_end, shade_thresh, refill_hits, prim_batch, w2;
 };
 inline FarLayout far_layout(const Params& pf) {
-    return FarLayout{pf.entries, pf.n_entries, pf.n_hot, pf.start, pf.prim_end, pf.shade_thresh, pf.refill_hits, pf.prim_batch};
+    return FarLayout{pf.entries, pf.n_entries, pf.n_hot, pf.start, pf.prim_end, pf.shade_thresh, pf.refill_hits, pf.prim_batch,
+                     pf.w2};
 }
 
 struct DrainArgs {
@@ -717,6 +721,7 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_drain(DrainArgs a) {
     pf.shade_thresh = k.fl.shade_thresh;
     pf.refill_hits = k.fl.refill_hits;
     pf.prim_batch = k.fl.prim_batch;
+    pf.w2 = k.fl.w2;
     pf.tier = 2;
     render_body<false, USE_LDS, false, false, WAVES, HYB, false, 2, false, false, true>(pf, t0);
 }
@@ -919,7 +924,7 @@ hipError_t launch_tiered(Params pn, Params pf, hipStream_t stream) {
     // The drain (render_drain, the timed kernels): the near grid's workgroups resume their own records in the
     // same LDS (the larger of the two layouts), when that keeps the near pass's occupancy.
     // (Not for a scene in HBM with LDS caches: the combined kernel spilled 24 VGPRs there, and config 4 took +2.3 %.)
-    constexpr bool CAN_DRAIN = !COUNT && !CLK && !HYB;
+    constexpr bool CAN_DRAIN = !COUNT && !CLK && (!HYB || RTX_HYB_DRAIN);
     const void* kd = nullptr;
     if constexpr (CAN_DRAIN) kd = (const void*)render_drain<USE_LDS, WN, MINW, HYB, POOL, ST>;
     const size_t sd = sn > sf ? sn : sf;

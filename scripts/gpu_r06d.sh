@@ -14,7 +14,7 @@ for i in 1 2; do
     python -c "import json,sys; d=json.load(open(sys.argv[1])); s=d['schedule']; print('w2=$w', d['ms_per_step'], d['kernel_ms_avg'], d['framebuffer_sha256_16'], d['node_visits_per_segment'], d['prim_tests_per_segment'], s.get('trav_lane_util'), s.get('lds_cache_hit_frac'))" "$OUT/c4_w${w}_$i.json"
   done
 done
-LIBS="karg nt" TAG=r06d bash scripts/gpu_pmc_libs.sh > "$OUT/pmc.txt" 2>&1
-rc=$?
-cut -c1-300 "$OUT/pmc.txt"
-exit $rc
+[ -n "$PMC" ] && { LIBS="$PMC" TAG=r06d bash scripts/gpu_pmc_libs.sh > "$OUT/pmc.txt" 2>&1 || exit 1; cut -c1-300 "$OUT/pmc.txt"; }
+
+
+exit 0
