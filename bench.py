@@ -54,10 +54,10 @@ def parse():
     ap.add_argument("--no-hash", action="store_true", help="skip the framebuffer hash")
     ap.add_argument("--no-verify", action="store_true",
                     help="one rank: skip the untimed render with the library's stats and error check after the timed "
-                         "steps (PMC profiles count every dispatch of the bench kernel: scripts/gpu_profiles_r05.sh)")
-    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_r05.jsonl"),
+                         "steps (PMC profiles count every dispatch of the bench kernel: scripts/gpu_profiles.sh)")
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_r06.jsonl"),
                     help="PMC HBM-traffic summaries (scripts/pmc_traffic.py): a .json, or a .jsonl of one per workload")
-    ap.add_argument("--valu", default=os.path.join(ROOT, "profiles", "valu_r05.jsonl"),
+    ap.add_argument("--valu", default=os.path.join(ROOT, "profiles", "valu_r06.jsonl"),
                     help="PMC VALU summaries (scripts/pmc_valu.py): a .json, or a .jsonl of one per workload")
     ap.add_argument("--stripe", type=int, default=1, help="rows per stripe of the shards, a power of two (1: single "
                     "rows interleaved, the fastest slowest-rank at N = 4 and 8, profiles/r05_stripe_sweep.jsonl)")

@@ -1,9 +1,9 @@
 #!/bin/bash
-# gpurun (round 5, final tree): the driver's round-end commands as it runs them — the GPU suite, smoke(), the bench.
+# gpurun (the final tree of a round): the driver's round-end commands as it runs them — the GPU suite, smoke(), the bench.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-OUT="$PWD/gpurun_out/r05_driver"; mkdir -p "$OUT"
+OUT="$PWD/gpurun_out/r${ROUND:-06}_driver"; mkdir -p "$OUT"
 timeout -k 10 900 python -m pytest tests/ -x -q -m gpu > "$OUT/pytest.log" 2>&1 || { tail -30 "$OUT/pytest.log"; exit 1; }
 tail -1 "$OUT/pytest.log"
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 || { tail -10 "$OUT/smoke.log"; exit 1; }

@@ -1,12 +1,12 @@
 #!/bin/bash
-# gpurun (round 5): PMC profiles of every bench workload on this library — the configs of SURVEY §8(d),
+# gpurun: PMC profiles of every bench workload on this library — the configs of SURVEY §8(d),
 # the Cornell box, and rank 0's rows of the 2/4/8-GPU headline runs (bench.py --shard 0/N) — then the
 # bench line of each, whose roofline.frac derives from them.  Per workload three rocprofv3 passes of one
 # timed render (bench.py --steps 1 --warmup 0): VALU + wave-state counters, FETCH_SIZE, WRITE_SIZE.
 # Summaries append to gpurun_out/$TAG/{valu,traffic}_r05.jsonl, copied into profiles/ on the box.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-TAG=${TAG:-prof05}; OUT="$PWD/gpurun_out/$TAG"; mkdir -p "$OUT"; export TMPDIR=/tmp
+R=${ROUND:-06}; TAG=${TAG:-prof$R}; OUT="$PWD/gpurun_out/$TAG"; mkdir -p "$OUT"; export TMPDIR=/tmp
 PV="SQ_INSTS_VALU SQ_THREAD_CYCLES_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_BUSY_CYCLES GRBM_GUI_ACTIVE"
 declare -a NAMES ARGS KEYS
 add() { NAMES+=("$1"); KEYS+=("$2"); ARGS+=("$3"); }
@@ -32,11 +32,11 @@ for i in "${!NAMES[@]}"; do
     timeout -s KILL 300 rocprofv3 --kernel-trace --pmc $P -d "$OUT/$n/$pass" -o run --output-format csv -- $cmd \
         > "$OUT/$n/$pass.log" 2>&1 || { rc=$?; echo "$n $pass failed rc=$rc"; break 2; }
   done
-  python scripts/pmc_valu.py "$OUT/$n/valu" "$OUT/valu_r05.jsonl" --workload "$k" --renders 1 > "$OUT/$n/valu.json" && \
-  python scripts/pmc_traffic.py "$OUT/$n" "$OUT/traffic_r05.jsonl" --workload "$k" --renders 1 > "$OUT/$n/traffic.json" || \
+  python scripts/pmc_valu.py "$OUT/$n/valu" "$OUT/valu_r$R.jsonl" --workload "$k" --renders 1 > "$OUT/$n/valu.json" && \
+  python scripts/pmc_traffic.py "$OUT/$n" "$OUT/traffic_r$R.jsonl" --workload "$k" --renders 1 > "$OUT/$n/traffic.json" || \
       { rc=$?; echo "$n summary failed"; break; }
   echo "$n: $(cut -c1-160 "$OUT/$n/valu.json")"
 done
-cp "$OUT/valu_r05.jsonl" "$OUT/traffic_r05.jsonl" profiles/ 2>/dev/null
+cp "$OUT/valu_r$R.jsonl" "$OUT/traffic_r$R.jsonl" profiles/ 2>/dev/null
 echo "profiles rc=$rc"
 exit $rc

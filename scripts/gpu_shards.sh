@@ -1,11 +1,11 @@
 #!/bin/bash
-# gpurun (round 5): EVERY rank's rows of the 2/4/8-GPU headline runs rendered alone on this one GPU
+# gpurun: EVERY rank's rows of the 2/4/8-GPU headline runs rendered alone on this one GPU
 # (bench.py --shard r/N: the timed kernel on rank r's rows y = r mod N, its tile shape), plus the one-process
 # band assembly of 8 simulated bands (rtx_render with RTX_SIM_BANDS=8: device copies + de-interleave).
 # Lines to gpurun_out/$TAG/shards.jsonl (scripts/scaling_prediction.py turns them into the predicted curve).
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-TAG=${TAG:-shards05}; OUT="$PWD/gpurun_out/$TAG"; mkdir -p "$OUT"; export TMPDIR=/tmp
+TAG=${TAG:-shards${ROUND:-06}}; OUT="$PWD/gpurun_out/$TAG"; mkdir -p "$OUT"; export TMPDIR=/tmp
 : > "$OUT/shards.jsonl"
 for N in 2 4 8; do
   for ((r = 0; r < N; r++)); do
