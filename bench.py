@@ -135,6 +135,17 @@ def cpu_model() -> str:
     return platform.processor() or "unknown"
 
 
+def cgroup_cpus():
+    """The CPUs the cgroup's quota allows this process (cgroup v2 cpu.max "quota period"), or None when unlimited:
+    the GPU box shares its host, so sched_getaffinity can list more CPUs than the process may use at once."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        return None if quota == "max" else round(int(quota) / int(period), 2)
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_baseline(scene, cam, seed: int, target_s: float, threads: int, stride: int = 0) -> dict:
     """The oracle (oracle/liboracle.so, a scalar C restatement) on host threads over a
     bounded sample of the same workload: full-width rows at a fixed stride, all spp.
@@ -176,6 +187,7 @@ def cpu_baseline(scene, cam, seed: int, target_s: float, threads: int, stride: i
         "stride": stride,
         "cpu_model": cpu_model(),
         "host_logical_cpus": logical,
+        "cgroup_cpu_quota": cgroup_cpus(),
         "sample": f"{nrows} full-width rows (every {stride}th) of the same {cam.image_width}x{H}x{cam.samples_per_pixel} "
                   f"render, {c['samples']} samples, C oracle on {threads} threads = {who} (Go absent on the host: the "
                   "C restatement stands in for the Go reference)",

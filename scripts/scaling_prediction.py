@@ -1,9 +1,9 @@
 #!/usr/bin/env python3
 """PREDICTED strong scaling of the headline (C2, 1920x1080x500) at N = 1/2/4/8 MI355X from one-GPU
-measurements: every rank's rows rendered alone (scripts/gpu_shards_r05.sh: bench.py --shard r/N, the
+measurements: every rank's rows rendered alone (scripts/gpu_shards.sh: bench.py --shard r/N, the
 timed kernel's HIP-event time per step) plus a gather model.  Nothing here ran on more than one device.
 
-  python scripts/scaling_prediction.py gpurun_out/shards05/shards.jsonl <full-frame ms> > profiles/r05_scaling_predicted.json
+  python scripts/scaling_prediction.py gpurun_out/shards06/shards.jsonl <full-frame ms> > profiles/r06_scaling_predicted.json
 
 A step at N ranks (bench.py --gpus N) = the slowest rank's render + the nccl gather of the padded shards
 to rank 0 + the de-interleave on rank 0.  The gather is modelled, not measured: rank 0 receives N-1 shards of
