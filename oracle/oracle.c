@@ -344,6 +344,7 @@ typedef struct {
     uint32_t material;
     int front;
     const rtx_sphere* sphere; /* the sphere hit (NULL for a quad): the tiered walk's hit check */
+    const rtx_quad* quad;     /* the quad hit (NULL for a sphere): the same check */
 } hit_t;
 
 typedef struct {
@@ -366,6 +367,7 @@ static hit_t new_hit_info(float t, float u, float v, vec3 dir, vec3 point, vec3 
     h.v = v;
     h.material = mat;
     h.sphere = NULL;
+    h.quad = NULL;
     return h;
 }
 
@@ -430,6 +432,7 @@ static int quad_hit(const rtx_quad* q, const ray_t* r, float tmin, float tmax, h
     float beta = v_dot(w, v_cross(v3(q->u[0], q->u[1], q->u[2]), php));    /* :183 */
     if (alpha < 0.0f || 1.0f < alpha || beta < 0.0f || 1.0f < beta) return 0; /* :185, :193 */
     *out = new_hit_info(t, alpha, beta, r->dir, point, n, q->material);    /* :189 */
+    out->quad = q;
     return 1;
 }
 
@@ -537,8 +540,10 @@ static int bvh_hit(const ctx_t* cx, const rtx_bvh_node* n, const ray_t* r, float
     if (!skip || !skip[id]) {
         cx->c->node_visits++;
         if (g_node_tested && !far) __atomic_fetch_add(&g_node_tested[id], 1, __ATOMIC_RELAXED);
-        /* :221; the tiered walk's near tree in its own form */
-        if (!(g_tier_far && !far ? aabb_hit_near(n, r, tmin, tmax) : aabb_hit(n, r, tmin, tmax))) return 0;
+        /* :221; the tiered walk's near tree in its own form (the FMA form in a scene of spheres; with quads the
+         * device's near walk keeps the reference's form, rtx_kernel.hip) */
+        if (!(g_tier_far && !far && cx->s->n_quads == 0 ? aabb_hit_near(n, r, tmin, tmax) : aabb_hit(n, r, tmin, tmax)))
+            return 0;
         if (g_node_passed && !far) __atomic_fetch_add(&g_node_passed[id], 1, __ATOMIC_RELAXED);
     }
     hit_t hl, hr;
@@ -611,13 +616,28 @@ static int world_hit(const ctx_t* cx, const ray_t* r, float tmin, float tmax, hi
              * hittables.go:85-94, inside its reference leaf's box) must pass Aabb.Hit with the
              * bound just past the hit; else the segment is walked again on the far tree. */
             int h = world_hit_tree(cx, r, tmin, tmax, out);
-            if (!h || !out->sphere) return h;
-            const rtx_sphere* sp = out->sphere;
+            if (!h || (!out->sphere && !out->quad)) return h;
             rtx_bvh_node own;
-            for (int k = 0; k < 3; ++k) {
-                float p1 = sp->center[k] + sp->radius * -1.0f, p2 = sp->center[k] + sp->radius;
-                own.bmin[k] = p1 < p2 ? p1 : p2;
-                own.bmax[k] = p1 < p2 ? p2 : p1;
+            if (out->sphere) {
+                const rtx_sphere* sp = out->sphere;
+                for (int k = 0; k < 3; ++k) {
+                    float p1 = sp->center[k] + sp->radius * -1.0f, p2 = sp->center[k] + sp->radius;
+                    own.bmin[k] = p1 < p2 ? p1 : p2;
+                    own.bmax[k] = p1 < p2 ? p2 : p1;
+                }
+            } else {  /* NewQuad's box: NewAabb(Q, Q + u + v).GetPaddedAabb(), hittables.go:162, bvh.go:63-84 */
+                const rtx_quad* q = out->quad;
+                const float eps = 0.0001f;
+                for (int k = 0; k < 3; ++k) {
+                    const float c = (q->q[k] + q->u[k]) + q->v[k];
+                    float lo = min_f32(q->q[k], c), hi = max_f32(q->q[k], c);
+                    if (hi - lo < eps) {
+                        lo = lo - eps;
+                        hi = hi + eps;
+                    }
+                    own.bmin[k] = lo;
+                    own.bmax[k] = hi;
+                }
             }
             if (aabb_hit(&own, r, tmin, nextafterf(out->t, INFINITY))) return h;
         }

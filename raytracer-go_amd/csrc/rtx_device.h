@@ -928,6 +928,59 @@ __device__ __forceinline__ bool own_box_pass(const Trav& t, const Ray& r, const 
     return lo < hi;
 }
 
+// Go's math.Min / math.Max on float32 operands (math.go:38-44, bvh.go:28-34): NaN wins, -0 below +0.
+__device__ __forceinline__ float go_minf(float a, float b) {
+    if (a != a || b != b) return __builtin_nanf("");
+    if (a == 0.0f && b == 0.0f) return __builtin_signbit(a) ? a : b;
+    return a < b ? a : b;
+}
+__device__ __forceinline__ float go_maxf(float a, float b) {
+    if (a != a || b != b) return __builtin_nanf("");
+    if (a == 0.0f && b == 0.0f) return __builtin_signbit(a) ? b : a;
+    return a > b ? a : b;
+}
+
+// The tiered walk's hit check for a quad: whether NewQuad's own box — NewAabb(Q, Q + u + v)
+// .GetPaddedAabb(), hittables.go:162, bvh.go:28-34, 63-84, formed in float32 as Go does from the quad record's
+// (Q, material), (u, 0), (v, 0) — passes Aabb.Hit (bvh.go:52-61, 84-102) with [0.001, the float after t.closest].
+// Every box the guarded walk tests above the quad contains it (NewAabbFromBoxes unions), so it reaches the quad with
+// a bound past the hit, as for a sphere (own_box_pass).
+__device__ __forceinline__ bool quad_own_box_pass(const Trav& t, const Ray& r, const float4 q0, const float4 q1,
+                                                  const float4 q2) {
+    const float eps = 0.0001f;
+    auto axis = [&](float qk, float uk, float vk, float& lo, float& hi) {
+        const float c = (qk + uk) + vk;
+        lo = go_minf(qk, c);
+        hi = go_maxf(qk, c);
+        if (hi - lo < eps) {
+            lo = lo - eps;
+            hi = hi + eps;
+        }
+    };
+    float mnx, mxx, mny, mxy, mnz, mxz;
+    axis(q0.x, q1.x, q2.x, mnx, mxx);
+    axis(q0.y, q1.y, q2.y, mny, mxy);
+    axis(q0.z, q1.z, q2.z, mnz, mxz);
+    // InBoundary per axis as the reference writes it: the NaN rules of `t0 > min` / `t1 < max` keep the bound
+    float lo = 0.001f, hi = __int_as_float(__float_as_int(t.closest) + 1);  // t.closest > 0, finite
+    auto slab = [&](float mn, float mx, float o, float inv, bool neg) {
+        float t0 = (mn - o) * inv, t1 = (mx - o) * inv;
+        if (neg) {
+            const float x = t0;
+            t0 = t1;
+            t1 = x;
+        }
+        if (t0 > lo) lo = t0;
+        if (t1 < hi) hi = t1;
+    };
+    slab(mnx, mxx, r.o.x, t.ix, t.nx);
+    if (!(lo < hi)) return false;
+    slab(mny, mxy, r.o.y, t.iy, t.ny);
+    if (!(lo < hi)) return false;
+    slab(mnz, mxz, r.o.z, t.iz, t.nz);
+    return lo < hi;
+}
+
 // FMA (the near walk): the slab distances as fma(b, 1/d, no) with no = -(o * (1/d))
 // per axis (the caller's, once per phase) — one rounding of b/d - o/d instead of two of (b - o) * (1/d).
 // The near tree's boxes carry the slack for either form (sphere_margin), and its walk is exact by the hit

@@ -457,7 +457,7 @@ __device__ __forceinline__ void render_body(const Params& p, const uint64_t t0 =
         if (TIME) clk = __builtin_amdgcn_s_memtime();
         // primitive batching only for a scene in LDS: a lane that waits re-reads its entry, which
         // from HBM cost config 4 +34 %
-        traverse_phase<COUNT, STEPS, QUADS, USE_LDS, HYB, USE_LDS || (RTX_HYB_BATCH && HYB), TIER == 1 && RTX_NEAR_FMA>(
+        traverse_phase<COUNT, STEPS, QUADS, USE_LDS, HYB, USE_LDS || (RTX_HYB_BATCH && HYB), TIER == 1 && RTX_NEAR_FMA && !QUADS>(
             mode, t, r, E, n_entries, thresh, cnt, wave_iters,
                                                               lane_steps, shade_phases, shade_lanes, idle_lanes,
                                                               parked, deferred, p.prim_batch, HYB && p.w2);
@@ -490,7 +490,14 @@ __device__ __forceinline__ void render_body(const Params& p, const uint64_t t0 =
             // segment is walked again on the guarded tree by the far pass.
             const bool check = mode == M_SHADE && t.hit >= 0;
             bool bad = false;
-            if (check) bad = !own_box_pass(t, r, E.a[t.hit]);
+            if (check) {
+                if (QUADS && __float_as_int(E.b[t.hit].w) == RTX_E_QUAD) {  // a quad's own box
+                    const uint32_t qi = 4u * (uint32_t)__float_as_int(E.b[t.hit].x);
+                    bad = !quad_own_box_pass(t, r, E.q[qi], E.q[qi + 1], E.q[qi + 2]);
+                } else {
+                    bad = !own_box_pass(t, r, E.a[t.hit]);
+                }
+            }
             if (COUNT && bad) --cnt.segments;  // the far pass walks the segment again and counts it
             defer(bad);
         }
@@ -649,7 +656,7 @@ __device__ __forceinline__ void render_body(const Params& p, const uint64_t t0 =
         if (TIME) split_clk(split[2], clk);
         if (ready) {  // begin a segment: world.Hit (ray.go:36)
             if (COUNT) ++cnt.segments;
-            trav_begin<TIER == 1 && RTX_NEAR_FMA>(t, r, p.start);
+            trav_begin<TIER == 1 && RTX_NEAR_FMA && !QUADS>(t, r, p.start);
             mode = n_entries > 0 ? M_TRAV : M_SHADE;
         }
         if (TIME) split_clk(split[3], clk);
@@ -701,10 +708,10 @@ struct DrainArgs {
     FarLayout fl;
 };
 
-template <bool USE_LDS, int WAVES, int MINW, bool HYB, bool POOL, bool ST>
+template <bool USE_LDS, int WAVES, int MINW, bool HYB, bool POOL, bool ST, bool QUADS = false>
 __global__ __launch_bounds__(64 * WAVES, MINW) void render_drain(DrainArgs a) {
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime() | 1ull;  // the watchdog's start for both phases (nonzero)
-    render_body<false, USE_LDS, false, false, WAVES, HYB, false, 1, POOL, ST, true>(a.pn, t0);
+    render_body<false, USE_LDS, QUADS, false, WAVES, HYB, false, 1, POOL, ST, true>(a.pn, t0);
     __syncthreads();  // every wave's near work and records done: the far phase overwrites the scene copy
     // The far phase reads its settings from the kernel arguments afresh, through an opaque copy of their address:
     // values it shares with the near phase are then not kept live through the near phase (which spilled 4 more VGPRs).
@@ -723,7 +730,7 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void render_drain(DrainArgs a) {
     pf.prim_batch = k.fl.prim_batch;
     pf.w2 = k.fl.w2;
     pf.tier = 2;
-    render_body<false, USE_LDS, false, false, WAVES, HYB, false, 2, false, false, true>(pf, t0);
+    render_body<false, USE_LDS, QUADS, false, WAVES, HYB, false, 2, false, false, true>(pf, t0);
 }
 
 // The redo list overflowed (more samples than p.redo_cap): its ids join the ones the near pass set in
@@ -832,11 +839,13 @@ constexpr uint32_t LDS_MAX_BYTES = 64 * 1024;
 // image's last units would run on a near-empty GPU).  Measured at 100 spp: 1920x1080 8 -1.6 % vs
 // 16; 400x225 2 -42 % vs 16; Cornell 600x600 8 -3 % vs 16.  16 when that still leaves >= 64
 // units per wave (the drain stays short): 1920x1080x500 -0.9 % vs 8 (142.5 vs 143.8 ms).
-// TIERED (the tiered walk, whose timed near pass drains: DESIGN.md §21): 4 instead of 2 below 8 units of 8 samples per resident wave
-// (C1 400x225x100: 1.68 ms against 1.77 at 2 and 1.77 at 8; profiles/r05_unit_sweep.jsonl).
+// 4 instead of 2 below 8 units of 8 samples per resident wave: the tiered walk (C1 400x225x100: 1.68 ms against 1.77 at
+// 2 and 1.77 at 8; profiles/r05_unit_sweep.jsonl), and since round 6 every render (quadDemo 400x225x100: 0.60 ms
+// against 0.99 at 2, perlinDemo 3.31 against 3.33; profiles/r06_demo_knobs.jsonl).
 inline uint32_t unit_samples(uint64_t tiles, uint32_t kn, int waves, int per_cu, int cus, bool tiered = false) {
     const uint64_t per_wave = tiles * kn / (8ull * waves * (uint64_t)per_cu * cus);
-    if (tiered && per_wave >= 2 && per_wave < 8) return 4u;
+    (void)tiered;
+    if (per_wave >= 2 && per_wave < 8) return 4u;
     return per_wave >= 128 ? RTX_SUB_MAX : (per_wave >= 8 ? 8u : (per_wave >= 4 ? 4u : (per_wave >= 2 ? 2u : 1u)));
 }
 
@@ -908,11 +917,11 @@ inline size_t items_shmem(const Params& p, bool use_lds, bool hyb) {
 // workgroups of WN waves (12: two per CU, each with its scene copy and 12 pools); the far and redo
 // passes keep WAVES.
 template <bool COUNT, int WAVES, int MINW, bool CLK = false, bool USE_LDS = true, bool HYB = false, bool POOL = false,
-          bool ST = false, int WN = POOL ? 12 : WAVES>
+          bool ST = false, bool QUADS = false, int WN = POOL ? 12 : WAVES>
 hipError_t launch_tiered(Params pn, Params pf, hipStream_t stream) {
-    const auto kn = render_items<COUNT, USE_LDS, false, false, WN, MINW, HYB, CLK, 1, POOL, ST>;
-    const auto kf = render_items<COUNT, USE_LDS, false, false, WAVES, MINW, HYB, CLK, 2>;  // (rows from the records)
-    const auto kr = render_items<COUNT, USE_LDS, false, false, WAVES, MINW, HYB, false, 3, false, ST>;
+    const auto kn = render_items<COUNT, USE_LDS, QUADS, false, WN, MINW, HYB, CLK, 1, POOL, ST>;
+    const auto kf = render_items<COUNT, USE_LDS, QUADS, false, WAVES, MINW, HYB, CLK, 2>;  // (rows from the records)
+    const auto kr = render_items<COUNT, USE_LDS, QUADS, false, WAVES, MINW, HYB, false, 3, false, ST>;
     const size_t sn = POOL ? (size_t)pool_f4_offset(pn) * 16 + WN * POOL_BYTES_PER_WAVE : items_shmem(pn, USE_LDS, HYB),
                  sf = items_shmem(pf, USE_LDS, HYB);
     constexpr int block = 64 * WAVES, block_n = 64 * WN;
@@ -926,7 +935,7 @@ hipError_t launch_tiered(Params pn, Params pf, hipStream_t stream) {
     // (Not for a scene in HBM with LDS caches: the combined kernel spilled 24 VGPRs there, and config 4 took +2.3 %.)
     constexpr bool CAN_DRAIN = !COUNT && !CLK && (!HYB || RTX_HYB_DRAIN);
     const void* kd = nullptr;
-    if constexpr (CAN_DRAIN) kd = (const void*)render_drain<USE_LDS, WN, MINW, HYB, POOL, ST>;
+    if constexpr (CAN_DRAIN) kd = (const void*)render_drain<USE_LDS, WN, MINW, HYB, POOL, ST, QUADS>;
     const size_t sd = sn > sf ? sn : sf;
     int per_d = 0;
     bool drain = CAN_DRAIN && pn.drain && pn.drain_count;
@@ -962,7 +971,7 @@ hipError_t launch_tiered(Params pn, Params pf, hipStream_t stream) {
         if (drain_now) {
             pn.drain_region = pf.drain_region = pn.defer_cap / (uint32_t)bn;
             if constexpr (CAN_DRAIN)
-                hipLaunchKernelGGL((render_drain<USE_LDS, WN, MINW, HYB, POOL, ST>), dim3((uint32_t)bn), dim3(block_n), sd,
+                hipLaunchKernelGGL((render_drain<USE_LDS, WN, MINW, HYB, POOL, ST, QUADS>), dim3((uint32_t)bn), dim3(block_n), sd,
                                    stream, DrainArgs{pn, far_layout(pf)});
         } else {
             hipLaunchKernelGGL(kn, dim3((uint32_t)bn), dim3(block_n), sn, stream, pn);
@@ -1026,8 +1035,26 @@ hipError_t launch_render_t(const Params& p, uint32_t flags, hipStream_t stream, 
     if (far) {  // the caller checked: spheres only, both layouts placed alike (tier_placement), no noise
         const uint32_t place = tier_placement(p, *far, flags);
         if ((p.w2 || far->w2) && place != RTX_SCENE_LDS_CACHE) return hipErrorInvalidValue;  // (records: cache kernels)
-        if (p.tier != 1 || far->tier != 2 || !p.defer || !far->defer || !p.redo_bits || p.n_quads || p.has_noise)
+        if (p.tier != 1 || far->tier != 2 || !p.defer || !far->defer || !p.redo_bits || p.has_noise)
             return hipErrorInvalidValue;
+        if (p.n_quads) {  // quads: single-row shards, the timed and counting kernels (rtx_capi's enqueue_on)
+            if (ST || (!count && (flags & RTX_FLAG_TIMING))) return hipErrorInvalidValue;
+            if constexpr (!ST) {
+                constexpr int V = RTX_V3_WAVES, MV = RTX_V3_MINW, H = RTX_HYB_WAVES, MH = RTX_HYB_MINW;
+                if (place == RTX_SCENE_IN_LDS) {
+                    const bool pool = pool_fits(p);
+                    if (count) return pool ? launch_tiered<true, V, 0, false, true, false, true, false, true>(p, *far, stream)
+                                           : launch_tiered<true, V, 0, false, true, false, false, false, true>(p, *far, stream);
+                    return pool ? launch_tiered<false, V, MV, false, true, false, true, false, true>(p, *far, stream)
+                                : launch_tiered<false, V, MV, false, true, false, false, false, true>(p, *far, stream);
+                }
+                if (place == RTX_SCENE_LDS_CACHE)
+                    return count ? launch_tiered<true, H, 0, false, false, true, false, false, true>(p, *far, stream)
+                                 : launch_tiered<false, H, MH, false, false, true, false, false, true>(p, *far, stream);
+                return count ? launch_tiered<true, V, 0, false, false, false, false, false, true>(p, *far, stream)
+                             : launch_tiered<false, V, MV, false, false, false, false, false, true>(p, *far, stream);
+            }
+        }
         const bool clk = !count && (flags & RTX_FLAG_TIMING);  // diagnostics: the wave-cycle split of the passes
         constexpr int V = RTX_V3_WAVES, MV = RTX_V3_MINW, H = RTX_HYB_WAVES, MH = RTX_HYB_MINW;
         if (place == RTX_SCENE_IN_LDS) {

@@ -55,12 +55,27 @@ struct Topology {
 // anything but spheres, a sphere outside a leaf node of one or two spheres (guarded), or fewer
 // than two units.
 // near_box (unguarded only): grow every sphere's box by sphere_margin for origins in that box.
-bool build_topology(const std::vector<rtx_entry>& ref, bool guarded, Topology& out, const float* near_box = nullptr);
+// quadtab (the scene's quad table, rtx_layout.h, 16 floats per quad): a near tree holds the quads too, each behind
+// its corners' box grown by quad_margin.
+bool build_topology(const std::vector<rtx_entry>& ref, bool guarded, Topology& out, const float* near_box = nullptr,
+                    const std::vector<float>* quadtab = nullptr);
 
 // The near region of a tiered walk: the box of the spheres that are not huge (precise_enough's
 // core) grown by `grow` times its largest extent on every side, min xyz then max xyz.  False when
 // the scene has no finite core.
-bool near_region(const std::vector<rtx_entry>& ref, float box[6], double grow = 1.0);
+// quadtab: the quads' own boxes join the core (a scene of quads only: they are the core).
+bool near_region(const std::vector<rtx_entry>& ref, float box[6], double grow = 1.0,
+                 const std::vector<float>* quadtab = nullptr);
+
+// NewQuad's box, NewAabb(Q, Q + u + v).GetPaddedAabb() (hittables.go:162, bvh.go:63-84), in float32 as Go forms it,
+// of the quad record q (16 floats of the quad table).
+void quad_own_box(const float* q, float mn[3], float mx[3]);
+
+// How far from its parallelogram the float32 quad test (hittables.go:167-190) can put a hit for a ray origin whose
+// coordinates are within omax, with room for the slab test's rounding: K u (|u| + |v| + 2B + 3 omax)(2 + 2 / sin)
+// + 4u (B + omax), B bounding the quad's coordinates, sin the sine of the angle of u and v, K = 64 (RTX_MARGIN_KQ
+// widens it).  DESIGN.md §26 derives the terms; tests/test_tier.py meets at most a small fraction of it.
+double quad_margin(const float* q, double omax);
 
 // How far outside a sphere (centre c, radius r) the float32 sphere test (hittables.go:96-116) can
 // put a hit for a ray origin at distance <= dmax from c (its coordinates <= omax in magnitude), with
@@ -78,7 +93,8 @@ bool precise_enough(const std::vector<rtx_entry>& ref);
 // hittables.go:85-94) of every sphere below it, and the scene holds spheres only: the tiered walk's
 // hit check accepts a near-tree hit by testing the sphere's own box in place of every
 // box the far walk would test above it.  NewBVH's nodes always qualify (NewAabbFromBoxes, bvh.go:44-50).
-bool own_boxes_nested(const std::vector<rtx_entry>& ref);
+// quadtab: the scene's quads too, each with its own box (quad_own_box).
+bool own_boxes_nested(const std::vector<rtx_entry>& ref, const std::vector<float>* quadtab = nullptr);
 
 // The node table of `t` as walked for camera octant `oct` (bit k: the viewing direction is
 // negative along axis k): at every SAH node the child on the near side of its split along the

@@ -1,4 +1,5 @@
-// rtx_topology.hip — the walk's own tree over a sphere scene (host code; see rtx_topology.h).
+// rtx_topology.hip — the walk's own tree over a sphere scene, and the near tree of a tiered walk (host code; see
+// rtx_topology.h).
 #include "rtx_topology.h"
 
 #include <algorithm>
@@ -180,14 +181,72 @@ void build_sah(const std::vector<Box>& boxes, const std::vector<int32_t>& item_r
 
 }  // namespace
 
+void quad_own_box(const float* q, float mn[3], float mx[3]) {
+    // NewAabb(Q, Q + u + v).GetPaddedAabb() (hittables.go:162, bvh.go:28-34, 63-84): Add(Add(Q, u), v) in float32,
+    // Go's Min / Max, then every axis thinner than 0.0001 widened by 0.0001 on both sides (float32 operations)
+    const float eps = 0.0001f;
+    for (int k = 0; k < 3; ++k) {
+        volatile float c = q[k] + q[4 + k];  // (no contraction: the reference's two float32 additions)
+        c = c + q[8 + k];
+        const float p1 = q[k], p2 = c;
+        float lo = go_min(p1, p2), hi = go_max(p1, p2);
+        volatile float ext = hi - lo;
+        if (ext < eps) {
+            lo = lo - eps;
+            hi = hi + eps;
+        }
+        mn[k] = lo;
+        mx[k] = hi;
+    }
+}
+
+// RTX_MARGIN_KQ (read once; default 64, at least 64): the constant K of quad_margin's bound.
+static double margin_kq() {
+    static const double k = [] {
+        const char* e = std::getenv("RTX_MARGIN_KQ");
+        const double v = e ? std::strtod(e, nullptr) : 64.0;
+        return v >= 64.0 && std::isfinite(v) ? v : 64.0;
+    }();
+    return k;
+}
+
+double quad_margin(const float* q, double omax) {
+    const double u[3] = {q[4], q[5], q[6]}, v[3] = {q[8], q[9], q[10]};
+    const double n[3] = {u[1] * v[2] - u[2] * v[1], u[2] * v[0] - u[0] * v[2], u[0] * v[1] - u[1] * v[0]};
+    const double U = std::sqrt(u[0] * u[0] + u[1] * u[1] + u[2] * u[2]), V = std::sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
+    const double S = std::sqrt(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]);
+    if (!(S > 0.0) || !std::isfinite(S) || !(U > 0.0) || !(V > 0.0)) return INFINITY;  // degenerate: no near box
+    double B = 0.0;  // a bound on the coordinates of points of the quad
+    for (int k = 0; k < 3; ++k) B = std::max(B, std::fabs((double)q[k]) + std::fabs(u[k]) + std::fabs(v[k]));
+    const double sin_t = S / (U * V);
+    const double m = std::ldexp(margin_kq() * (U + V + 2.0 * B + 3.0 * omax) * (2.0 + 2.0 / sin_t), -24);
+    return m + std::ldexp(B + omax + m, -21);  // + 4u (|b| + |o|): the slab test's rounding, either form
+}
+
 namespace {
 // The box of the spheres that are not huge (a sphere is huge when its radius exceeds the extent
 // of all smaller ones: main.go's ground, r = 1000), and the smallest radius.
-bool core_box(const std::vector<rtx_entry>& ref, Box& core, double& rmin) {
+bool core_box(const std::vector<rtx_entry>& ref, Box& core, double& rmin, const std::vector<float>* quadtab = nullptr) {
     std::vector<std::pair<float, uint32_t>> rad;  // (radius, entry), spheres only
     for (uint32_t i = 0; i < ref.size(); ++i)
         if (tag_of(ref[i]) >= 0) rad.push_back({std::fabs(ref[i].a[3]), i});
-    if (rad.empty()) return false;
+    // quads (the near region of a scene with quads): their own boxes join the core, which they hold when the
+    // scene has no sphere
+    bool have_q = false;
+    Box qb;
+    for (uint32_t i = 0; quadtab && i < ref.size(); ++i)
+        if (tag_of(ref[i]) == RTX_E_QUAD) {
+            Box b;
+            quad_own_box(&(*quadtab)[16 * (size_t)word(&ref[i].b[0])], b.mn, b.mx);
+            qb = have_q ? unite(qb, b) : b;
+            have_q = true;
+        }
+    if (rad.empty()) {
+        if (!have_q) return false;
+        core = qb;
+        rmin = 0.0;
+        return true;
+    }
     std::sort(rad.begin(), rad.end());
     std::vector<Box> pre(rad.size());  // union of the boxes of the k + 1 smallest spheres
     for (size_t k = 0; k < rad.size(); ++k) {
@@ -206,7 +265,7 @@ bool core_box(const std::vector<rtx_entry>& ref, Box& core, double& rmin) {
         if (!(rad[keep - 1].first > ext)) break;
         --keep;
     }
-    core = pre[keep - 1];
+    core = have_q ? unite(pre[keep - 1], qb) : pre[keep - 1];
     rmin = rad[0].first;
     return true;
 }
@@ -229,7 +288,7 @@ bool precise_enough(const std::vector<rtx_entry>& ref) {
     return rmin > 0.0 && std::ldexp(d2, -24) / (rmin * rmin) < std::ldexp(1.0, -7);
 }
 
-bool own_boxes_nested(const std::vector<rtx_entry>& ref) {
+bool own_boxes_nested(const std::vector<rtx_entry>& ref, const std::vector<float>* quadtab) {
     std::vector<uint32_t> open;  // the nodes whose subtree holds entry i (host layout: a[3] = escape index)
     bool any = false;
     for (uint32_t i = 0; i < ref.size(); ++i) {
@@ -239,12 +298,14 @@ bool own_boxes_nested(const std::vector<rtx_entry>& ref) {
             open.push_back(i);
             continue;
         }
-        if (tag < 0) return false;  // a quad
+        if (tag < 0 && !(tag == RTX_E_QUAD && quadtab)) return false;  // a quad (without its table)
         any = true;
         const rtx_entry& e = ref[i];
+        float qmn[3], qmx[3];
+        if (tag < 0) quad_own_box(&(*quadtab)[16 * (size_t)word(&e.b[0])], qmn, qmx);
         for (int k = 0; k < 3; ++k) {
             const float p1 = e.a[k] + (e.a[3] * -1.0f), p2 = e.a[k] + e.a[3];
-            const float mn = go_min(p1, p2), mx = go_max(p1, p2);
+            const float mn = tag < 0 ? qmn[k] : go_min(p1, p2), mx = tag < 0 ? qmx[k] : go_max(p1, p2);
             if (!(mn == mn) || !(mx == mx)) return false;
             for (uint32_t n : open)
                 if (!(ref[n].a[k] <= mn && ref[n].b[k] >= mx)) return false;
@@ -253,10 +314,10 @@ bool own_boxes_nested(const std::vector<rtx_entry>& ref) {
     return any;
 }
 
-bool near_region(const std::vector<rtx_entry>& ref, float box[6], double grow) {
+bool near_region(const std::vector<rtx_entry>& ref, float box[6], double grow, const std::vector<float>* quadtab) {
     Box b;
     double rmin = 0.0;
-    if (!core_box(ref, b, rmin)) return false;
+    if (!core_box(ref, b, rmin, quadtab)) return false;
     double ext = 0.0;
     for (int q = 0; q < 3; ++q) ext = std::max(ext, (double)b.mx[q] - (double)b.mn[q]);
     if (!std::isfinite(ext)) return false;
@@ -290,7 +351,8 @@ double sphere_margin(double r, double dmax, double omax) {
     return rho - r + std::ldexp(dmax + rho, -20) + std::ldexp(omax, -23);                       // + 16u (D + rho) + 2u omax
 }
 
-bool build_topology(const std::vector<rtx_entry>& ref, bool guarded, Topology& out, const float* near_box) {
+bool build_topology(const std::vector<rtx_entry>& ref, bool guarded, Topology& out, const float* near_box,
+                    const std::vector<float>* quadtab) {
     if (guarded && near_box) return false;
     // the units, in the reference's walk order: [first entry, end) of each
     std::vector<std::pair<uint32_t, uint32_t>> units;
@@ -308,6 +370,9 @@ bool build_topology(const std::vector<rtx_entry>& ref, bool guarded, Topology& o
                 ++i;
             }
         } else if (tag >= 0 && !guarded) {  // a sphere
+            units.push_back({i, i + 1});
+            ++i;
+        } else if (tag == RTX_E_QUAD && near_box && quadtab) {  // a quad of a near tree
             units.push_back({i, i + 1});
             ++i;
         } else {
@@ -336,6 +401,20 @@ bool build_topology(const std::vector<rtx_entry>& ref, bool guarded, Topology& o
                 boxes[u].mx[k] = h.b[k];
             }
             item_ref[u] = (int32_t)(t.n_internal + u);
+        } else if (near_box && tag_of(h) == RTX_E_QUAD) {  // the quad's corners' box grown by quad_margin
+            const int32_t qi = word(&h.b[0]);
+            const float* q = &(*quadtab)[16 * (size_t)qi];
+            double omax = 0.0;
+            for (int k = 0; k < 6; ++k) omax = std::max(omax, std::fabs((double)near_box[k]));
+            const double m = quad_margin(q, omax);
+            for (int k = 0; k < 3; ++k) {
+                const double c0 = q[k], c1 = c0 + q[4 + k], c2 = c0 + q[8 + k], c3 = c1 + q[8 + k];
+                const double lo = std::min({c0, c1, c2, c3}) - m, hi = std::max({c0, c1, c2, c3}) + m;
+                boxes[u].mn[k] = std::nextafter((float)lo, -INFINITY);  // rounded outward
+                boxes[u].mx[k] = std::nextafter((float)hi, INFINITY);
+                if (!(std::fabs(boxes[u].mn[k]) <= 0x1p32f) || !(std::fabs(boxes[u].mx[k]) <= 0x1p32f)) return false;
+            }
+            item_ref[u] = RTX_REF_PRIM(RTX_PRIM_QUAD, qi);
         } else if (near_box) {  // the sphere's box grown by its margin for origins in the near region
             const double r = std::fabs((double)h.a[3]);
             double d2 = 0.0, omax = 0.0;  // farthest corner of the region from the centre; its largest coordinate

@@ -72,12 +72,14 @@ def test_near_region(built, scene):
     assert (np.array(list(cam.center)) > lo).all() and (np.array(list(cam.center)) < hi).all()
 
 
-@pytest.mark.parametrize("scene,flags", [("random_spheres", rtx.RTX_SCENE_NO_TIER),
-                                         ("random_spheres", rtx.RTX_SCENE_REFERENCE_BVH),
-                                         ("cornell_box", 0), ("perlin_demo", 0)])
-def test_no_near_tree(built, scene, flags):
-    """No tiers with RTX_SCENE_NO_TIER or the caller's tree (RTX_SCENE_REFERENCE_BVH), or for quads; a
-    Perlin scene has a near tree but does not qualify."""
+@pytest.mark.parametrize("scene,flags,env", [("random_spheres", rtx.RTX_SCENE_NO_TIER, None),
+                                             ("random_spheres", rtx.RTX_SCENE_REFERENCE_BVH, None),
+                                             ("cornell_box", 0, "RTX_TIER_QUADS"), ("perlin_demo", 0, None)])
+def test_no_near_tree(built, monkeypatch, scene, flags, env):
+    """No tiers with RTX_SCENE_NO_TIER or the caller's tree (RTX_SCENE_REFERENCE_BVH), or for quads unless
+    RTX_TIER_QUADS=1; a Perlin scene has a near tree but does not qualify."""
+    if env:
+        monkeypatch.setenv(env, "0")
     s = rtx.HostScene(scene, 1)
     cam = s.camera(width=64, spp=1)
     box, active = rtx.walk_near_region(s.desc, cam, flags)
@@ -312,11 +314,13 @@ def test_margin_bound_adversarial(built, scene, n_spheres, rscale, dscale):
     print(f"{scene}: {n_hits} reported hits, largest K = {k_max:.2f} (the margin assumes 24)")
 
 
-@pytest.mark.parametrize("scene,width,spp", [("random_spheres", 192, 4), ("earth_dielectric", 160, 3)])
-def test_tiered_oracle_equals_reference(built, scene, width, spp):
+@pytest.mark.parametrize("scene,width,spp", [("random_spheres", 192, 4), ("earth_dielectric", 160, 3),
+                                             ("cornell_box", 96, 4), ("quad_demo", 160, 4)])
+def test_tiered_oracle_equals_reference(built, monkeypatch, scene, width, spp):
     """The oracle's tiered walk (near tree for paths in the near region, the guarded tree from a path's
     first segment outside it on) against the reference's tree: the same image bit for bit and the same
-    segments, hits, texel fetches and draws; fewer box and sphere tests."""
+    segments, hits, texel fetches and draws; fewer box and sphere tests.  (Quads: RTX_TIER_QUADS=1)"""
+    monkeypatch.setenv("RTX_TIER_QUADS", "1")
     s = rtx.HostScene(scene, 1)
     cam = s.camera(width=width, spp=spp)
     box, active = rtx.walk_near_region(s.desc, cam)
@@ -329,7 +333,8 @@ def test_tiered_oracle_equals_reference(built, scene, width, spp):
     assert np.array_equal(a, b)
     for k in ("samples", "segments", "hits", "texel_fetches", "rng_draws"):
         assert ca[k] == cb[k], k
-    assert cb["prim_tests"] < 0.7 * ca["prim_tests"] and cb["node_visits"] < 0.7 * ca["node_visits"]
+    if s.desc.contents.n_quads == 0:  # (a near tree over quads saves box tests only: DESIGN.md §26)
+        assert cb["prim_tests"] < 0.7 * ca["prim_tests"] and cb["node_visits"] < 0.7 * ca["node_visits"]
     # every segment in the near tree alone (no far tier): the same image here too
     c, _ = ob.render(near, cam, 2024, reg, ob.ORDER_ITERATIVE, rank=ob.sphere_ranks(s.desc))
     assert np.array_equal(a, c)
@@ -362,3 +367,143 @@ def test_tiered_oracle_known_cases(built, scene, width, spp, px, py, k):
         L.oracle_sphere_rank(None)
     assert np.array_equal(np.asarray(got), np.asarray(want)), (got, want)
     assert gc["segments"] == wc["segments"] and gc["rng_draws"] == wc["rng_draws"]
+
+
+# ---- quads in the near tree ----------------------------------------------------------------------
+def quads_of(desc):
+    d = desc.contents
+    g = lambda f: np.array([list(getattr(d.quads[i], f)) for i in range(d.n_quads)], F)  # noqa: E731
+    return g("q"), g("u"), g("v"), g("w"), g("normal"), np.array([d.quads[i].d for i in range(d.n_quads)], F)
+
+
+def quad_t(o, d, Q, U, V, W, N, D, tmin=F(0.001)):
+    """Quad.Hit (hittables.go:167-194) in float32, left-associative, no FMA: (t, point) with t NaN = no hit."""
+    denom = (d[:, 0] * N[:, 0] + d[:, 1] * N[:, 1]) + d[:, 2] * N[:, 2]
+    ok = ~(np.abs(denom.astype(np.float64)) < 1e-8)
+    num = D - ((N[:, 0] * o[:, 0] + N[:, 1] * o[:, 1]) + N[:, 2] * o[:, 2])
+    with np.errstate(divide="ignore", invalid="ignore", over="ignore"):
+        t = (num / np.where(ok, denom, F(1))).astype(F)
+    ok &= tmin < t
+    P = (d * t[:, None] + o).astype(F)  # Add(Scale(dir, t), origin)
+    php = (P - Q).astype(F)
+
+    def cross(l, r):  # vec3.go:129-135
+        return np.stack([l[:, 1] * r[:, 2] - l[:, 2] * r[:, 1], l[:, 2] * r[:, 0] - l[:, 0] * r[:, 2],
+                         l[:, 0] * r[:, 1] - l[:, 1] * r[:, 0]], 1).astype(F)
+
+    def dot(l, r):
+        return ((l[:, 0] * r[:, 0] + l[:, 1] * r[:, 1]) + l[:, 2] * r[:, 2]).astype(F)
+
+    alpha, beta = dot(W, cross(php, V)), dot(W, cross(U, php))
+    ok &= ~((alpha < 0) | (1 < alpha) | (beta < 0) | (1 < beta))
+    return np.where(ok, t, F(np.nan)).astype(F)
+
+
+def quad_ancestors(arr, root):
+    out, stack = {}, [(root, [])]
+    while stack:
+        i, anc = stack.pop()
+        chain = anc + [i]
+        for ch in (arr[i].left, arr[i].right):
+            if ch >= 0:
+                stack.append((ch, chain))
+            elif ((~ch) & 0xFFFFFFFF) >> 28 == rtx.RTX_PRIM_QUAD:
+                out[(~ch) & 0x0FFFFFFF] = chain
+    return out
+
+
+@pytest.mark.parametrize("scene", ["cornell_box", "quad_demo"])
+def test_quad_margin_adversarial(built, monkeypatch, scene):
+    """The bound behind quad_margin (rtx_topology.h), adversarially: from the near region's corners, face centres
+    and random points, rays at every quad's edges and corners (in-plane offsets of 1e-7 .. 1e-1 of the edge,
+    inside and out) and at grazing angles, direction lengths 1e-2 .. 1e2.  Every hit the float32 quad test reports
+    lies within the quad's margin of its parallelogram — so inside its near-tree box — and every box above the quad
+    passes the float32 slab test with the bound just past the hit (the near walk reaches it)."""
+    monkeypatch.setenv("RTX_TIER_QUADS", "1")
+    s = rtx.HostScene(scene, 1)
+    cam = s.camera(width=96, spp=2)
+    box, active = rtx.walk_near_region(s.desc, cam)
+    assert box is not None and active
+    arr, root = near_tree(s.desc, cam)
+    anc = quad_ancestors(arr, root)
+    Q, U, V, W, N, D = quads_of(s.desc)
+    assert len(anc) == len(Q) > 0
+    bmin = np.array([list(arr[i].bmin) for i in range(len(arr))], F)
+    bmax = np.array([list(arr[i].bmax) for i in range(len(arr))], F)
+    rng = np.random.default_rng(5)
+    lo, hi = np.array(box[:3], np.float64), np.array(box[3:], np.float64)
+    corners = np.array([[box[3 * ((m >> k) & 1) + k] for k in range(3)] for m in range(8)], np.float64)
+    faces = np.array([np.where(np.arange(3) == k, v, 0.5 * (lo + hi)) for k in range(3) for v in (lo[k], hi[k])])
+    origins = np.concatenate([corners, faces, rng.uniform(lo, hi, (20, 3))])
+    omax = float(np.abs(corners).max())
+    n_hits, worst = 0, 0.0
+    for qi in range(len(Q)):
+        q, u, v = Q[qi].astype(np.float64), U[qi].astype(np.float64), V[qi].astype(np.float64)
+        # targets: points at the edges and corners, pushed in or out by a relative 1e-7 .. 1e-1 of the edges
+        a = rng.choice([0.0, 1.0], 4000) + rng.choice([-1, 1], 4000) * 10.0 ** rng.uniform(-7, -1, 4000)
+        b = np.where(rng.random(4000) < 0.5, rng.uniform(0, 1, 4000),
+                     rng.choice([0.0, 1.0], 4000) + rng.choice([-1, 1], 4000) * 10.0 ** rng.uniform(-7, -1, 4000))
+        swap = rng.random(4000) < 0.5
+        a, b = np.where(swap, b, a), np.where(swap, a, b)
+        tgt = q + a[:, None] * u + b[:, None] * v
+        o = origins[rng.integers(0, len(origins), 4000)]
+        # grazing rays (a quarter): the target seen from an origin moved along the plane
+        n = np.cross(u, v)
+        n /= np.linalg.norm(n)
+        gr = rng.random(4000) < 0.25
+        o = np.where(gr[:, None], tgt + (o - tgt) - ((o - tgt) @ n)[:, None] * n * (1 - 10.0 ** rng.uniform(-6, -2, 4000))[:, None], o)
+        o = np.clip(o, lo, hi).astype(F)
+        d = ((tgt - o.astype(np.float64)) * np.exp(rng.uniform(np.log(1e-2), np.log(1e2), 4000))[:, None]).astype(F)
+        k = np.full(4000, qi)
+        t = quad_t(o, d, Q[k], U[k], V[k], W[k], N[k], D[k])
+        hit = ~np.isnan(t)
+        n_hits += int(hit.sum())
+        if not hit.any():
+            continue
+        X = o[hit].astype(np.float64) + t[hit].astype(np.float64)[:, None] * d[hit].astype(np.float64)
+        # distance of the exact point from the parallelogram: solve X = q + a u + b v + c n
+        M = np.stack([u, v, n], 1)
+        abc = np.linalg.solve(M, (X - q).T).T
+        ea = np.maximum(0, np.maximum(-abc[:, 0], abc[:, 0] - 1)) * np.linalg.norm(u)
+        eb = np.maximum(0, np.maximum(-abc[:, 1], abc[:, 1] - 1)) * np.linalg.norm(v)
+        dist = ea + eb + np.abs(abc[:, 2])
+        m = margin_q(Q[qi], U[qi], V[qi], omax)
+        worst = max(worst, float(dist.max() / m))
+        assert (dist <= m).all(), (qi, float(dist.max()), m)
+        bound = np.nextafter(t[hit], F(np.inf))
+        for node in anc[qi]:
+            cnt = int(hit.sum())
+            ok = slab_pass(o[hit], d[hit], np.tile(bmin[node], (cnt, 1)), np.tile(bmax[node], (cnt, 1)),
+                           np.full(cnt, F(0.001)), bound)
+            assert ok.all(), (qi, node, int((~ok).sum()))
+    assert n_hits > 5_000
+    assert worst < 0.25, worst  # the hits stay well inside the margin
+    print(f"{scene}: {n_hits} reported hits, the farthest at {worst:.4f} of the margin")
+
+
+def margin_q(q, u, v, omax):
+    """rtx_topology.h quad_margin, restated (K = 64)."""
+    q, u, v = q.astype(np.float64), u.astype(np.float64), v.astype(np.float64)
+    U, V, S = np.linalg.norm(u), np.linalg.norm(v), np.linalg.norm(np.cross(u, v))
+    B = float((np.abs(q) + np.abs(u) + np.abs(v)).max())
+    m = math.ldexp(64.0 * (U + V + 2 * B + 3 * omax) * (2 + 2 * U * V / S), -24)
+    return m + math.ldexp(B + omax + m, -21)
+
+
+def test_quad_ties_gate(built, monkeypatch):
+    """Coplanar, overlapping quads enter a near tree only when a tie between them cannot change a path (the same
+    material, not an image texture, and the same normal): the Cornell box's box bottoms on its floor qualify
+    (RTX_TIER_QUADS=1; off by default)."""
+    monkeypatch.setenv("RTX_TIER_QUADS", "1")
+    s = rtx.HostScene("cornell_box", 1)
+    cam = s.camera(width=64, spp=1)
+    assert rtx.walk_near_region(s.desc, cam)[1]
+    d = s.desc.contents
+    floor = next(i for i in range(d.n_quads) if list(d.quads[i].normal) == [0.0, -1.0, 0.0] and d.quads[i].q[1] == 0.0
+                 and d.quads[i].u[0] == 555.0)
+    old = d.quads[floor].material
+    d.quads[floor].material = next(m for m in range(d.n_materials) if m != old)  # another material: no tiers
+    try:
+        assert not rtx.walk_near_region(s.desc, cam)[1]
+    finally:
+        d.quads[floor].material = old
