@@ -69,6 +69,12 @@ namespace rtxd {
 #ifndef RTX_NEAR_AND  // 1: the near region's test reads its bounds at once (0: short-circuit form, A/B)
 #define RTX_NEAR_AND 1
 #endif
+#ifndef RTX_PRIO_WALK  // >= 0: the wave's issue priority (s_setprio) in the walk / the shading phase (A/B; -1: unset)
+#define RTX_PRIO_WALK 1
+#endif
+#ifndef RTX_PRIO_SHADE
+#define RTX_PRIO_SHADE 0
+#endif
 #ifndef RTX_CAM_DEFER  // 1: the near pass also tests each new camera ray against the near region (the host's gate,
 #define RTX_CAM_DEFER 0  // camera_in_near, already admits only cameras whose defocus disk lies inside it)
 #endif
@@ -469,6 +475,7 @@ __device__ __forceinline__ void render_body(const Params& p, const uint64_t t0 =
             }
         }
         if (TIME) clk = __builtin_amdgcn_s_memtime();
+        if (RTX_PRIO_WALK >= 0) __builtin_amdgcn_s_setprio(RTX_PRIO_WALK);
         // primitive batching only for a scene in LDS: a lane that waits re-reads its entry, which
         // from HBM cost config 4 +34 %
         traverse_phase<COUNT, STEPS, QUADS, USE_LDS, HYB, USE_LDS || (RTX_HYB_BATCH && HYB), TIER == 1 && RTX_NEAR_FMA && !QUADS>(
@@ -481,6 +488,7 @@ __device__ __forceinline__ void render_body(const Params& p, const uint64_t t0 =
             clk = now;
         }
         if (ballot(mode != M_DONE) == 0) break;
+        if (RTX_PRIO_SHADE >= 0) __builtin_amdgcn_s_setprio(RTX_PRIO_SHADE);
 
         // ---- shading phase ----------------------------------------------------------
         // POOL: a MISS PHASE instead when fewer than p.refill_hits of the waiting lanes hit something: only
