@@ -510,13 +510,17 @@ constexpr uint32_t DRAIN_WORDS = 16384;  // Params::drain_count's words: near gr
 // The camera-ray pool of render_items<POOL>: after the fixed layout's scene copy (16-B aligned), 64 rays
 // of 2 float4 per wave (2 KB).
 constexpr uint32_t POOL_BYTES_PER_WAVE = 64 * 32;
+#ifndef RTX_POOL_WAVES  // waves per workgroup of the pooled kernels (two workgroups per CU) and their waves per SIMD
+#define RTX_POOL_WAVES 12
+#define RTX_POOL_MINW 6
+#endif
 __host__ __device__ __forceinline__ uint32_t pool_f4_offset(const Params& p) {
     return (lds_fixed_bytes(p.n_entries, p.n_quads, p.n_materials, p.n_textures) + 15u) / 16u;
 }
 // Whether a render of a scene in the LDS copy takes the camera-ray pool: wanted (Params::cam_pool) and two
 // 12-wave workgroups' scene copies and pools fit a CU's 160 KB.
 __host__ __device__ __forceinline__ bool pool_fits(const Params& p) {
-    return p.cam_pool && (size_t)pool_f4_offset(p) * 16 + 12 * POOL_BYTES_PER_WAVE <= 80u * 1024u;
+    return p.cam_pool && (size_t)pool_f4_offset(p) * 16 + RTX_POOL_WAVES * POOL_BYTES_PER_WAVE <= 80u * 1024u;
 }
 
 // The words of Params::error_flag, the device's sticky error word (rtx_capi.hip KernErr): counters

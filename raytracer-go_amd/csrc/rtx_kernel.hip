@@ -60,6 +60,12 @@ namespace rtxd {
 #ifndef RTX_KARG_RELOAD  // 1: uniform values of the shading phase re-read from the kernel arguments at their use (0: A/B)
 #define RTX_KARG_RELOAD 1
 #endif
+#ifndef RTX_KARG_CAM  // the pool's camera / the near region's bounds re-read from the kernel arguments (A/B)
+#define RTX_KARG_CAM RTX_KARG_RELOAD
+#endif
+#ifndef RTX_KARG_NEAR
+#define RTX_KARG_NEAR RTX_KARG_RELOAD
+#endif
 #ifndef RTX_HYB_DRAIN  // 1: the drain also for scenes in HBM with an LDS cache (A/B; round 5: +2.3 % at config 4)
 #define RTX_HYB_DRAIN 0
 #endif
@@ -443,7 +449,7 @@ __device__ __forceinline__ void render_body(const Params& p, const uint64_t t0 =
         }
     };
     auto defer_far = [&](bool& ready) {  // segments that would start outside the near region
-        const Params& q = RTX_KARG_RELOAD && !HYB ? karg_params() : p;  // (the cache kernels: kept live)
+        const Params& q = RTX_KARG_NEAR && !HYB ? karg_params() : p;  // (the cache kernels: kept live)
         // all six bounds read unconditionally and combined with `&`: through the opaque kernel-argument pointer the
         // compiler cannot speculate a load, so `&&` became six scalar loads, each behind its own wait and branch
         // (C2 +2.6 % with two such tests per phase)
@@ -592,7 +598,7 @@ __device__ __forceinline__ void render_body(const Params& p, const uint64_t t0 =
                 const uint32_t blk = cursor >> 6;
                 if (blk != pool_blk) {  // the block's 64 camera rays, one per lane (sample u_k0 + blk, pixel lane)
                     pool_blk = blk;
-                    const rtx_camera& c = RTX_KARG_RELOAD ? karg_params().cam : p.cam;
+                    const rtx_camera& c = RTX_KARG_CAM ? karg_params().cam : p.cam;
                     const uint32_t lx = u_x + (lane & tw_mask), lr = u_r + (lane >> twl);
                     if (lx < p.width && lr < p.rows) {
                         const uint32_t x = p.x0 + lx, y = ST ? u_y + (lane >> twl) : p.y0 + p.rank + lr * p.world;
@@ -941,9 +947,10 @@ inline size_t items_shmem(const Params& p, bool use_lds, bool hyb) {
 // workgroups of WN waves (12: two per CU, each with its scene copy and 12 pools); the far and redo
 // passes keep WAVES.
 template <bool COUNT, int WAVES, int MINW, bool CLK = false, bool USE_LDS = true, bool HYB = false, bool POOL = false,
-          bool ST = false, bool QUADS = false, int WN = POOL ? 12 : WAVES>
+          bool ST = false, bool QUADS = false, int WN = POOL ? RTX_POOL_WAVES : WAVES>
 hipError_t launch_tiered(Params pn, Params pf, hipStream_t stream) {
-    const auto kn = render_items<COUNT, USE_LDS, QUADS, false, WN, MINW, HYB, CLK, 1, POOL, ST>;
+    constexpr int MN = POOL && MINW ? RTX_POOL_MINW : MINW;  // the near (and drain) kernel's waves per SIMD
+    const auto kn = render_items<COUNT, USE_LDS, QUADS, false, WN, MN, HYB, CLK, 1, POOL, ST>;
     const auto kf = render_items<COUNT, USE_LDS, QUADS, false, WAVES, MINW, HYB, CLK, 2>;  // (rows from the records)
     const auto kr = render_items<COUNT, USE_LDS, QUADS, false, WAVES, MINW, HYB, false, 3, false, ST>;
     const size_t sn = POOL ? (size_t)pool_f4_offset(pn) * 16 + WN * POOL_BYTES_PER_WAVE : items_shmem(pn, USE_LDS, HYB),
@@ -959,7 +966,7 @@ hipError_t launch_tiered(Params pn, Params pf, hipStream_t stream) {
     // (Not for a scene in HBM with LDS caches: the combined kernel spilled 24 VGPRs there, and config 4 took +2.3 %.)
     constexpr bool CAN_DRAIN = !COUNT && !CLK && (!HYB || RTX_HYB_DRAIN);
     const void* kd = nullptr;
-    if constexpr (CAN_DRAIN) kd = (const void*)render_drain<USE_LDS, WN, MINW, HYB, POOL, ST, QUADS>;
+    if constexpr (CAN_DRAIN) kd = (const void*)render_drain<USE_LDS, WN, MN, HYB, POOL, ST, QUADS>;
     const size_t sd = sn > sf ? sn : sf;
     int per_d = 0;
     bool drain = CAN_DRAIN && pn.drain && pn.drain_count;
@@ -995,7 +1002,7 @@ hipError_t launch_tiered(Params pn, Params pf, hipStream_t stream) {
         if (drain_now) {
             pn.drain_region = pf.drain_region = pn.defer_cap / (uint32_t)bn;
             if constexpr (CAN_DRAIN)
-                hipLaunchKernelGGL((render_drain<USE_LDS, WN, MINW, HYB, POOL, ST, QUADS>), dim3((uint32_t)bn), dim3(block_n), sd,
+                hipLaunchKernelGGL((render_drain<USE_LDS, WN, MN, HYB, POOL, ST, QUADS>), dim3((uint32_t)bn), dim3(block_n), sd,
                                    stream, DrainArgs{pn, far_layout(pf)});
         } else {
             hipLaunchKernelGGL(kn, dim3((uint32_t)bn), dim3(block_n), sn, stream, pn);
@@ -1027,13 +1034,13 @@ hipError_t launch_items_for(const Params& p, bool use_lds, hipStream_t stream) {
         return p.n_quads ? launch_items<COUNT, true, false, 4, 0, false, false, ST>(p, use_lds, stream)
                          : launch_items<COUNT, false, false, 4, 0, false, false, ST>(p, use_lds, stream);
     // 6 waves per SIMD: at most 80 VGPRs (the allocation granule is 8)
-    constexpr int MV = COUNT ? 0 : RTX_V3_MINW, MH = COUNT ? 0 : RTX_HYB_MINW;
+    constexpr int MV = COUNT ? 0 : RTX_V3_MINW, MH = COUNT ? 0 : RTX_HYB_MINW, MP = COUNT ? 0 : RTX_POOL_MINW;
     if (!use_lds && p.n_hot > HOT_ENTRIES_8W)  // an LDS cache past a third of the CU: 12-wave workgroups, two per CU
         return p.n_quads ? launch_items<COUNT, true, false, RTX_HYB_WAVES, MH, false, false, ST>(p, use_lds, stream)
                          : launch_items<COUNT, false, false, RTX_HYB_WAVES, MH, false, false, ST>(p, use_lds, stream);
     if (use_lds && pool_fits(p))  // the camera-ray pool (12-wave workgroups, two per CU) when the scene copy leaves room
-        return p.n_quads ? launch_items<COUNT, true, false, 12, MV, false, true, ST>(p, use_lds, stream)
-                         : launch_items<COUNT, false, false, 12, MV, false, true, ST>(p, use_lds, stream);
+        return p.n_quads ? launch_items<COUNT, true, false, RTX_POOL_WAVES, MP, false, true, ST>(p, use_lds, stream)
+                         : launch_items<COUNT, false, false, RTX_POOL_WAVES, MP, false, true, ST>(p, use_lds, stream);
     return p.n_quads ? launch_items<COUNT, true, false, RTX_V3_WAVES, MV, false, false, ST>(p, use_lds, stream)
                      : launch_items<COUNT, false, false, RTX_V3_WAVES, MV, false, false, ST>(p, use_lds, stream);
 }
