@@ -500,6 +500,10 @@ struct Params {
     // early walks its far records while the others still render, and the long paths of the far tree start then.
     uint32_t* drain_count;   // 2 x the near grid, zeroed per chunk
     uint32_t drain_region;   // records per workgroup (the queue's capacity over the near grid)
+    // render_drain (RTX_DRAIN_LDS): the workgroup's record count and far unit cursor are two LDS words at this float4
+    // index of the dynamic LDS, past both phases' layouts, instead of drain_count's (a global atomic with return,
+    // which the wave waits on, in every phase that defers)
+    uint32_t drain_lds;
     uint32_t drain;          // 1: the timed tiered render drains (RTX_DRAIN=0: the far pass's own launch, A/B)
     // The layout is the paired walk's records (rtx_capi.hip build_w2): a layout in HBM with an LDS
     // cache, walked by trav_step_w2 (only the cache kernels, HYB, ever get one; never a drain launch).

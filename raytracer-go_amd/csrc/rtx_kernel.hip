@@ -81,6 +81,9 @@ namespace rtxd {
 #ifndef RTX_PRIO_SHADE
 #define RTX_PRIO_SHADE 0
 #endif
+#ifndef RTX_DRAIN_LDS  // 1: the drain's per-workgroup record count and far unit cursor in LDS (0: in HBM, A/B)
+#define RTX_DRAIN_LDS 1
+#endif
 #ifndef RTX_CAM_DEFER  // 1: the near pass also tests each new camera ray against the near region (the host's gate,
 #define RTX_CAM_DEFER 0  // camera_in_near, already admits only cameras whose defocus disk lies inside it)
 #endif
@@ -339,9 +342,16 @@ __device__ __forceinline__ void render_body(const Params& p, const uint64_t t0 =
     const uint32_t nsub = (p.kn + p.sub - 1u) / p.sub;
     // far pass: units of 64 queue records
     // (DRAIN: this workgroup's records, written by its own waves before the barrier that ended its near phase)
+    // DRAIN: the workgroup's record count and far unit cursor (in LDS past both layouts when p.drain_lds, else HBM)
+    // (a compile-time choice: a pointer that may be either would make every claim a flat atomic)
+    uint32_t* const rec_count = !DRAIN           ? p.defer_count
+                                : RTX_DRAIN_LDS ? reinterpret_cast<uint32_t*>(lds_entries + p.drain_lds)
+                                                : p.drain_count + blockIdx.x;
+    uint32_t* const far_cursor = !DRAIN           ? p.tile_counter
+                                 : RTX_DRAIN_LDS ? reinterpret_cast<uint32_t*>(lds_entries + p.drain_lds) + 1
+                                                 : p.drain_count + gridDim.x + blockIdx.x;
     const uint32_t n_rec =
-        TIER == 2 ? (DRAIN ? min(__builtin_amdgcn_readfirstlane(*(volatile uint32_t*)(p.drain_count + blockIdx.x)),
-                                 p.drain_region)
+        TIER == 2 ? (DRAIN ? min(__builtin_amdgcn_readfirstlane(*(volatile uint32_t*)rec_count), p.drain_region)
                            : min(__builtin_amdgcn_readfirstlane(*(volatile uint32_t*)p.defer_count), p.defer_cap))
                   : 0u;
     // redo pass: the compacted list of flagged samples when it held them all (else the bits, unit by unit)
@@ -411,7 +421,7 @@ __device__ __forceinline__ void render_body(const Params& p, const uint64_t t0 =
             return;
         }
         uint32_t b = 0;
-        if (lane == 0) b = atomicAdd(DRAIN ? p.drain_count + blockIdx.x : p.defer_count, (uint32_t)__popcll(fm));
+        if (lane == 0) b = atomicAdd(rec_count, (uint32_t)__popcll(fm));
         b = __builtin_amdgcn_readfirstlane(b);
         bool full = false;
         if (far) {
@@ -562,7 +572,7 @@ __device__ __forceinline__ void render_body(const Params& p, const uint64_t t0 =
                 exhausted = true;  // (debug library: the even lanes reach the claim alone)
             } else if (cursor >= u_items && !exhausted) {  // claim the next unit (wave-uniform)
                 uint32_t un = 0;
-                if (lane == 0) un = atomicAdd(DRAIN && TIER == 2 ? p.drain_count + gridDim.x + blockIdx.x : p.tile_counter, 1u);
+                if (lane == 0) un = atomicAdd(DRAIN && TIER == 2 ? far_cursor : p.tile_counter, 1u);
                 uint32_t uu = __builtin_amdgcn_readfirstlane(un);  // the whole wave is here: lane 0's
                 if (partial_wave()) {  // else: the wave stops (exhausted) and the render fails
                     RTX_SET_KERR();
@@ -741,6 +751,11 @@ struct DrainArgs {
 template <bool USE_LDS, int WAVES, int MINW, bool HYB, bool POOL, bool ST, bool QUADS = false>
 __global__ __launch_bounds__(64 * WAVES, MINW) void render_drain(DrainArgs a) {
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime() | 1ull;  // the watchdog's start for both phases (nonzero)
+    if constexpr (RTX_DRAIN_LDS) {  // the workgroup's two drain words in LDS (past both phases' layouts): zero first
+        extern __shared__ float4 lds_words[];
+        if (threadIdx.x < 2) reinterpret_cast<uint32_t*>(lds_words + a.pn.drain_lds)[threadIdx.x] = 0u;
+        __syncthreads();
+    }
     render_body<false, USE_LDS, QUADS, false, WAVES, HYB, false, 1, POOL, ST, true>(a.pn, t0);
     __syncthreads();  // every wave's near work and records done: the far phase overwrites the scene copy
     // The far phase reads its settings from the kernel arguments afresh, through an opaque copy of their address:
@@ -967,7 +982,9 @@ hipError_t launch_tiered(Params pn, Params pf, hipStream_t stream) {
     constexpr bool CAN_DRAIN = !COUNT && !CLK && (!HYB || RTX_HYB_DRAIN);
     const void* kd = nullptr;
     if constexpr (CAN_DRAIN) kd = (const void*)render_drain<USE_LDS, WN, MN, HYB, POOL, ST, QUADS>;
-    const size_t sd = sn > sf ? sn : sf;
+    // (RTX_DRAIN_LDS: the drain's two per-workgroup words in LDS after the larger layout)
+    const size_t sl = ((sn > sf ? sn : sf) + 15) / 16 * 16, sd = RTX_DRAIN_LDS ? sl + 16 : sl;
+    pn.drain_lds = RTX_DRAIN_LDS ? (uint32_t)(sl / 16) : 0u;
     int per_d = 0;
     bool drain = CAN_DRAIN && pn.drain && pn.drain_count;
     if (drain && (e = resident_grid(kd, block_n, sd, &per_d, &cus)) != hipSuccess) return e;
