@@ -673,15 +673,17 @@ __device__ __forceinline__ Scatter coop_scatter(const Params& p, const SceneRef 
     Scatter out{v3(0.0f, 0.0f, 0.0f), 0u, 0u};
     bool need = false;
     float x = 0.0f, y = 0.0f, z = 0.0f;
+    uint32_t ty = 0xFFFFFFFFu;  // (no hit: no material)
     if (hit >= 0) {
         const uint32_t mi = hit_material<QUADS>(E, (uint32_t)hit);
-        const uint32_t ty = E.m[mi].type;
-        need = ty == RTX_MAT_LAMBERTIAN || ty == RTX_MAT_METAL;
+        ty = E.m[mi].type;
         out.u0 = b0.x;
         x = signed_unit(b0.x);
         y = signed_unit(b0.y);
         z = signed_unit(b0.z);
     }
+    static_assert(RTX_MAT_LAMBERTIAN == 0 && RTX_MAT_METAL == 1, "need: one unsigned compare");
+    need = ty < 2u;  // Lambertian or Metal (a single compare: its ballot needs no lane-mask materialisation)
     uint32_t att = 0;
     uint64_t pend = ballot(need) & ~ballot(x * x + y * y + z * z < 1.0f);  // lensq(v) < 1
     const uint32_t lane = __lane_id();
@@ -719,7 +721,7 @@ __device__ __forceinline__ Scatter coop_scatter(const Params& p, const SceneRef 
             z = fz;
             att = base + kk;
         }
-        pend = ballot(mine) & ~ballot(mine_good != 0ull);
+        pend &= ~ballot(mine_good != 0ull);  // (ballot(mine) is pend)
         base += K;
     }
     if (need) {
@@ -921,7 +923,7 @@ __device__ __forceinline__ float med3(float a, float b, float c) {
 // NewAabb(c - r, c + r) as NewSphere makes it (hittables.go:85-94), passes Aabb.Hit (bvh.go:52-61,
 // 84-102) for the ray with interval [0.001, the float after t.closest] — the bound at which the
 // guarded walk's test of the sphere's leaf box (a superset) would still accept this hit.
-__device__ __forceinline__ bool own_box_pass(const Trav& t, const Ray& r, const float4 sa) {
+__device__ __forceinline__ void own_box_interval(const Trav& t, const Ray& r, const float4 sa, float& lo, float& hi) {
     const float rr = sa.w * -1.0f;
     const float ax = sa.x + rr, bx = sa.x + sa.w, ay = sa.y + rr, by = sa.y + sa.w, az = sa.z + rr, bz = sa.z + sa.w;
     const float mnx = __builtin_fminf(ax, bx), mxx = __builtin_fmaxf(ax, bx);
@@ -931,8 +933,12 @@ __device__ __forceinline__ bool own_box_pass(const Trav& t, const Ray& r, const 
     const float t0y = ((t.ny ? mxy : mny) - r.o.y) * t.iy, t1y = ((t.ny ? mny : mxy) - r.o.y) * t.iy;
     const float t0z = ((t.nz ? mxz : mnz) - r.o.z) * t.iz, t1z = ((t.nz ? mnz : mxz) - r.o.z) * t.iz;
     const float bound = __int_as_float(__float_as_int(t.closest) + 1);  // t.closest > 0, finite
-    const float lo = __builtin_fmaxf(__builtin_fmaxf(__builtin_fmaxf(0.001f, t0x), t0y), t0z);
-    const float hi = __builtin_fminf(__builtin_fminf(__builtin_fminf(bound, t1x), t1y), t1z);
+    lo = __builtin_fmaxf(__builtin_fmaxf(__builtin_fmaxf(0.001f, t0x), t0y), t0z);
+    hi = __builtin_fminf(__builtin_fminf(__builtin_fminf(bound, t1x), t1y), t1z);
+}
+__device__ __forceinline__ bool own_box_pass(const Trav& t, const Ray& r, const float4 sa) {
+    float lo, hi;
+    own_box_interval(t, r, sa, lo, hi);
     return lo < hi;
 }
 

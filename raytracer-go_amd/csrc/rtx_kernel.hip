@@ -517,7 +517,8 @@ __device__ __forceinline__ void render_body(const Params& p, const uint64_t t0 =
         bool mini = false;
         if constexpr (POOL) {
             if (mode == M_START) mode = M_SHADE;
-            const uint64_t wait = ballot(mode == M_SHADE), miss = ballot(mode == M_SHADE && t.hit < 0);
+            // (ballots of single compares, combined on SALU: a ballot of `a && b` costs a lane-mask materialisation)
+            const uint64_t wait = ballot(mode == M_SHADE), miss = wait & ballot(t.hit < 0);
             mini = miss != 0 && (uint32_t)__popcll(wait & ~miss) < p.refill_hits;
             if (mini && mode == M_SHADE && t.hit >= 0) mode = M_START;
         }
@@ -527,15 +528,16 @@ __device__ __forceinline__ void render_body(const Params& p, const uint64_t t0 =
             // its reference leaf's) passes with the bound just past the hit; else the
             // segment is walked again on the guarded tree by the far pass.
             const bool check = mode == M_SHADE && t.hit >= 0;
-            bool bad = false;
+            float lo = 0.0f, hi = 1.0f;  // the test's interval (a lane without a hit passes); bad = !(lo < hi), one compare
             if (check) {
                 if (QUADS && __float_as_int(E.b[t.hit].w) == RTX_E_QUAD) {  // a quad's own box
                     const uint32_t qi = 4u * (uint32_t)__float_as_int(E.b[t.hit].x);
-                    bad = !quad_own_box_pass(t, r, E.q[qi], E.q[qi + 1], E.q[qi + 2]);
+                    if (!quad_own_box_pass(t, r, E.q[qi], E.q[qi + 1], E.q[qi + 2])) lo = 1.0f;
                 } else {
-                    bad = !own_box_pass(t, r, E.a[t.hit]);
+                    own_box_interval(t, r, E.a[t.hit], lo, hi);
                 }
             }
+            const bool bad = !(lo < hi);
             if (COUNT && bad) --cnt.segments;  // the far pass walks the segment again and counts it
             defer(bad);
         }
