@@ -81,6 +81,9 @@ namespace rtxd {
 #ifndef RTX_PRIO_SHADE
 #define RTX_PRIO_SHADE 0
 #endif
+#ifndef RTX_PRIO_CLAIM  // >= 0: the priority from the claims on (new items, camera rays, the segment's begin; A/B)
+#define RTX_PRIO_CLAIM -1
+#endif
 #ifndef RTX_DRAIN_LDS  // 1: the drain's per-workgroup record count and far unit cursor in LDS (0: in HBM, A/B)
 #define RTX_DRAIN_LDS 1
 #endif
@@ -565,6 +568,7 @@ __device__ __forceinline__ void render_body(const Params& p, const uint64_t t0 =
         }
         if constexpr (TIER == 1) defer_far(ready);  // before the claims: the lane takes a new item now
         if (TIME) split_clk(split[1], clk);
+        if (RTX_PRIO_CLAIM >= 0) __builtin_amdgcn_s_setprio(RTX_PRIO_CLAIM);
         // Lanes without an item take the next ones of the wave's unit; new camera rays
         // at one program point.  Loops only for max depth 0 and ragged tiles.
         for (;;) {
