@@ -345,8 +345,9 @@ __device__ __forceinline__ void render_body(const Params& p, const uint64_t t0 =
     const uint32_t nsub = (p.kn + p.sub - 1u) / p.sub;
     // far pass: units of 64 queue records
     // (DRAIN: this workgroup's records, written by its own waves before the barrier that ended its near phase)
-    // DRAIN: the workgroup's record count and far unit cursor (in LDS past both layouts when p.drain_lds, else HBM)
-    // (a compile-time choice: a pointer that may be either would make every claim a flat atomic)
+    // DRAIN: the workgroup's record count and far unit cursor: two LDS words at float4 index p.drain_lds, past both
+    // phases' layouts (RTX_DRAIN_LDS), else drain_count's HBM words (a compile-time choice: a pointer that may be
+    // either would make every claim a flat atomic)
     uint32_t* const rec_count = !DRAIN           ? p.defer_count
                                 : RTX_DRAIN_LDS ? reinterpret_cast<uint32_t*>(lds_entries + p.drain_lds)
                                                 : p.drain_count + blockIdx.x;
