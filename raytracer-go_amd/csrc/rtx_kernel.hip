@@ -87,6 +87,9 @@ namespace rtxd {
 #ifndef RTX_DRAIN_LDS  // 1: the drain's per-workgroup record count and far unit cursor in LDS (0: in HBM, A/B)
 #define RTX_DRAIN_LDS 1
 #endif
+#ifndef RTX_STATIC_FIRST  // 1: a wave's first unit from its grid index, no atomic (0: every unit claimed, A/B)
+#define RTX_STATIC_FIRST 1
+#endif
 #ifndef RTX_CAM_DEFER  // 1: the near pass also tests each new camera ray against the near region (the host's gate,
 #define RTX_CAM_DEFER 0  // camera_in_near, already admits only cameras whose defocus disk lies inside it)
 #endif
@@ -578,9 +581,19 @@ __device__ __forceinline__ void render_body(const Params& p, const uint64_t t0 =
             if (cursor >= u_items && !exhausted && dbg_skip(p, 3u, lane)) {
                 exhausted = true;  // (debug library: the even lanes reach the claim alone)
             } else if (cursor >= u_items && !exhausted) {  // claim the next unit (wave-uniform)
-                uint32_t un = 0;
-                if (lane == 0) un = atomicAdd(DRAIN && TIER == 2 ? far_cursor : p.tile_counter, 1u);
-                uint32_t uu = __builtin_amdgcn_readfirstlane(un);  // the whole wave is here: lane 0's
+                // RTX_STATIC_FIRST (a render's own units, TIER 0 / 1): a wave's first unit is its index in the grid, the
+                // counter hands out the rest from there, so the launch does not start with every wave's atomic queued
+                // on one address (u_items is 0 only before the first claim: a claimed unit holds >= 64 items)
+                constexpr bool STATIC_FIRST = RTX_STATIC_FIRST && TIER <= 1;
+                const uint32_t n_waves = gridDim.x * WAVES;
+                uint32_t uu;
+                if (STATIC_FIRST && u_items == 0u) {
+                    uu = __builtin_amdgcn_readfirstlane(blockIdx.x * WAVES + (threadIdx.x >> 6));
+                } else {
+                    uint32_t un = 0;
+                    if (lane == 0) un = atomicAdd(DRAIN && TIER == 2 ? far_cursor : p.tile_counter, 1u);
+                    uu = __builtin_amdgcn_readfirstlane(un) + (STATIC_FIRST ? n_waves : 0u);  // the whole wave is here: lane 0's
+                }
                 if (partial_wave()) {  // else: the wave stops (exhausted) and the render fails
                     RTX_SET_KERR();
                     uu = 0xFFFFFFFFu;
