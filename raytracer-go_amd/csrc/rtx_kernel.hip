@@ -581,10 +581,10 @@ __device__ __forceinline__ void render_body(const Params& p, const uint64_t t0 =
             if (cursor >= u_items && !exhausted && dbg_skip(p, 3u, lane)) {
                 exhausted = true;  // (debug library: the even lanes reach the claim alone)
             } else if (cursor >= u_items && !exhausted) {  // claim the next unit (wave-uniform)
-                // RTX_STATIC_FIRST (a render's own units, TIER 0 / 1): a wave's first unit is its index in the grid, the
+                // RTX_STATIC_FIRST (units on a global counter: TIER 0 / 1, a far launch): a wave's first unit is its grid index, the
                 // counter hands out the rest from there, so the launch does not start with every wave's atomic queued
                 // on one address (u_items is 0 only before the first claim: a claimed unit holds >= 64 items)
-                constexpr bool STATIC_FIRST = RTX_STATIC_FIRST && TIER <= 1;
+                constexpr bool STATIC_FIRST = RTX_STATIC_FIRST && (TIER <= 1 || (TIER == 2 && !DRAIN));
                 const uint32_t n_waves = gridDim.x * WAVES;
                 uint32_t uu;
                 if (STATIC_FIRST && u_items == 0u) {
