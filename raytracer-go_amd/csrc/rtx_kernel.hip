@@ -87,7 +87,7 @@ namespace rtxd {
 #ifndef RTX_DRAIN_LDS  // 1: the drain's per-workgroup record count and far unit cursor in LDS (0: in HBM, A/B)
 #define RTX_DRAIN_LDS 1
 #endif
-#ifndef RTX_STATIC_FIRST  // 1: a wave's first unit from its grid index, no atomic (0: every unit claimed, A/B)
+#ifndef RTX_STATIC_FIRST  // 1: a wave's first unit from its grid index, no atomic (0: every unit claimed; 2: wave-major, A/B)
 #define RTX_STATIC_FIRST 1
 #endif
 #ifndef RTX_CAM_DEFER  // 1: the near pass also tests each new camera ray against the near region (the host's gate,
@@ -588,7 +588,8 @@ __device__ __forceinline__ void render_body(const Params& p, const uint64_t t0 =
                 const uint32_t n_waves = gridDim.x * WAVES;
                 uint32_t uu;
                 if (STATIC_FIRST && u_items == 0u) {
-                    uu = __builtin_amdgcn_readfirstlane(blockIdx.x * WAVES + (threadIdx.x >> 6));
+                    uu = __builtin_amdgcn_readfirstlane(RTX_STATIC_FIRST == 2 ? (threadIdx.x >> 6) * gridDim.x + blockIdx.x
+                                                                              : blockIdx.x * WAVES + (threadIdx.x >> 6));
                 } else {
                     uint32_t un = 0;
                     if (lane == 0) un = atomicAdd(DRAIN && TIER == 2 ? far_cursor : p.tile_counter, 1u);
